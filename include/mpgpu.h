@@ -1,0 +1,238 @@
+/*
+ * mpgpu.h — C ABI of libmpgpu.so, the MI355X (gfx950) hot path of
+ * congkaishen/MotionPlanning.
+ *
+ * The reference is pure Julia; these entry points are what its planner calls
+ * through `ccall` (binding shown in INTEGRATION.md, wrapper in julia/MPGPU.jl).
+ * Every entry point cites the reference interface it replaces.
+ *
+ * Conventions
+ *  - All functions return an int status: MP_OK (0) or an MP_ERR_* code; the
+ *    message is available from mp_last_error(ctx).  This mirrors the
+ *    reference's `error(...)` validation (OptimalControl/MPPI/src/setup.jl:19-38).
+ *  - Arrays are dense, C row-major.  Shapes are written in C order; the
+ *    equivalent Julia column-major shape is the reverse, e.g. noise
+ *    [S][K][H][2] here == Array{Float64}(2, H, K, S) in Julia.
+ *  - Functions without the _dev suffix take HOST pointers, are synchronous,
+ *    and return after all results have been copied back (Julia arrays are
+ *    rooted for the duration of the ccall).  _dev variants take DEVICE
+ *    pointers, enqueue on the context's stream and do not synchronise.
+ *  - A context owns one HIP device, one stream and cached device workspaces.
+ *    It is not thread-safe; use one context per GPU / thread.
+ *  - Precision: Float64 throughout, like the reference.
+ */
+#ifndef MPGPU_H
+#define MPGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPGPU_VERSION "0.1.0"
+
+#define MP_OK 0
+#define MP_ERR_INVALID 1   /* bad argument (shape, NULL, range)            */
+#define MP_ERR_HIP 2       /* HIP runtime error                            */
+#define MP_ERR_NOMEM 3     /* device allocation failed                     */
+#define MP_ERR_NUMERIC 4   /* NaN / domain flag raised (outputs written)   */
+#define MP_ERR_UNSUPPORTED 5
+
+typedef struct mp_ctx mp_ctx;
+
+/* ------------------------------------------------------------- context */
+int mp_ctx_create(int device, mp_ctx** out);
+int mp_ctx_destroy(mp_ctx* ctx);
+const char* mp_last_error(mp_ctx* ctx);
+const char* mp_version(void);
+int mp_device_count(int* n);
+/* Synchronise the context stream (after _dev calls). */
+int mp_ctx_synchronize(mp_ctx* ctx);
+/* The hipStream_t the context launches on (for HIP-event timing). */
+void* mp_ctx_stream(mp_ctx* ctx);
+
+/* ---------------------------------------------------------------- MPPI */
+#define MP_NX 7 /* [x, y, v, r, psi, ux, sa]  vehicledynamics.jl:20-26 */
+#define MP_NU 2 /* [sr, ax]                    vehicledynamics.jl:27-28 */
+
+#define MP_NOISE_EXTERNAL 0 /* z ~ N(0,I) supplied by the caller (parity mode) */
+#define MP_NOISE_PHILOX 1   /* Philox4x32-10 + Box–Muller on device            */
+
+/* Planner settings; fields mirror MPPISetting (OptimalControl/MPPI/src/types.jl:10-31). */
+typedef struct mp_mppi_params {
+  int32_t K;                 /* SamplingNumber                                  */
+  int32_t H;                 /* N, horizon steps                                */
+  int32_t feasibility_count; /* FeasibilityCount (default 1300); >= K disables  */
+  int32_t n_obs;             /* circles per scene ([x, y, R] each)              */
+  double dt;                 /* T / N                                           */
+  double lambda;             /* λ                                               */
+  double sigma[4];           /* Σ, row-major 2x2                                */
+  double XL[MP_NX], XU[MP_NX];
+  double CL[MP_NU], CU[MP_NU];
+  double slack_penalty;      /* SlackPenalty (1e5)                              */
+  double obs_penalty;        /* 100*712.5 (MPPIUtils.jl:127); DWA: 10000*712.5  */
+  int32_t grid_nx, grid_ny;  /* occupancy grid (build extension), 0 = none      */
+  double grid_x0, grid_y0, grid_dx, grid_dy;
+  int32_t noise_mode;        /* MP_NOISE_*                                      */
+  int32_t ctrl_cost;         /* 1: λ·u_nomᵀΣ⁻¹(u−u_nom) term (MPPIUtils.jl:45)  */
+  uint64_t seed;             /* Philox key                                      */
+  uint64_t offset;           /* Philox counter word (advance per solve)         */
+} mp_mppi_params;
+
+/*
+ * mp_mppi_plan — one MPPIPlan(mppi) per scene (OptimalControl/MPPI/src/MPPIUtils.jl:169-203),
+ * S independent scenes per call.
+ *
+ * in : X0[S][7]       MPPI.s.X0 (ShiftInitialCondition, MPPIUtils.jl:24-27)
+ *      goal[S][2]     MPPI.s.goal
+ *      U_nom[S][H][2] MPPI.s.NominalControl (defineMPPINominalControl!, setup.jl:70-80)
+ *      obstacles[S][n_obs][3]  MPPI.s.obstacle_list (defineMPPIobs!, setup.jl:61-64), may be NULL if n_obs == 0
+ *      grid[S][ny][nx] uint8 occupancy (1 = occupied), NULL if grid_nx == 0
+ *      noise[S][K][H][2]  standard normals z (MP_NOISE_EXTERNAL), else NULL;
+ *                     control = clamp(U_nom + L z, CL, CU), L = chol(Σ).L (MPPIUtils.jl:5-20)
+ * out: U_out[S][H][2]       MPPI.r.Control (= MPPICtrl)
+ *      traj_out[S][H+1][7]  MPPI.r.Traj
+ *      cost_out[S]          MPPI.r.cost
+ *      feasible_out[S]      MPPI.r.Feasibility (1 = :Feasible)
+ *      rollout_count_out[S] MPPI.r.RolloutCount (= m + 1, reference off-by-one)
+ *      feasible_count_out[S] MPPI.r.FeasibleTrajCount
+ * optional (NULL to skip) — MPPI.p.TrajectoryCollection[1:K] (types.jl:3-8):
+ *      coll_traj[S][K][H+1][7], coll_ctrl[S][K][H][2], coll_cost[S][K], coll_feas[S][K]
+ *      (all K rollouts are written; the planner uses the first m = rollout_count-1).
+ * Returns MP_ERR_NUMERIC (after writing outputs) if any rollout cost was NaN.
+ */
+int mp_mppi_plan(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* X0,
+                 const double* goal, const double* U_nom, const double* obstacles,
+                 const uint8_t* grid, const double* noise, double* U_out, double* traj_out,
+                 double* cost_out, int32_t* feasible_out, int32_t* rollout_count_out,
+                 int32_t* feasible_count_out, double* coll_traj, double* coll_ctrl,
+                 double* coll_cost, uint8_t* coll_feas);
+
+/* Same contract, DEVICE pointers, asynchronous on the context stream. */
+int mp_mppi_plan_dev(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* X0,
+                     const double* goal, const double* U_nom, const double* obstacles,
+                     const uint8_t* grid, const double* noise, double* U_out, double* traj_out,
+                     double* cost_out, int32_t* feasible_out, int32_t* rollout_count_out,
+                     int32_t* feasible_count_out, double* coll_traj, double* coll_ctrl,
+                     double* coll_cost, uint8_t* coll_feas);
+
+/*
+ * mp_rollout — batched TrajectoryRollout with given controls
+ * (MPPIUtils.jl:31-57; DynamicWindow/src/DWAUtils.jl:16-42).
+ * ctrl[S][K][H][2] with the H stride given in elements (ctrl_stride_h = 2 for a
+ * full control list, 0 for DWA's constant controls [S][K][2]); no clamping.
+ * U_nom[S][H][2] is used only when p->ctrl_cost != 0.
+ * out: traj[S][K][H+1][7] (optional), cost[S][K], feas[S][K],
+ *      argmin[S] (optional; first minimum, Julia `minimum`/`argmin` on cost).
+ * p->K is ignored; K is the argument.
+ */
+int mp_rollout(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, int32_t K, const double* X0,
+               const double* goal, const double* ctrl, int64_t ctrl_stride_h,
+               const double* U_nom, const double* obstacles, const uint8_t* grid,
+               double* traj, double* cost, uint8_t* feas, int32_t* argmin);
+
+/*
+ * mp_vehicle_euler — the closed-loop plant of MPPI/main.jl:259-261 and
+ * DynamicWindow/main.jl:155-156: states .+= VehicleDynamics(states, u)*δt for
+ * nsteps steps with control ctrl[n][2] held constant (zero-order hold).
+ * states[n][7] updated in place; his[n][nsteps][7] (optional) gets every state.
+ */
+int mp_vehicle_euler(mp_ctx* ctx, int32_t n, double* states, const double* ctrl, double dt,
+                     int32_t nsteps, double* his);
+
+/* ---------------------------------------------------------------- iLQR */
+#define MP_ILQR_NX 4 /* [x, y, ux, ψ]  OptimalControl/ILQR/Dynamics.jl:4-7 */
+#define MP_ILQR_NU 2 /* [ax, δ]                                          */
+#define MP_ILQR_OPTIMALCONTROL 0 /* OptimalControl/ILQR/Cost.jl           */
+#define MP_ILQR_PARKING 1        /* PathPlanning/Parking_ILQR/Cost.jl     */
+
+typedef struct mp_ilqr_params {
+  int32_t N;           /* knots per trajectory (ILQR.jl:15: 20; Parking: 30) */
+  int32_t variant;     /* MP_ILQR_*: cost weights                            */
+  double dT;           /* δT = 0.05                                          */
+  double eps;          /* finite-difference step ϵ = 1e-3 (GetMatrix.jl:4)   */
+  double alpha_floor;  /* 0: none (ILQR.jl:71-82); 1e-3 Parking_ILQR.jl:83-85 */
+  double tol;          /* |ΔJ/J| stop (ILQR.jl:44): 1e-6                     */
+  int32_t max_iter;    /* safety cap on outer iterations (reference: none)   */
+  int32_t max_ls;      /* safety cap on line-search halvings (reference: none) */
+} mp_ilqr_params;
+
+/* Layouts (Julia column-major in parentheses):
+ *   X[B][N][4]  (StatesList 4×N per instance)   U[B][N][2]  (CtrlsList 2×N)
+ *   k[B][N-1][2]  (klist 2×1×(N-1))              Kg[B][N-1][4][2]  (Klist 2×4×(N-1))  */
+
+/* Initial-guess roll out (ILQR.jl:31-37) + TotalCost (Cost.jl:1-8). */
+int mp_ilqr_rollout(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* x0,
+                    const double* U, double* X, double* J);
+/* One backward Riccati sweep (ILQR.jl:46-67). */
+int mp_ilqr_backward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X,
+                     const double* U, double* k, double* Kg);
+/* One forward trial at step size alpha[B] (ILQR.jl:72-80): closed-loop RK4 roll out. */
+int mp_ilqr_forward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X,
+                    const double* U, const double* k, const double* Kg, const double* alpha,
+                    double* Xnew, double* Unew, double* Jnew);
+/* The whole script loop (ILQR.jl:39-88) per instance: backward + halving line
+ * search until |ΔJ/J| <= tol.  X/U in: initial guess; out: solution. */
+int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U,
+                  double* J, int32_t* iters);
+
+/* ---------------------------------------------------------- Hybrid A* */
+/* Settings mirror HybridAstarSettings (PathPlanning/HybridAstar/src/types.jl:20-43). */
+typedef struct mp_ha_params {
+  double vehicle_len, vehicle_wid; /* vehicle_size                               */
+  double minR;                     /* minimum turning radius                     */
+  double expand_time;              /* primitive length in time (2.5)             */
+  double res[3];                   /* resolutions [x, y, ψ]                      */
+  double stbound[6];               /* regulated [xmin, xmax, ymin, ymax, ψmin, ψmax] */
+  int32_t n_walls;                 /* obstacle blocks per scene, [x,y,ψ,l/2,w/2] */
+  int32_t n_prim;                  /* num_neighbors = num_gear*num_steer (62)    */
+  int32_t n_col;                   /* primitive path columns (250)               */
+  int32_t max_pops;                /* safety cap on search iterations            */
+} mp_ha_params;
+
+/* Primitive table of neighbor_origin (hybrid_astar_utils.jl:483-503):
+ * states_candi[n_prim][3], paths_candi[n_prim][n_col][3]  (Julia 3×n_prim, 3×n_col×n_prim). */
+int mp_ha_set_primitives(mp_ctx* ctx, const mp_ha_params* p, const double* states_candi,
+                         const double* paths_candi);
+
+/* Batched FindNewNode device part (hybrid_astar_utils.jl:391-421) for B popped nodes:
+ *   node[B][3], goal[B][3] (ending_states), walls[B][n_walls][5]
+ * out: nb_states[B][n_prim][3] regulated neighbor states,
+ *      idx[B][n_prim]  Encode (0 = out of bounds),
+ *      free_[B][n_prim] 1 if in bounds and dg_cost finite (collision free),
+ *      h[B][n_prim]     rs_heuristic (valid where free_ == 1). */
+int mp_ha_expand(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* node,
+                 const double* goal, const double* walls, double* nb_states, int64_t* idx,
+                 uint8_t* free_, double* h);
+
+/* Batched RS_connected (hybrid_astar_utils.jl:224-233): optimal Reeds–Shepp
+ * path from node to goal, its 100-steps-per-segment Euler path and the
+ * collision check.  path[B][501][3] (first path_len[B] columns valid). */
+int mp_ha_rs_connect(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* node,
+                     const double* goal, const double* walls, uint8_t* ok, double* path,
+                     int32_t* path_len);
+
+/* allpath (ReedsSheppsCurves/src/ReedsSheppsUtils.jl:468-511) for B normalised
+ * states; out: cost[B][48] (Inf where infeasible), cmds[B][48][5][3], best[B]. */
+int mp_ha_allpath(mp_ctx* ctx, int32_t B, const double* norm_states, double* cost,
+                  double* cmds, int32_t* best);
+
+/* Whole planHybridAstar! search loop (hybrid_astar_utils.jl:235-296) for B
+ * scenes in lockstep: the open-list / Dict bookkeeping runs on the host (C++),
+ * every expansion and RS-connect runs on the device, one fused launch per
+ * iteration.  start[B][3], goal[B][3] already regulated (setup.jl:110-112).
+ * out: found[B], pops[B] (loop_count), n_nodes[B] (length(nodes_collection)),
+ *      pop_seq[B][max_pops] (Encode index of each popped node, -1 padded),
+ *      n_states[B] and states_out[B][max_pops][3] (hybrid_astar_states, goal→start order),
+ *      rs_len[B] and rs_path[B][501][3] (RSpath_final). */
+int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* start,
+               const double* goal, const double* walls, int32_t* found, int32_t* pops,
+               int32_t* n_nodes, int64_t* pop_seq, int32_t* n_states, double* states_out,
+               int32_t* rs_len, double* rs_path);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPGPU_H */
