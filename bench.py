@@ -1,0 +1,196 @@
+"""MPPI rollout-step throughput on MI355X (BASELINE.json metric, configs[1]).
+
+One step = one MPPIPlan (OptimalControl/MPPI/src/MPPIUtils.jl:169-203) per scene at
+K=8192 rollouts, H=50 horizon steps, 7-state dynamic bicycle, 100x100 occupancy
+grid, device Philox noise, the full TrajectoryCollection (every rollout's
+trajectory and control list) written to HBM, weights + MPPICtrl + final rollout:
+ONE kernel launch (mp_mppi_plan_dev).  Inputs are resident in HBM before the timed
+region.  N>1: one process per GPU, each solves its own scene(s) (weak scaling) and
+the ranks all-gather the optimal controls over RCCL (the north star's exchange step).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scenes S] [--cpu-seconds T]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch  # import before libmpgpu so both share torch's HIP runtime
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (AMD spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scenes", type=int, default=1, help="scenes per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--rotate", type=int, default=12, help="output buffer sets rotated to defeat the 256 MB MALL")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(S, K, H):
+    """HBM bytes one launch must move (full TrajectoryCollection contract), see DESIGN.md §4."""
+    per_rollout = (H * 16  # control list written (types.jl:5)
+                   + (H + 1) * 56  # trajectory written (types.jl:4)
+                   + 8 + 1  # cost + feasibility
+                   + H * 16)  # control list read back for Σ w·u
+    return S * K * per_rollout
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from motionplanning_amd import configs
+    from motionplanning_amd.abi import MP_NOISE_PHILOX, ptr
+    from motionplanning_amd.context import Context
+
+    ctx = Context(local)
+    c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415 + rank)
+    p = c["params"]
+    K, H, S = p.K, p.H, a.scenes
+
+    def t(x, dt=torch.float64):
+        return torch.as_tensor(np.ascontiguousarray(x), dtype=dt, device=dev).contiguous()
+
+    X0 = np.tile(c["X0"], (S, 1))
+    X0[:, 1] = np.linspace(-0.5, 0.5, S) if S > 1 else 0.0
+    dX0, dgoal = t(X0), t(np.tile(c["goal"], (S, 1)))
+    dun = t(np.zeros((S, H, 2)))
+    dgrid = t(np.tile(c["grid"], (S, 1, 1)), torch.uint8)
+    sets = []
+    for _ in range(max(1, a.rotate)):
+        sets.append(dict(
+            U=torch.empty((S, H, 2), dtype=torch.float64, device=dev),
+            traj=torch.empty((S, H + 1, 7), dtype=torch.float64, device=dev),
+            cost=torch.empty(S, dtype=torch.float64, device=dev),
+            feas=torch.empty(S, dtype=torch.int32, device=dev),
+            rc=torch.empty(S, dtype=torch.int32, device=dev),
+            fc=torch.empty(S, dtype=torch.int32, device=dev),
+            ctraj=torch.empty((S, K, H + 1, 7), dtype=torch.float64, device=dev),
+            cctrl=torch.empty((S, K, H, 2), dtype=torch.float64, device=dev),
+            ccost=torch.empty((S, K), dtype=torch.float64, device=dev),
+            cfeas=torch.empty((S, K), dtype=torch.uint8, device=dev),
+        ))
+    gathered = torch.empty((world * S, H, 2), dtype=torch.float64, device=dev)
+    stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
+    torch.cuda.set_stream(stream)  # RCCL all_gather is ordered after the plan kernel
+
+    ev = []
+
+    def step(i, timed):
+        b = sets[i % len(sets)]
+        p.offset = i
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+        ctx.check(ctx.lib.mp_mppi_plan_dev(
+            ctx.handle, ctypes.byref(p), S, ptr(dX0), ptr(dgoal), ptr(dun), None, ptr(dgrid), None, ptr(b["U"]),
+            ptr(b["traj"]), ptr(b["cost"]), ptr(b["feas"]), ptr(b["rc"]), ptr(b["fc"]), ptr(b["ctraj"]),
+            ptr(b["cctrl"]), ptr(b["ccost"]), ptr(b["cfeas"])))
+        if timed:
+            e1.record(stream)
+            ev.append((e0, e1))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, b["U"])
+
+    for i in range(a.warmup):
+        step(i, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(a.warmup + i, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    if world > 1:
+        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(tt[0]), float(tt[1])
+    ok = bool((sets[0]["rc"] == K + 1).all().item()) and bool(torch.isfinite(sets[0]["cost"]).all().item())
+
+    units = world * S * K * H * a.steps
+    value = units / elapsed
+    nbytes = algorithmic_bytes(S, K, H)
+    achieved = nbytes / (kern_ms * 1e-3) / 1e9
+    out = {
+        "metric": BASE["metric"],
+        "value": value,
+        "unit": "rollout-steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded Philox noise; cfg1 circles rasterised into a 100x100 grid)",
+        "config": {
+            "workload": "configs[1]: MPPI K=8192 H=50 dynamic bicycle, 2-D occupancy-grid cost, full "
+                        "TrajectoryCollection, weights + MPPICtrl + final rollout",
+            "K": K, "H": H, "scenes_per_gpu": S, "feasibility_count": p.feasibility_count,
+            "parallelism": f"scene-sharded x{world}" + (" + RCCL all_gather(MPPICtrl)" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "kernel": "mppi_plan_kernel", "kernel_ms": kern_ms, "algorithmic_bytes": nbytes,
+        },
+        "valid": ok,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu and a.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(budget_s):
+    """The oracle (scalar C port, 1 thread) on the same cfg2 workload, bounded to ~budget_s."""
+    import oracle
+    from motionplanning_amd import configs
+    from motionplanning_amd.abi import MP_NOISE_PHILOX
+
+    c = configs.cfg2(noise_mode=MP_NOISE_PHILOX)
+    p = c["params"]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        p.offset = n
+        oracle.mppi_plan(p, c["X0"], c["goal"], c["unom"], None, c["grid"], None)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": p.K * p.H * n / dt, "unit": "rollout-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} full cfg2 MPPIPlan solves (K=8192, H=50, grid, Philox noise) in {dt:.1f} s, "
+                      f"scalar C oracle, 1 thread on {os.cpu_count()}-CPU host"}
+
+
+if __name__ == "__main__":
+    main()

@@ -232,6 +232,12 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                int32_t* n_nodes, int64_t* pop_seq, int32_t* n_states, double* states_out,
                int32_t* rs_len, double* rs_path);
 
+/* ---------------------------------------------------------- diagnostics */
+/* Evaluate one include/mp_jlmath.h function on the device for n inputs
+ * (bit-exactness check against the CPU build).  fn: 0 sin, 1 cos, 2 tan, 3 atan,
+ * 4 atan2(x, y), 5 asin, 6 acos, 7 exp, 8 log, 9 modpi, 10 sqrt. */
+int mp_math_eval(mp_ctx* ctx, int32_t fn, int64_t n, const double* x, const double* y, double* out);
+
 #ifdef __cplusplus
 }
 #endif

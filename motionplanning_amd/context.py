@@ -1,0 +1,57 @@
+"""Device context: one libmpgpu mp_ctx per (process, GPU)."""
+import ctypes
+import threading
+
+from .abi import MP_OK, MPGPUError, load_library
+
+_local = threading.local()
+
+
+class Context:
+    """Owns an mp_ctx (device, HIP stream, cached workspaces).  Not thread-safe."""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        st = self.lib.mp_ctx_create(int(device), ctypes.byref(h))
+        if st != MP_OK:
+            raise MPGPUError(st, self.lib.mp_last_error(None).decode())
+        self.handle = h
+        self.device = device
+
+    def check(self, st):
+        if st != MP_OK:
+            raise MPGPUError(st, self.lib.mp_last_error(self.handle).decode())
+        return st
+
+    def synchronize(self):
+        self.check(self.lib.mp_ctx_synchronize(self.handle))
+
+    @property
+    def stream(self):
+        return self.lib.mp_ctx_stream(self.handle)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.mp_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def default_context(device=None):
+    """Per-thread default context on `device` (default: LOCAL_RANK or 0)."""
+    import os
+
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", "0"))
+    ctxs = getattr(_local, "ctxs", None)
+    if ctxs is None:
+        ctxs = _local.ctxs = {}
+    if device not in ctxs:
+        ctxs[device] = Context(device)
+    return ctxs[device]

@@ -1,0 +1,551 @@
+// mppi.hip — MPPIPlan / TrajectoryRollout / plant kernels for gfx950 and their C-ABI
+// entry points (include/mpgpu.h).
+//
+// mp_mppi_plan is ONE kernel launch per call (no memset, no host round trip):
+//   phase 1  every block: NT/2 rollouts (lane pairs) — noise draw, clamp, RK2
+//            dynamics and all step costs fused; per-rollout cost/flag and the
+//            control list go to HBM (the TrajectoryCollection contract);
+//            then the block's online-softmax partial (ρ_b, η_b, Σ e·u) is
+//            published with an agent-scope release and an arrival ticket.
+//   phase 2  the last block to arrive for a scene (acquire) applies the
+//            FeasibilityCount prefix (MPPIUtils.jl:175), combines the partials
+//            with a log-sum-exp rescale into MPPICtrl (:186-190) and runs the
+//            final TrajectoryRollout (:192-198).  It resets the ticket.
+#include "mppi_device.hpp"
+#include "runtime.hpp"
+
+using namespace mpk;
+
+namespace {
+
+constexpr int NT = 256;     // threads per block (4 waves)
+constexpr int RPB = NT / 2; // rollouts per block
+
+__device__ __forceinline__ double block_reduce_min(double v, double* sh) {
+  for (int o = 32; o >= 1; o >>= 1) v = nanmin(v, __shfl_xor(v, o));
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double r = sh[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); i++) r = nanmin(r, sh[i]);
+  __syncthreads();
+  return r;
+}
+
+// deterministic block sum: fixed shuffle tree per wave, then waves in order
+__device__ __forceinline__ double block_reduce_sum(double v, double* sh) {
+  for (int o = 32; o >= 1; o >>= 1) v = v + __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double r = sh[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); i++) r = r + sh[i];
+  __syncthreads();
+  return r;
+}
+
+struct PlanArgs {
+  const double* X0;
+  const double* goal;
+  const double* unom;
+  const double* obs;
+  const unsigned char* grid;
+  const double* noise;
+  double* ctrl_all;    // [S][K][H][2]
+  double* cost_all;    // [S][K]
+  unsigned char* feas_all;  // [S][K]
+  double* part;        // [S][nb][pstride]
+  double* coll_traj;   // [S][K][H+1][7] or null
+  unsigned* tickets;
+  int* flags;
+  double* U_out;
+  double* traj_out;
+  double* cost_out;
+  int* feas_out;
+  int* rc_out;
+  int* fc_out;
+  int nb;
+  int pstride;
+};
+
+__global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
+  __shared__ double sh_red[NT / 64];
+  __shared__ double sh_e[RPB];
+  __shared__ double sh_q[2][128];
+  __shared__ int sh_last;
+  extern __shared__ double dyn[];  // H*2 (final MPPICtrl) + nb scales
+  const int H = P.H, H2 = 2 * H, K = P.K;
+  const int s = blockIdx.x / A.nb, b = blockIdx.x % A.nb;
+  const int tid = threadIdx.x, pair = tid >> 1, side = tid & 1;
+  const int k = b * RPB + pair;
+  const bool active = k < K;
+  const int kk = active ? k : K - 1;
+
+  const double* X0 = A.X0 + 7 * s;
+  const double* goal = A.goal + 2 * s;
+  const double* unom = A.unom + (size_t)H2 * s;
+  const double* obs = A.obs ? A.obs + (size_t)3 * P.n_obs * s : nullptr;
+  const unsigned char* grid = A.grid ? A.grid + (size_t)P.gnx * P.gny * s : nullptr;
+  const double* noise = A.noise ? A.noise + (size_t)K * H2 * s : nullptr;
+  double* ctrl_k = A.ctrl_all + ((size_t)s * K + kk) * H2;
+
+  // ---------------- phase 1: the rollout of this lane pair
+  int feas;
+  double c;
+  {
+    auto ctrl = [&](int j, double* u) { draw_ctrl(P, noise, unom, (unsigned)s, kk, j, u); };
+    auto store = [&](int j, const double* u) {
+      if (active) ctrl_k[2 * j + side] = u[side];
+    };
+    double* traj = (A.coll_traj && active) ? A.coll_traj + ((size_t)s * K + k) * (H + 1) * 7 : nullptr;
+    c = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas);
+  }
+  if (active && side == 0) {
+    A.cost_all[(size_t)s * K + k] = c;
+    A.feas_all[(size_t)s * K + k] = (unsigned char)feas;
+    if (c != c) atomicOr(A.flags, 1);
+  }
+  // ---------------- block partial (online softmax), MPPIUtils.jl:154-167
+  const double cm = active ? c : __builtin_inf();
+  const double rho_b = block_reduce_min(cm, sh_red);
+  const double e = active ? mpj_exp(P.nil * (c - rho_b)) : 0.0;
+  if (side == 0) sh_e[pair] = e;
+  const double eta_b = block_reduce_sum(side == 0 ? e : 0.0, sh_red);
+  const double fc_b = block_reduce_sum((side == 0 && active && feas) ? 1.0 : 0.0, sh_red);
+  __syncthreads();  // ctrl_all stores of this block -> visible to its own loads below (same CU)
+  double* part = A.part + ((size_t)s * A.nb + b) * A.pstride;
+  {
+    // Σ_i e_i u_i[t] over this block's rollouts; two fixed halves per output, summed in order
+    const int t = tid % 128, q = tid / 128;
+    const int r0 = q * (RPB / 2), r1 = r0 + RPB / 2;
+    for (int t0 = 0; t0 < H2; t0 += 128) {  // block-uniform trip count: barriers are safe
+      const int tt = t0 + t;
+      double acc = 0.0;
+      if (tt < H2) {
+        for (int r = r0; r < r1; r++) {
+          const int kr = b * RPB + r;
+          if (kr < K) acc = acc + sh_e[r] * A.ctrl_all[((size_t)s * K + kr) * H2 + tt];
+        }
+      }
+      sh_q[q][t] = acc;
+      __syncthreads();
+      if (q == 0 && tt < H2) part[4 + tt] = sh_q[0][t] + sh_q[1][t];
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {
+    part[0] = rho_b;
+    part[1] = eta_b;
+    part[2] = fc_b;
+  }
+  // ---------------- arrival: release (Guideline 16 recipe), ticket
+  __syncthreads();  // every wave's stores done (workgroup release waits vmcnt(0))
+  if (tid == 0) {
+    __threadfence();  // agent-scope release: write back this XCD's L2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = atomicAdd(A.tickets + s, 1u);
+    sh_last = (t == (unsigned)(A.nb - 1));
+    if (sh_last) {
+      __threadfence();  // agent-scope acquire: invalidate this CU's L1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!sh_last) return;
+
+  // ---------------- phase 2: combine + final rollout (last block of scene s)
+  double* Ush = dyn;          // [H2]
+  double* scale = dyn + H2;   // [nb]
+  const double* partS = A.part + (size_t)s * A.nb * A.pstride;
+  // FeasibilityCount prefix (MPPIUtils.jl:175): m = rollouts actually run
+  __shared__ int sh_m, sh_bstar, sh_fc;
+  if (tid == 0) {
+    int tot = 0;
+    for (int i = 0; i < A.nb; i++) tot += (int)partS[(size_t)i * A.pstride + 2];
+    int m = K, bstar = A.nb, fcount = tot;
+    if (tot > P.FC) {
+      int cum = 0;
+      for (int i = 0; i < A.nb; i++) {
+        const int f = (int)partS[(size_t)i * A.pstride + 2];
+        if (cum + f > P.FC) { bstar = i; break; }
+        cum += f;
+      }
+      for (int r = 0; r < RPB; r++) {
+        const int kr = bstar * RPB + r;
+        cum += A.feas_all[(size_t)s * K + kr];
+        if (cum == P.FC + 1) { m = kr + 1; break; }
+      }
+      fcount = P.FC + 1;
+    }
+    sh_m = m;
+    sh_bstar = (m == K) ? A.nb : bstar;
+    sh_fc = fcount;
+  }
+  __syncthreads();
+  const int m = sh_m, nfull = sh_bstar;  // blocks [0, nfull) complete; [nfull*RPB, m) partial
+  // partial boundary block, recomputed from the stored per-rollout costs / controls
+  double rho_p = __builtin_inf(), eta_p = 0.0;
+  const int p0 = nfull * RPB;
+  const bool has_p = p0 < m;
+  if (has_p) {
+    const int kr = p0 + pair;
+    const bool in = kr < m;
+    const double cr = in ? A.cost_all[(size_t)s * K + kr] : __builtin_inf();
+    rho_p = block_reduce_min(cr, sh_red);
+    const double er = in ? mpj_exp(P.nil * (cr - rho_p)) : 0.0;
+    if (side == 0) sh_e[pair] = er;
+    eta_p = block_reduce_sum(side == 0 ? er : 0.0, sh_red);
+  }
+  __syncthreads();
+  // global ρ
+  double rho = rho_p;
+  for (int i = tid; i < nfull; i += NT) rho = nanmin(rho, partS[(size_t)i * A.pstride]);
+  rho = block_reduce_min(rho, sh_red);
+  for (int i = tid; i < nfull; i += NT) scale[i] = mpj_exp(P.nil * (partS[(size_t)i * A.pstride] - rho));
+  __syncthreads();
+  const double scale_p = has_p ? mpj_exp(P.nil * (rho_p - rho)) : 0.0;
+  // η and MPPICtrl = Σ_b scale_b Σ_i e_i u_i  /  η      (fixed order over blocks)
+  __shared__ double sh_eta;
+  if (tid == 0) {
+    double eta = 0.0;
+    for (int i = 0; i < nfull; i++) eta = eta + partS[(size_t)i * A.pstride + 1] * scale[i];
+    if (has_p) eta = eta + eta_p * scale_p;
+    sh_eta = eta;
+  }
+  __syncthreads();
+  const double inv_eta = 1.0 / sh_eta;
+  for (int t = tid; t < H2; t += NT) {
+    double acc = 0.0;
+    for (int i = 0; i < nfull; i++) acc = acc + partS[(size_t)i * A.pstride + 4 + t] * scale[i];
+    if (has_p) {
+      double ap = 0.0;
+      for (int r = 0; r < m - p0; r++) ap = ap + sh_e[r] * A.ctrl_all[((size_t)s * K + p0 + r) * H2 + t];
+      acc = acc + ap * scale_p;
+    }
+    Ush[t] = acc * inv_eta;
+  }
+  __syncthreads();
+  // final TrajectoryRollout(MPPICtrl) — every pair runs it redundantly, pair 0 writes
+  {
+    auto ctrl = [&](int j, double* u) { u[0] = Ush[2 * j]; u[1] = Ush[2 * j + 1]; };
+    auto store = [&](int, const double*) {};
+    double* traj = (pair == 0) ? A.traj_out + (size_t)s * (H + 1) * 7 : nullptr;
+    int f2;
+    const double c2 = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &f2);
+    if (tid == 0) {
+      A.cost_out[s] = c2;
+      A.feas_out[s] = f2;
+      A.rc_out[s] = m + 1;
+      A.fc_out[s] = sh_fc;
+      A.tickets[s] = 0u;  // every block of this scene has arrived
+      if (c2 != c2 || rho != rho) atomicOr(A.flags, 1);
+    }
+  }
+  for (int t = tid; t < H2; t += NT) A.U_out[(size_t)s * H2 + t] = Ush[t];
+}
+
+// ------------------------------------------------------------- mp_rollout
+__global__ __launch_bounds__(NT) void rollout_kernel(MppiDev P, int K, const double* X0, const double* goal,
+                                                     const double* ctrl, long long cs, const double* unom,
+                                                     const double* obs, const unsigned char* grid, double* traj,
+                                                     double* cost, unsigned char* feas, int nb) {
+  const int H = P.H;
+  const int s = blockIdx.x / nb, b = blockIdx.x % nb;
+  const int tid = threadIdx.x, pair = tid >> 1, side = tid & 1;
+  const int k = b * RPB + pair;
+  const bool active = k < K;
+  const int kk = active ? k : K - 1;
+  const double* cu = ctrl + ((size_t)s * K + kk) * (cs ? (size_t)cs * H : 2);
+  auto cf = [&](int j, double* u) {
+    const double* q = cu + (size_t)j * cs;
+    u[0] = q[0];
+    u[1] = q[1];
+  };
+  auto store = [&](int, const double*) {};
+  double* tr = (traj && active) ? traj + ((size_t)s * K + k) * (H + 1) * 7 : nullptr;
+  int f;
+  const double c = rollout_pair(P, X0 + 7 * s, goal + 2 * s, obs ? obs + (size_t)3 * P.n_obs * s : nullptr,
+                                grid ? grid + (size_t)P.gnx * P.gny * s : nullptr,
+                                unom ? unom + (size_t)2 * H * s : nullptr, side, cf, store, tr, &f);
+  if (active && side == 0) {
+    cost[(size_t)s * K + k] = c;
+    feas[(size_t)s * K + k] = (unsigned char)f;
+  }
+}
+
+// first minimum per scene with Julia isless semantics (DWAUtils.jl:152 `minimum`)
+__global__ __launch_bounds__(NT) void argmin_kernel(int K, const double* cost, int* out) {
+  __shared__ double sv[NT];
+  __shared__ int si[NT];
+  const int s = blockIdx.x;
+  double bv = 0.0;
+  int bi = -1;
+  for (int i = threadIdx.x; i < K; i += NT) {
+    const double v = cost[(size_t)s * K + i];
+    if (bi < 0 || mpj_isless(v, bv)) { bv = v; bi = i; }
+  }
+  sv[threadIdx.x] = bv;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double v = sv[0];
+    int ix = si[0];
+    for (int t = 1; t < NT; t++) {
+      if (si[t] < 0) continue;
+      if (ix < 0 || mpj_isless(sv[t], v) || (!mpj_isless(v, sv[t]) && si[t] < ix)) { v = sv[t]; ix = si[t]; }
+    }
+    out[s] = ix;
+  }
+}
+
+// ------------------------------------------------------------ plant (Euler)
+// MPPI/main.jl:259-261: states .+= VehicleDynamics(states, u)*δt; one lane pair per vehicle
+__global__ __launch_bounds__(64) void euler_kernel(int n, double* states, const double* ctrl, double dt,
+                                                   int nsteps, double* his) {
+  const int tid = blockIdx.x * 64 + threadIdx.x;
+  const int v = tid >> 1, side = tid & 1;
+  const int vv = v < n ? v : n - 1;
+  double x[7], d[7];
+  for (int i = 0; i < 7; i++) x[i] = states[7 * vv + i];
+  const double sr = ctrl[2 * vv], ax = ctrl[2 * vv + 1];
+  for (int t = 0; t < nsteps; t++) {
+    dyn_pair(x, sr, ax, d, side);
+    for (int i = 0; i < 7; i++) x[i] = x[i] + d[i] * dt;
+    if (his && v < n && side == 0)
+      for (int i = 0; i < 7; i++) his[((size_t)v * nsteps + t) * 7 + i] = x[i];
+  }
+  if (v < n && side == 0)
+    for (int i = 0; i < 7; i++) states[7 * v + i] = x[i];
+}
+
+// ----------------------------------------------------------------- host
+static void inv2(const double* A, double* Ai) {
+  const double a = A[0], b = A[1], c = A[2], d = A[3];
+  if (b == 0.0 && c == 0.0) {
+    Ai[0] = 1.0 / a; Ai[1] = 0.0; Ai[2] = 0.0; Ai[3] = 1.0 / d;
+    return;
+  }
+  const bool swap = __builtin_fabs(c) > __builtin_fabs(a);
+  const double p11 = swap ? c : a, p12 = swap ? d : b, q11 = swap ? a : c, q12 = swap ? b : d;
+  const double l = q11 / p11, u22 = q12 - l * p12;
+  const double iu11 = 1.0 / p11, iu22 = 1.0 / u22, iu12 = -(p12 * iu11) * iu22;
+  const double m11 = iu11 - iu12 * l, m12 = iu12, m21 = -iu22 * l, m22 = iu22;
+  if (swap) { Ai[0] = m12; Ai[1] = m11; Ai[2] = m22; Ai[3] = m21; }
+  else { Ai[0] = m11; Ai[1] = m12; Ai[2] = m21; Ai[3] = m22; }
+}
+
+static int make_dev_params(mp_ctx* ctx, const mp_mppi_params* p, int K, MppiDev* D) {
+  MP_CHECK(ctx, p != nullptr, "params is NULL");
+  MP_CHECK(ctx, K >= 1, "SamplingNumber K (%d) must be >= 1", K);
+  MP_CHECK(ctx, p->H >= 1 && p->H <= 4096, "horizon N (%d) must be in [1, 4096]", p->H);
+  MP_CHECK(ctx, p->n_obs >= 0, "n_obs (%d) must be >= 0", p->n_obs);
+  MP_CHECK(ctx, p->dt > 0.0, "dt (%g) must be > 0", p->dt);
+  MP_CHECK(ctx, p->grid_nx >= 0 && p->grid_ny >= 0, "grid dims must be >= 0");
+  MP_CHECK(ctx, p->noise_mode == MP_NOISE_EXTERNAL || p->noise_mode == MP_NOISE_PHILOX, "bad noise_mode %d",
+           p->noise_mode);
+  D->K = K;
+  D->H = p->H;
+  D->FC = p->feasibility_count;
+  D->n_obs = p->n_obs;
+  D->dt = p->dt;
+  D->lambda = p->lambda;
+  D->nil = (-1.0) / p->lambda;
+  const double* S = p->sigma;
+  MP_CHECK(ctx, S[0] > 0.0, "Σ must be positive definite");
+  const double l11 = __builtin_sqrt(S[0]);
+  const double l21 = S[2] / l11;
+  const double r22 = S[3] - l21 * l21;
+  MP_CHECK(ctx, r22 > 0.0, "Σ must be positive definite");
+  D->L[0] = l11; D->L[1] = 0.0; D->L[2] = l21; D->L[3] = __builtin_sqrt(r22);
+  inv2(S, D->Si);
+  for (int i = 0; i < 7; i++) { D->XL[i] = p->XL[i]; D->XU[i] = p->XU[i]; }
+  for (int i = 0; i < 2; i++) { D->CL[i] = p->CL[i]; D->CU[i] = p->CU[i]; }
+  D->slack = p->slack_penalty;
+  D->obs_pen = p->obs_penalty;
+  D->gnx = p->grid_nx;
+  D->gny = p->grid_ny;
+  D->gx0 = p->grid_x0; D->gy0 = p->grid_y0; D->gdx = p->grid_dx; D->gdy = p->grid_dy;
+  D->noise_mode = p->noise_mode;
+  D->ctrl_cost = p->ctrl_cost;
+  D->seed = p->seed;
+  D->offset = p->offset;
+  return MP_OK;
+}
+
+static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, const double* goal,
+                       const double* U_nom, const double* obstacles, const uint8_t* grid, const double* noise,
+                       double* U_out, double* traj_out, double* cost_out, int32_t* feasible_out,
+                       int32_t* rc_out, int32_t* fc_out, double* coll_traj, double* coll_ctrl,
+                       double* coll_cost, uint8_t* coll_feas) {
+  const int K = D.K, H = D.H;
+  const int nb = (K + RPB - 1) / RPB;
+  const int pstride = 4 + 2 * H;
+  PlanArgs A;
+  A.X0 = X0; A.goal = goal; A.unom = U_nom; A.obs = D.n_obs > 0 ? obstacles : nullptr;
+  A.grid = D.gnx > 0 ? grid : nullptr; A.noise = noise;
+  A.ctrl_all = coll_ctrl ? coll_ctrl : (double*)mp_ws(ctx, WS_IO14, sizeof(double) * (size_t)S * K * 2 * H);
+  A.cost_all = coll_cost ? coll_cost : (double*)mp_ws(ctx, WS_MPPI_COST, sizeof(double) * (size_t)S * K);
+  A.feas_all = coll_feas ? coll_feas : (unsigned char*)mp_ws(ctx, WS_MPPI_FEAS, (size_t)S * K);
+  A.part = (double*)mp_ws(ctx, WS_MPPI_PART, sizeof(double) * (size_t)S * nb * pstride);
+  if (!A.ctrl_all || !A.cost_all || !A.feas_all || !A.part) return MP_ERR_NOMEM;
+  A.coll_traj = coll_traj;
+  int st = mp_ticket_reserve(ctx, S);
+  if (st) return st;
+  A.tickets = ctx->tickets;
+  A.flags = ctx->flags;
+  A.U_out = U_out; A.traj_out = traj_out; A.cost_out = cost_out; A.feas_out = feasible_out;
+  A.rc_out = rc_out; A.fc_out = fc_out;
+  A.nb = nb;
+  A.pstride = pstride;
+  const size_t shmem = sizeof(double) * (size_t)(2 * H + nb);
+  MP_CHECK(ctx, shmem <= 60 * 1024, "K/H too large for one scene (dynamic LDS %zu B)", shmem);
+  hipLaunchKernelGGL(mppi_plan_kernel, dim3(S * nb), dim3(NT), shmem, ctx->stream, D, A);
+  MP_HIP(ctx, hipGetLastError());
+  return MP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mp_mppi_plan_dev(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* X0, const double* goal,
+                     const double* U_nom, const double* obstacles, const uint8_t* grid, const double* noise,
+                     double* U_out, double* traj_out, double* cost_out, int32_t* feasible_out,
+                     int32_t* rollout_count_out, int32_t* feasible_count_out, double* coll_traj,
+                     double* coll_ctrl, double* coll_cost, uint8_t* coll_feas) {
+  if (!ctx) return MP_ERR_INVALID;
+  MppiDev D;
+  int st = make_dev_params(ctx, p, p ? p->K : 0, &D);
+  if (st) return st;
+  MP_CHECK(ctx, S >= 1, "S (%d) must be >= 1", S);
+  MP_CHECK(ctx, X0 && goal && U_nom && U_out && traj_out && cost_out && feasible_out && rollout_count_out &&
+               feasible_count_out, "required pointer is NULL");
+  MP_CHECK(ctx, p->noise_mode != MP_NOISE_EXTERNAL || noise, "noise is NULL in MP_NOISE_EXTERNAL mode");
+  MP_CHECK(ctx, p->n_obs == 0 || obstacles, "obstacles NULL with n_obs > 0");
+  MP_CHECK(ctx, p->grid_nx == 0 || grid, "grid NULL with grid_nx > 0");
+  return plan_launch(ctx, D, S, X0, goal, U_nom, obstacles, grid, noise, U_out, traj_out, cost_out, feasible_out,
+                     rollout_count_out, feasible_count_out, coll_traj, coll_ctrl, coll_cost, coll_feas);
+}
+
+int mp_mppi_plan(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* X0, const double* goal,
+                 const double* U_nom, const double* obstacles, const uint8_t* grid, const double* noise,
+                 double* U_out, double* traj_out, double* cost_out, int32_t* feasible_out,
+                 int32_t* rollout_count_out, int32_t* feasible_count_out, double* coll_traj, double* coll_ctrl,
+                 double* coll_cost, uint8_t* coll_feas) {
+  if (!ctx) return MP_ERR_INVALID;
+  MppiDev D;
+  int st = make_dev_params(ctx, p, p ? p->K : 0, &D);
+  if (st) return st;
+  MP_CHECK(ctx, S >= 1, "S (%d) must be >= 1", S);
+  MP_CHECK(ctx, X0 && goal && U_nom && U_out && traj_out && cost_out && feasible_out && rollout_count_out &&
+               feasible_count_out, "required pointer is NULL");
+  MP_CHECK(ctx, p->noise_mode != MP_NOISE_EXTERNAL || noise, "noise is NULL in MP_NOISE_EXTERNAL mode");
+  MP_CHECK(ctx, p->n_obs == 0 || obstacles, "obstacles NULL with n_obs > 0");
+  MP_CHECK(ctx, p->grid_nx == 0 || grid, "grid NULL with grid_nx > 0");
+  MP_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t K = p->K, H = p->H;
+  st = MP_OK;
+  const double* dX0 = mp_upload(ctx, WS_IO0, X0, 7 * (size_t)S, &st);
+  const double* dgoal = mp_upload(ctx, WS_IO1, goal, 2 * (size_t)S, &st);
+  const double* dun = mp_upload(ctx, WS_IO2, U_nom, 2 * H * S, &st);
+  const double* dobs = mp_upload(ctx, WS_IO3, p->n_obs ? obstacles : nullptr, 3 * (size_t)p->n_obs * S, &st);
+  const uint8_t* dgrid = mp_upload(ctx, WS_IO4, p->grid_nx ? grid : nullptr, (size_t)p->grid_nx * p->grid_ny * S, &st);
+  const double* dnoise = mp_upload(ctx, WS_IO5, p->noise_mode == MP_NOISE_EXTERNAL ? noise : nullptr, K * H * 2 * S, &st);
+  double* dU = mp_alloc_out(ctx, WS_IO6, U_out, 2 * H * S, &st);
+  double* dtraj = mp_alloc_out(ctx, WS_IO7, traj_out, (H + 1) * 7 * S, &st);
+  double* dcost = mp_alloc_out(ctx, WS_IO8, cost_out, (size_t)S, &st);
+  int32_t* dfe = mp_alloc_out(ctx, WS_IO9, feasible_out, (size_t)S, &st);
+  int32_t* drc = mp_alloc_out(ctx, WS_IO10, rollout_count_out, (size_t)S, &st);
+  int32_t* dfc = mp_alloc_out(ctx, WS_IO11, feasible_count_out, (size_t)S, &st);
+  double* dct = mp_alloc_out(ctx, WS_IO12, coll_traj, K * (H + 1) * 7 * S, &st);
+  double* dcc = mp_alloc_out(ctx, WS_IO13, coll_ctrl, K * H * 2 * S, &st);
+  double* dco = mp_alloc_out(ctx, WS_IO15, coll_cost, K * S, &st);
+  uint8_t* dcf = mp_alloc_out(ctx, WS_IO16, coll_feas, K * S, &st);
+  if (st) return st;
+  MP_HIP(ctx, hipMemsetAsync(ctx->flags, 0, sizeof(int), ctx->stream));
+  st = plan_launch(ctx, D, S, dX0, dgoal, dun, dobs, dgrid, dnoise, dU, dtraj, dcost, dfe, drc, dfc, dct, dcc,
+                   dco, dcf);
+  if (st) return st;
+  int flag = 0;
+  if ((st = mp_download(ctx, U_out, dU, 2 * H * S))) return st;
+  if ((st = mp_download(ctx, traj_out, dtraj, (H + 1) * 7 * S))) return st;
+  if ((st = mp_download(ctx, cost_out, dcost, (size_t)S))) return st;
+  if ((st = mp_download(ctx, feasible_out, dfe, (size_t)S))) return st;
+  if ((st = mp_download(ctx, rollout_count_out, drc, (size_t)S))) return st;
+  if ((st = mp_download(ctx, feasible_count_out, dfc, (size_t)S))) return st;
+  if ((st = mp_download(ctx, coll_traj, dct, K * (H + 1) * 7 * S))) return st;
+  if ((st = mp_download(ctx, coll_ctrl, dcc, K * H * 2 * S))) return st;
+  if ((st = mp_download(ctx, coll_cost, dco, K * S))) return st;
+  if ((st = mp_download(ctx, coll_feas, dcf, K * S))) return st;
+  if ((st = mp_download(ctx, &flag, ctx->flags, 1))) return st;
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (flag & 1) return mp_fail(ctx, MP_ERR_NUMERIC, "NaN rollout cost (Julia would have produced NaN weights)");
+  return MP_OK;
+}
+
+int mp_rollout(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, int32_t K, const double* X0, const double* goal,
+               const double* ctrl, int64_t ctrl_stride_h, const double* U_nom, const double* obstacles,
+               const uint8_t* grid, double* traj, double* cost, uint8_t* feas, int32_t* argmin) {
+  if (!ctx) return MP_ERR_INVALID;
+  MppiDev D;
+  int st = make_dev_params(ctx, p, K, &D);
+  if (st) return st;
+  MP_CHECK(ctx, S >= 1, "S (%d) must be >= 1", S);
+  MP_CHECK(ctx, X0 && goal && ctrl && cost && feas, "required pointer is NULL");
+  MP_CHECK(ctx, ctrl_stride_h == 0 || ctrl_stride_h == 2, "ctrl_stride_h must be 0 or 2");
+  MP_CHECK(ctx, !p->ctrl_cost || U_nom, "U_nom NULL with ctrl_cost");
+  MP_CHECK(ctx, p->n_obs == 0 || obstacles, "obstacles NULL with n_obs > 0");
+  MP_CHECK(ctx, p->grid_nx == 0 || grid, "grid NULL with grid_nx > 0");
+  MP_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t H = p->H, KK = K;
+  const size_t nctrl = ctrl_stride_h ? KK * H * 2 * S : KK * 2 * S;
+  st = MP_OK;
+  const double* dX0 = mp_upload(ctx, WS_IO0, X0, 7 * (size_t)S, &st);
+  const double* dgoal = mp_upload(ctx, WS_IO1, goal, 2 * (size_t)S, &st);
+  const double* dun = mp_upload(ctx, WS_IO2, p->ctrl_cost ? U_nom : nullptr, 2 * H * S, &st);
+  const double* dobs = mp_upload(ctx, WS_IO3, p->n_obs ? obstacles : nullptr, 3 * (size_t)p->n_obs * S, &st);
+  const uint8_t* dgrid = mp_upload(ctx, WS_IO4, p->grid_nx ? grid : nullptr, (size_t)p->grid_nx * p->grid_ny * S, &st);
+  const double* dctrl = mp_upload(ctx, WS_IO5, ctrl, nctrl, &st);
+  double* dtraj = mp_alloc_out(ctx, WS_IO6, traj, KK * (H + 1) * 7 * S, &st);
+  double* dcost = mp_alloc_out(ctx, WS_IO7, cost, KK * S, &st);
+  uint8_t* dfeas = mp_alloc_out(ctx, WS_IO8, feas, KK * S, &st);
+  int32_t* dam = mp_alloc_out(ctx, WS_IO9, argmin, (size_t)S, &st);
+  if (st) return st;
+  const int nb = (K + RPB - 1) / RPB;
+  hipLaunchKernelGGL(rollout_kernel, dim3(S * nb), dim3(NT), 0, ctx->stream, D, K, dX0, dgoal, dctrl,
+                     (long long)ctrl_stride_h, dun, dobs, dgrid, dtraj, dcost, dfeas, nb);
+  MP_HIP(ctx, hipGetLastError());
+  if (dam) {
+    hipLaunchKernelGGL(argmin_kernel, dim3(S), dim3(NT), 0, ctx->stream, K, dcost, dam);
+    MP_HIP(ctx, hipGetLastError());
+  }
+  if ((st = mp_download(ctx, traj, dtraj, KK * (H + 1) * 7 * S))) return st;
+  if ((st = mp_download(ctx, cost, dcost, KK * S))) return st;
+  if ((st = mp_download(ctx, feas, dfeas, KK * S))) return st;
+  if ((st = mp_download(ctx, argmin, dam, (size_t)S))) return st;
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MP_OK;
+}
+
+int mp_vehicle_euler(mp_ctx* ctx, int32_t n, double* states, const double* ctrl, double dt, int32_t nsteps,
+                     double* his) {
+  if (!ctx) return MP_ERR_INVALID;
+  MP_CHECK(ctx, n >= 1 && nsteps >= 0 && states && ctrl, "bad arguments to mp_vehicle_euler");
+  MP_HIP(ctx, hipSetDevice(ctx->device));
+  int st = MP_OK;
+  double* ds = (double*)mp_upload(ctx, WS_IO0, states, 7 * (size_t)n, &st);
+  const double* dc = mp_upload(ctx, WS_IO1, ctrl, 2 * (size_t)n, &st);
+  double* dh = mp_alloc_out(ctx, WS_IO2, his, (size_t)n * nsteps * 7, &st);
+  if (st) return st;
+  const int blocks = (2 * n + 63) / 64;
+  hipLaunchKernelGGL(euler_kernel, dim3(blocks), dim3(64), 0, ctx->stream, n, ds, dc, dt, nsteps, dh);
+  MP_HIP(ctx, hipGetLastError());
+  if ((st = mp_download(ctx, states, (const double*)ds, 7 * (size_t)n))) return st;
+  if ((st = mp_download(ctx, his, (const double*)dh, (size_t)n * nsteps * 7))) return st;
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,240 @@
+// mppi_device.hpp — device-side restatement of the MPPI rollout
+// (OptimalControl/MPPI/src/MPPIUtils.jl:31-57, vehicledynamics.jl:1-54).
+//
+// Mapping (gfx950): one rollout = one LANE PAIR of a 64-wide wavefront.
+// The two lanes of a pair evaluate the two tire models of VehicleDynamics in
+// SIMD (front on the even lane, rear on the odd lane: the same instruction
+// stream with lane-selected constants, bit-identical to the scalar formulas),
+// exchange the lateral forces with one DPP/ds_swizzle shuffle, and carry the
+// 7-state replicated in registers.  That halves the serial transcendental
+// chain per step (4 instead of 8 dependent atan/sin per dynamics call) and
+// doubles the waves in flight for a fixed K.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/mp_jlmath.h"
+
+namespace mpk {
+
+struct MppiDev {
+  int K, H, FC, n_obs;
+  double dt, lambda, nil;  // nil = (-1)/λ as evaluated by the reference (MPPIUtils.jl:160)
+  double L[4];             // chol(Σ).L row-major
+  double Si[4];            // inv(Σ) row-major
+  double XL[7], XU[7], CL[2], CU[2];
+  double slack, obs_pen;
+  int gnx, gny;
+  double gx0, gy0, gdx, gdy;
+  int noise_mode, ctrl_cost;
+  unsigned long long seed, offset;
+};
+
+// ---------------------------------------------------------------- dynamics
+// VehicleDynamics for a lane pair.  side = lane & 1 (0: front tire, 1: rear).
+__device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side) {
+  const double la = 1.56, lb = 1.64, M = 2020.0, Izz = 4095.0, g = 9.81, mu = 0.8;
+  const double KFZF = 1018.28 / 2, KFZR = 963.34 / 2, KFZX = 186.22;
+  const double B = -10.4 / mu, C = 1.3, E = 0.1556;
+  const double v = x[2], r = x[3], psi = x[4], ux = x[5], sa = x[6];
+  const double t = (ax - r * v) * KFZX;
+  // front: 2*(KFZF*g - t);  rear: 2*(KFZR*g + t)   (vehicledynamics.jl:30-31)
+  const double FZ = 2 * ((side ? KFZR : KFZF) * g + (side ? t : -t));
+  // front: (v + la*r) ... - sa;  rear: (v - lb*r) ... [(-lb)*r == -(lb*r) exactly]  (:32-33)
+  const double alpha = mpj_atan((v + (side ? -lb : la) * r) / (ux + 0.01)) - (side ? 0.0 : sa);
+  const double X1 = B * alpha;
+  const double FY = mu * FZ * 1.0 * mpj_sin(C * mpj_atan(X1 - E * (X1 - mpj_atan(X1))));  // (:35-38)
+  const double FYo = __shfl_xor(FY, 1);
+  const double FY1 = side ? FYo : FY, FY2 = side ? FY : FYo;
+  const double uxc = ux <= 0 ? 0.0 : ux;  // (:40-42)
+  double sp, cp;
+  mpj_sincos(psi, &sp, &cp);
+  d[0] = uxc * cp - v * sp;
+  d[1] = uxc * sp + v * cp;
+  d[2] = (FY1 + FY2) / M - r * uxc;
+  d[3] = (FY1 * la - FY2 * lb) / Izz;
+  d[4] = r;
+  d[5] = ax;
+  d[6] = sr;
+}
+
+// running cost, vehicledynamics.jl:52
+__device__ __forceinline__ double run_cost(const double* x, double sr, double ax) {
+  const double y = x[1], v = x[2], r = x[3], sa = x[6];
+  return v * v * 1 + 1 * (r * r) + 5 * (ax * ax) + 3 * (sr * sr) + 2 * (sa * sa) + 10 * (y * y);
+}
+
+// ObstacleEvaluation (MPPIUtils.jl:120-132) + occupancy grid (build extension)
+__device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* x, const double* obs,
+                                                const unsigned char* grid, int* ok) {
+  double c = 0.0;
+  for (int o = 0; o < P.n_obs; o++) {
+    const double dx = x[0] - obs[3 * o], dy = x[1] - obs[3 * o + 1], R = obs[3 * o + 2];
+    if (dx * dx + dy * dy <= R * R) {
+      *ok = 0;
+      c = c + P.obs_pen;
+    }
+  }
+  if (P.gnx > 0) {
+    const double fx = (x[0] - P.gx0) / P.gdx;
+    const double fy = (x[1] - P.gy0) / P.gdy;
+    if (fx >= 0.0 && fy >= 0.0 && fx < (double)P.gnx && fy < (double)P.gny) {
+      const int ix = (int)fx, iy = (int)fy;
+      if (grid[iy * P.gnx + ix]) {
+        *ok = 0;
+        c = c + P.obs_pen;
+      }
+    }
+  }
+  return c;
+}
+
+// BoundEvaluation, MPPIUtils.jl:135-151
+__device__ __forceinline__ double bound_cost(const MppiDev& P, const double* x, int* ok) {
+  double c = 0.0;
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    if (x[i] < P.XL[i]) {
+      *ok = 0;
+      c = c + P.slack * __builtin_fabs(x[i] - P.XL[i]);
+    }
+    if (x[i] > P.XU[i]) {
+      *ok = 0;
+      c = c + P.slack * __builtin_fabs(x[i] - P.XU[i]);
+    }
+  }
+  return c;
+}
+
+// ------------------------------------------------------------------ noise
+__device__ __forceinline__ void philox4x32(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned k0,
+                                           unsigned k1, unsigned* o) {
+#pragma unroll
+  for (int i = 0; i < 10; i++) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c2;
+    const unsigned hi0 = (unsigned)(p0 >> 32), lo0 = (unsigned)p0;
+    const unsigned hi1 = (unsigned)(p1 >> 32), lo1 = (unsigned)p1;
+    const unsigned n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  o[0] = c0;
+  o[1] = c1;
+  o[2] = c2;
+  o[3] = c3;
+}
+
+// two N(0,1) draws for (scene, rollout k, step h): Philox4x32-10 + Box–Muller
+__device__ __forceinline__ void philox_normal2(const MppiDev& P, unsigned scene, unsigned k, unsigned h,
+                                               double* z) {
+  unsigned o[4];
+  philox4x32(k, h, scene, (unsigned)P.offset, (unsigned)P.seed,
+             (unsigned)(P.seed >> 32) ^ (unsigned)(P.offset >> 32), o);
+  const unsigned long long b1 = ((unsigned long long)(o[0] >> 5) << 26) | (unsigned long long)(o[1] >> 6);
+  const unsigned long long b2 = ((unsigned long long)(o[2] >> 5) << 26) | (unsigned long long)(o[3] >> 6);
+  const double u1 = ((double)b1 + 0.5) * 1.1102230246251565e-16;
+  const double u2 = ((double)b2 + 0.5) * 1.1102230246251565e-16;
+  const double rr = mpj_sqrt(-2.0 * mpj_log(u1));
+  double sn, cs;
+  mpj_sincos(MPJ_TWO_PI * u2, &sn, &cs);
+  z[0] = rr * cs;
+  z[1] = rr * sn;
+}
+
+// SampleMPPIControl + PushInBounds (MPPIUtils.jl:5-20): u = clamp(u_nom + L z, CL, CU)
+__device__ __forceinline__ void sample_ctrl(const MppiDev& P, const double* z, const double* un, double* u) {
+  const double n0 = P.L[0] * z[0];
+  const double n1 = P.L[3] * z[1] + P.L[2] * z[0];
+  const double v0 = n0 + un[0], v1 = n1 + un[1];
+  u[0] = __builtin_fmin(__builtin_fmax(v0, P.CL[0]), P.CU[0]);
+  u[1] = __builtin_fmin(__builtin_fmax(v1, P.CL[1]), P.CU[1]);
+}
+
+__device__ __forceinline__ void draw_ctrl(const MppiDev& P, const double* noise_s, const double* unom_s,
+                                          unsigned scene, int k, int h, double* u) {
+  double z[2];
+  if (P.noise_mode == 0) {
+    const double2 zz = *reinterpret_cast<const double2*>(noise_s + ((size_t)k * P.H + h) * 2);
+    z[0] = zz.x;
+    z[1] = zz.y;
+  } else {
+    philox_normal2(P, scene, (unsigned)k, (unsigned)h, z);
+  }
+  sample_ctrl(P, z, unom_s + 2 * h, u);
+}
+
+// --------------------------------------------------------------- rollout
+// TrajectoryRollout for the lane pair (MPPIUtils.jl:31-57).  `ctrl(j, u)` yields the
+// control of step j.  traj (optional) gets (H+1)x7 states: the even lane stores
+// x[0..3], the odd lane x[4..6].  Returns cost_total; *feas = constraint.
+template <class CtrlFn, class StoreFn>
+__device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X0, const double* goal,
+                                               const double* obs, const unsigned char* grid,
+                                               const double* unom, int side, CtrlFn ctrl, StoreFn store,
+                                               double* traj, int* feas) {
+  double x[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) x[i] = X0[i];
+  if (traj) {
+    if (side == 0) { for (int i = 0; i < 4; i++) traj[i] = x[i]; }
+    else { for (int i = 4; i < 7; i++) traj[i] = x[i]; }
+  }
+  double sum = 0.0;
+  int ok_all = 1;
+  for (int j = 0; j < P.H; j++) {
+    double u[2];
+    ctrl(j, u);
+    store(j, u);
+    int okc = 1, okb = 1;
+    double cc = 0.0, cb = 0.0;
+    if (j > 0) {
+      cc = obstacle_cost(P, x, obs, grid, &okc);
+      cb = bound_cost(P, x, &okb);
+    }
+    const double pc = run_cost(x, u[0], u[1]);
+    double k1[7], k2[7], x2[7];
+    dyn_pair(x, u[0], u[1], k1, side);
+#pragma unroll
+    for (int i = 0; i < 7; i++) x2[i] = x[i] + k1[i] * P.dt;
+    dyn_pair(x2, u[0], u[1], k2, side);
+#pragma unroll
+    for (int i = 0; i < 7; i++) x[i] = x[i] + P.dt * (k1[i] + k2[i]) / 2;
+    double cj = pc + cb + cc;
+    if (P.ctrl_cost) {
+      const double un0 = unom[2 * j], un1 = unom[2 * j + 1];
+      const double a0 = P.lambda * un0, a1 = P.lambda * un1;
+      const double t0 = a0 * P.Si[0] + a1 * P.Si[2], t1 = a0 * P.Si[1] + a1 * P.Si[3];
+      const double d0 = u[0] - un0, d1 = u[1] - un1;
+      cj = cj + (t0 * d0 + t1 * d1);
+    }
+    sum = sum + cj;
+    ok_all &= okc & okb;
+    if (traj) {
+      double* t = traj + 7 * (j + 1);
+      if (side == 0) { for (int i = 0; i < 4; i++) t[i] = x[i]; }
+      else { for (int i = 4; i < 7; i++) t[i] = x[i]; }
+    }
+  }
+  {  // terminal (:49-54): only the running cost of the extra RK2 step is used
+    int okc = 1, okb = 1;
+    const double pc = run_cost(x, 0.0, 0.0);
+    const double cc = obstacle_cost(P, x, obs, grid, &okc);
+    const double cb = bound_cost(P, x, &okb);
+    sum = sum + (pc + cb + cc);
+    ok_all &= okc & okb;
+  }
+  const double tx = x[0] - goal[0], ty = x[1] - goal[1];
+  const double term = tx * tx + ty * ty;
+  const double dx0 = X0[0] - goal[0], dy0 = X0[1] - goal[1];
+  *feas = ok_all;
+  return sum + term / (dx0 * dx0 + dy0 * dy0) * 10000.0;
+}
+
+// Julia isless-style min that treats NaN as the smallest (findmin semantics)
+__device__ __forceinline__ double nanmin(double a, double b) { return (a != a || a < b) ? a : b; }
+
+}  // namespace mpk

@@ -1,0 +1,139 @@
+// runtime.cpp — libmpgpu context lifecycle, error strings, workspaces.
+#include "runtime.hpp"
+
+#include <cstdlib>
+#include <cstring>
+
+static thread_local std::string g_noctx_err;
+
+int mp_fail(mp_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  else g_noctx_err = buf;
+  return code;
+}
+
+void* mp_ws(mp_ctx* ctx, int slot, size_t bytes) {
+  if (slot < 0) return nullptr;
+  if ((int)ctx->ws_ptr.size() <= slot) {
+    ctx->ws_ptr.resize(slot + 1, nullptr);
+    ctx->ws_size.resize(slot + 1, 0);
+  }
+  if (bytes == 0) bytes = 16;
+  if (ctx->ws_size[slot] >= bytes) return ctx->ws_ptr[slot];
+  if (ctx->ws_ptr[slot]) {
+    hipStreamSynchronize(ctx->stream);
+    hipFree(ctx->ws_ptr[slot]);
+    ctx->ws_ptr[slot] = nullptr;
+    ctx->ws_size[slot] = 0;
+  }
+  size_t cap = bytes + bytes / 4;  // grow with headroom
+  void* p = nullptr;
+  if (hipMalloc(&p, cap) != hipSuccess) {
+    mp_fail(ctx, MP_ERR_NOMEM, "hipMalloc(%zu) failed for workspace slot %d", cap, slot);
+    return nullptr;
+  }
+  ctx->ws_ptr[slot] = p;
+  ctx->ws_size[slot] = cap;
+  return p;
+}
+
+int mp_ticket_reserve(mp_ctx* ctx, int n) {
+  if (ctx->n_tickets >= n) return MP_OK;
+  if (ctx->tickets) {
+    hipStreamSynchronize(ctx->stream);
+    hipFree(ctx->tickets);
+    ctx->tickets = nullptr;
+  }
+  int cap = n < 64 ? 64 : n;
+  MP_HIP(ctx, hipMalloc(&ctx->tickets, cap * sizeof(unsigned int)));
+  MP_HIP(ctx, hipMemset(ctx->tickets, 0, cap * sizeof(unsigned int)));
+  ctx->n_tickets = cap;
+  return MP_OK;
+}
+
+void* mp_pinned(mp_ctx* ctx, size_t bytes) {
+  if (ctx->pinned_size >= bytes) return ctx->pinned;
+  if (ctx->pinned) hipHostFree(ctx->pinned);
+  ctx->pinned = nullptr;
+  ctx->pinned_size = 0;
+  if (hipHostMalloc(&ctx->pinned, bytes, 0) != hipSuccess) return nullptr;
+  ctx->pinned_size = bytes;
+  return ctx->pinned;
+}
+
+extern "C" {
+
+const char* mp_version(void) { return MPGPU_VERSION " (gfx950)"; }
+
+int mp_device_count(int* n) {
+  if (!n) return MP_ERR_INVALID;
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    *n = 0;
+    return mp_fail(nullptr, MP_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+  }
+  return MP_OK;
+}
+
+int mp_ctx_create(int device, mp_ctx** out) {
+  if (!out) return MP_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return mp_fail(nullptr, MP_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= n) return mp_fail(nullptr, MP_ERR_INVALID, "device %d out of range [0,%d)", device, n);
+  e = hipSetDevice(device);
+  if (e != hipSuccess) return mp_fail(nullptr, MP_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e));
+  mp_ctx* c = new mp_ctx();
+  c->device = device;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return mp_fail(nullptr, MP_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  if (hipMalloc(&c->flags, 64 * sizeof(int)) != hipSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return mp_fail(nullptr, MP_ERR_NOMEM, "flag buffer allocation failed");
+  }
+  hipMemset(c->flags, 0, 64 * sizeof(int));
+  *out = c;
+  return MP_OK;
+}
+
+int mp_ctx_destroy(mp_ctx* ctx) {
+  if (!ctx) return MP_OK;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  for (void* p : ctx->ws_ptr)
+    if (p) hipFree(p);
+  if (ctx->pinned) hipHostFree(ctx->pinned);
+  if (ctx->tickets) hipFree(ctx->tickets);
+  if (ctx->flags) hipFree(ctx->flags);
+  if (ctx->ha_states_candi) hipFree(ctx->ha_states_candi);
+  if (ctx->ha_paths_candi) hipFree(ctx->ha_paths_candi);
+  hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return MP_OK;
+}
+
+const char* mp_last_error(mp_ctx* ctx) {
+  if (!ctx) return g_noctx_err.c_str();
+  return ctx->err.c_str();
+}
+
+int mp_ctx_synchronize(mp_ctx* ctx) {
+  if (!ctx) return MP_ERR_INVALID;
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MP_OK;
+}
+
+void* mp_ctx_stream(mp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+}  // extern "C"

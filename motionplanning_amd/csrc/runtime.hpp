@@ -1,0 +1,104 @@
+// runtime.hpp — context, error reporting and cached device workspaces for libmpgpu.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "../../include/mpgpu.h"
+
+struct mp_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // growable device scratch buffers, keyed by slot
+  std::vector<void*> ws_ptr;
+  std::vector<size_t> ws_size;
+  // pinned host staging
+  void* pinned = nullptr;
+  size_t pinned_size = 0;
+  // Hybrid A* primitive table (device)
+  double* ha_states_candi = nullptr;
+  double* ha_paths_candi = nullptr;
+  int ha_n_prim = 0, ha_n_col = 0;
+  // per-scene arrival counters for the MPPI last-block combine (zero at rest)
+  unsigned int* tickets = nullptr;
+  int n_tickets = 0;
+  int* flags = nullptr;  // device status flags (NaN seen, ...)
+};
+
+// workspace slots
+enum {
+  WS_MPPI_PART = 0,
+  WS_MPPI_COST,
+  WS_MPPI_FEAS,
+  WS_IO0,
+  WS_IO1,
+  WS_IO2,
+  WS_IO3,
+  WS_IO4,
+  WS_IO5,
+  WS_IO6,
+  WS_IO7,
+  WS_IO8,
+  WS_IO9,
+  WS_IO10,
+  WS_IO11,
+  WS_IO12,
+  WS_IO13,
+  WS_IO14,
+  WS_IO15,
+  WS_IO16,
+  WS_ILQR0,
+  WS_ILQR1,
+  WS_ILQR2,
+  WS_HA0,
+  WS_HA1,
+  WS_HA2,
+  WS_COUNT
+};
+
+int mp_fail(mp_ctx* ctx, int code, const char* fmt, ...);
+void* mp_ws(mp_ctx* ctx, int slot, size_t bytes);  // nullptr on failure (error set)
+int mp_ticket_reserve(mp_ctx* ctx, int n);
+void* mp_pinned(mp_ctx* ctx, size_t bytes);
+
+#define MP_HIP(ctx, call)                                                                \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return mp_fail((ctx), MP_ERR_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                     __FILE__, __LINE__);                                                \
+  } while (0)
+
+#define MP_CHECK(ctx, cond, ...)                              \
+  do {                                                        \
+    if (!(cond)) return mp_fail((ctx), MP_ERR_INVALID, __VA_ARGS__); \
+  } while (0)
+
+// Copy host -> device scratch slot (nullptr-safe); returns device pointer or nullptr.
+template <typename T>
+static inline T* mp_upload(mp_ctx* ctx, int slot, const T* host, size_t n, int* st) {
+  if (!host || n == 0) return nullptr;
+  T* d = (T*)mp_ws(ctx, slot, n * sizeof(T));
+  if (!d) { *st = MP_ERR_NOMEM; return nullptr; }
+  hipError_t e = hipMemcpyAsync(d, host, n * sizeof(T), hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) { *st = mp_fail(ctx, MP_ERR_HIP, "H2D copy failed: %s", hipGetErrorString(e)); return nullptr; }
+  return d;
+}
+template <typename T>
+static inline T* mp_alloc_out(mp_ctx* ctx, int slot, const T* host, size_t n, int* st) {
+  if (!host || n == 0) return nullptr;
+  T* d = (T*)mp_ws(ctx, slot, n * sizeof(T));
+  if (!d) *st = MP_ERR_NOMEM;
+  return d;
+}
+template <typename T>
+static inline int mp_download(mp_ctx* ctx, T* host, const T* dev, size_t n) {
+  if (!host || !dev || n == 0) return MP_OK;
+  MP_HIP(ctx, hipMemcpyAsync(host, dev, n * sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+  return MP_OK;
+}

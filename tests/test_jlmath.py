@@ -1,0 +1,47 @@
+"""include/mp_jlmath.h (FDLIBM restatement shared by device and oracle) vs glibc: <= 1 ulp."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle
+
+
+def _ulps(a, b):
+    a, b = np.float64(a), np.float64(b)
+    if a == b or (math.isnan(a) and math.isnan(b)):
+        return 0
+    return abs(int(np.array(a).view(np.int64)) - int(np.array(b).view(np.int64)))
+
+
+CASES = [
+    ("sin", math.sin, (-20, 20)), ("cos", math.cos, (-20, 20)), ("tan", math.tan, (-1.5, 1.5)),
+    ("atan", math.atan, (-50, 50)), ("asin", math.asin, (-1, 1)), ("acos", math.acos, (-1, 1)),
+    ("exp", math.exp, (-700, 700)), ("log", math.log, (1e-300, 1e3)),
+]
+
+
+@pytest.mark.parametrize("name,ref,rng", CASES)
+def test_accuracy(name, ref, rng):
+    r = np.random.default_rng(7)
+    xs = np.concatenate([r.uniform(*rng, 4000), r.uniform(-1, 1, 500) * min(1.0, rng[1]),
+                         np.array([0.0, 0.5, 0.4375, 0.6875, 1.1875, 2.4375]) if rng[0] <= 0 else np.array([1.0])])
+    xs = xs[(xs >= rng[0]) & (xs <= rng[1])]
+    worst = max(_ulps(oracle.m(name, float(x)), ref(float(x))) for x in xs)
+    assert worst <= 1, (name, worst)
+
+
+def test_atan2_quadrants():
+    r = np.random.default_rng(3)
+    for y, x in list(r.uniform(-5, 5, (2000, 2))) + [(0.0, -1.0), (-0.0, -1.0), (1.0, 0.0), (-1.0, 0.0), (2.0, 1.0)]:
+        assert _ulps(oracle.m("atan2", float(y), float(x)), math.atan2(y, x)) <= 1
+
+
+def test_modpi():
+    """modπ (ReedsSheppsUtils.jl:32-46) with Julia's mod (fmod + sign fix)."""
+    pi = math.pi
+    assert oracle.m("modpi", pi) == pi and oracle.m("modpi", -pi) == -pi
+    for a in np.linspace(-20, 20, 1001):
+        v = oracle.m("modpi", float(a))
+        assert -pi <= v <= pi
+        assert abs(math.remainder(v - a, 2 * pi)) < 1e-12
