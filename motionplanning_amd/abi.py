@@ -117,7 +117,7 @@ SIGNATURES = {
     "mp_mppi_plan": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), _I] + [_V] * 16),
     "mp_mppi_plan_dev": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), _I] + [_V] * 16),
     "mp_rollout": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), _I, _I, _V, _V, _V, ctypes.c_int64]
-                   + [_V] * 8),
+                   + [_V] * 7),
     "mp_vehicle_euler": (ctypes.c_int, [_V, _I, _V, _V, ctypes.c_double, _I, _V]),
     "mp_ilqr_rollout": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
     "mp_ilqr_backward": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),

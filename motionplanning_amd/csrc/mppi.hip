@@ -68,6 +68,7 @@ struct PlanArgs {
   int* fc_out;
   int nb;
   int pstride;
+  int lds_unom, lds_obs, lds_grid;  // offsets (in doubles) into dynamic LDS; lds_grid < 0: grid stays in HBM
 };
 
 __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
@@ -85,10 +86,33 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
 
   const double* X0 = A.X0 + 7 * s;
   const double* goal = A.goal + 2 * s;
-  const double* unom = A.unom + (size_t)H2 * s;
-  const double* obs = A.obs ? A.obs + (size_t)3 * P.n_obs * s : nullptr;
-  const unsigned char* grid = A.grid ? A.grid + (size_t)P.gnx * P.gny * s : nullptr;
   const double* noise = A.noise ? A.noise + (size_t)K * H2 * s : nullptr;
+  // Stage the scene's read-only inputs in LDS: the rollout loop then issues no
+  // global loads, so no s_waitcnt vmcnt ever waits on the (uncoalesced) stream
+  // of TrajectoryCollection stores (CDNA4 vmcnt counts stores too).
+  double* unom = dyn + A.lds_unom;
+  double* obs = A.obs ? dyn + A.lds_obs : nullptr;
+  const unsigned char* grid = nullptr;
+  {
+    const double* gu = A.unom + (size_t)H2 * s;
+    for (int i = tid; i < H2; i += NT) unom[i] = gu[i];
+    if (A.obs) {
+      const double* go = A.obs + (size_t)3 * P.n_obs * s;
+      for (int i = tid; i < 3 * P.n_obs; i += NT) obs[i] = go[i];
+    }
+    if (A.grid) {
+      const int gb = P.gnx * P.gny;
+      const unsigned char* gg = A.grid + (size_t)gb * s;
+      if (A.lds_grid >= 0) {
+        unsigned char* lg = reinterpret_cast<unsigned char*>(dyn + A.lds_grid);
+        for (int i = tid; i < gb; i += NT) lg[i] = gg[i];
+        grid = lg;
+      } else {
+        grid = gg;
+      }
+    }
+    __syncthreads();
+  }
   double* ctrl_k = A.ctrl_all + ((size_t)s * K + kk) * H2;
 
   // ---------------- phase 1: the rollout of this lane pair
@@ -156,7 +180,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   if (!sh_last) return;
 
   // ---------------- phase 2: combine + final rollout (last block of scene s)
-  double* Ush = dyn;          // [H2]
+  double* Ush = dyn;          // [H2]  (phase 1 is done with the staging area below)
   double* scale = dyn + H2;   // [nb]
   const double* partS = A.part + (size_t)s * A.nb * A.pstride;
   // FeasibilityCount prefix (MPPIUtils.jl:175): m = rollouts actually run
@@ -399,8 +423,20 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   A.rc_out = rc_out; A.fc_out = fc_out;
   A.nb = nb;
   A.pstride = pstride;
-  const size_t shmem = sizeof(double) * (size_t)(2 * H + nb);
-  MP_CHECK(ctx, shmem <= 60 * 1024, "K/H too large for one scene (dynamic LDS %zu B)", shmem);
+  // dynamic LDS: [phase-2 scratch: 2H + nb] [unom: 2H] [obs: 3 n_obs] [grid bytes]
+  int off = 2 * H + nb;
+  A.lds_unom = off;
+  off += 2 * H;
+  A.lds_obs = off;
+  off += 3 * D.n_obs;
+  const size_t gbytes = (size_t)D.gnx * D.gny;
+  A.lds_grid = -1;
+  if (D.gnx > 0 && (size_t)off * 8 + gbytes <= 48 * 1024) {
+    A.lds_grid = off;
+    off += (int)((gbytes + 7) / 8);
+  }
+  const size_t shmem = sizeof(double) * (size_t)off;
+  MP_CHECK(ctx, shmem <= 60 * 1024, "K/H/obstacles too large for one scene (dynamic LDS %zu B)", shmem);
   hipLaunchKernelGGL(mppi_plan_kernel, dim3(S * nb), dim3(NT), shmem, ctx->stream, D, A);
   MP_HIP(ctx, hipGetLastError());
   return MP_OK;
