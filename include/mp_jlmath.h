@@ -34,6 +34,7 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
 #define MPJ_FN __host__ __device__ static inline
 #else
 #define MPJ_FN static inline
@@ -531,6 +532,86 @@ MPJ_FN double mpj_log(double x) {
   }
   if (k == 0) return f - s * (f - R);
   return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+}
+
+
+/* ------------------------------------------------- branchless hot variants */
+/* Bit-identical to mpj_atan / mpj_sin / mpj_cos / mpj_sincos (checked on CPU in
+ * tests/test_jlmath.py and on the GPU in tests/test_gpu_mppi.py), written with
+ * selects instead of branches so a wavefront whose lanes fall in different
+ * argument ranges executes ONE instruction stream (no exec-mask serialisation)
+ * and independent chains can interleave.  Arguments outside the fast range take
+ * the exact branchy routine; on the device that fallback is wave-uniform. */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MPJ_ANY(c) __any((int)(c))
+#else
+#define MPJ_ANY(c) (c)
+#endif
+
+MPJ_FN double mpj_atan_bl(double x) {
+  const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+               aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+               aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+               aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+               aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+               aT10 = 1.62858201153657823623e-02;
+  const uint32_t hx = mpj_hi(x);
+  const uint32_t ix = hx & 0x7fffffffu;
+  if (MPJ_ANY(ix >= 0x44100000u)) return mpj_atan(x); /* |x| >= 2^66 or NaN */
+  const int small = ix < 0x3fdc0000u;
+  const int c0 = ix < 0x3fe60000u, c1 = ix < 0x3ff30000u, c2 = ix < 0x40038000u;
+  const double a = small ? x : mpj_fabs(x);
+  /* (na*a - nb) / (dc + dd*a): id -1 -> x/1, 0 -> (2x-1)/(2+x), 1 -> (x-1)/(1+x),
+   * 2 -> (x-1.5)/(1+1.5x), 3 -> -1/x */
+  const double na = small ? 1.0 : (c0 ? 2.0 : (c1 ? 1.0 : (c2 ? 1.0 : 0.0)));
+  const double nb = small ? 0.0 : (c0 ? 1.0 : (c1 ? 1.0 : (c2 ? 1.5 : 1.0)));
+  const double dc = small ? 1.0 : (c0 ? 2.0 : (c1 ? 1.0 : (c2 ? 1.0 : 0.0)));
+  const double dd = small ? 0.0 : (c0 ? 1.0 : (c1 ? 1.0 : (c2 ? 1.5 : 1.0)));
+  const double hi = small ? 0.0 : (c0 ? 4.63647609000806093515e-01 : (c1 ? 7.85398163397448278999e-01 :
+                    (c2 ? 9.82793723247329054082e-01 : 1.57079632679489655800e+00)));
+  const double lo = small ? 0.0 : (c0 ? 2.26987774529616870924e-17 : (c1 ? 3.06161699786838301793e-17 :
+                    (c2 ? 1.39033110312309984516e-17 : 6.12323399573676603587e-17)));
+  const double ax = (na * a - nb) / (dc + dd * a);
+  const double z = ax * ax;
+  const double w = z * z;
+  const double s1 = z * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT10, aT8), aT6), aT4), aT2), aT0);
+  const double s2 = w * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT9, aT7), aT5), aT3), aT1);
+  /* id -1: x - x*s == -((x*s - 0) - x) == hi - ((x*s - lo) - x) with hi = lo = 0 */
+  const double r = hi - ((ax * (s1 + s2) - lo) - ax);
+  const double rs = (!small && (hx >> 31)) ? -r : r;
+  return ix < 0x3e400000u ? x : rs;
+}
+
+/* sin and cos for |x| <= ~9π/4 without a branch (cw2c reduction, n in {0, ±1..±4}). */
+MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
+  const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
+  const double ax = mpj_fabs(x);
+  const int small = ax < MPJ_PIO4;
+  /* exact-path cases: |x| > ~9π/4, NaN/Inf, or the cwext points near kπ/2 (e_rem_pio2.c) */
+  const int ext = (xhp <= 0x400f6a7au && (xhp & 0xfffffu) == 0x921fbu) || xhp == 0x4012d97cu || xhp == 0x401921fbu;
+  if (MPJ_ANY(xhp > 0x401c463bu || (!small && ext))) {
+    mpj_sincos(x, so, co);
+    return;
+  }
+  const double fa = xhp <= 0x4002d97cu ? 1.0 : (xhp <= 0x400f6a7au ? 2.0 : (xhp <= 0x4015fdbcu ? 3.0 : 4.0));
+  const double fn = x > 0.0 ? fa : -fa;
+  double y0, y1;
+  mpj_cw2c(x, fn, 0, &y0, &y1);
+  const double sk = mpj_sin_k(y0, y1), ck = mpj_cos_k(y0, y1);
+  const double s0 = ax < MPJ_SQRT_EPS ? x : mpj_sin_k0(x);
+  const double c0 = ax < MPJ_SQRT_HALF_EPS ? 1.0 : mpj_cos_k(x, 0.0);
+  const int n = ((int)fn) & 3;
+  const double sr = n == 0 ? sk : (n == 1 ? ck : (n == 2 ? -sk : -ck));
+  const double cr = n == 0 ? ck : (n == 1 ? -sk : (n == 2 ? -ck : sk));
+  *so = small ? s0 : sr;
+  *co = small ? c0 : cr;
+}
+
+/* sin only, same fast range. */
+MPJ_FN double mpj_sin_bl(double x) {
+  double s, c;
+  mpj_sincos_bl(x, &s, &c);
+  return s;
 }
 
 /* ----------------------------------------------------------- Julia idioms */

@@ -40,14 +40,14 @@ __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, 
   // front: 2*(KFZF*g - t);  rear: 2*(KFZR*g + t)   (vehicledynamics.jl:30-31)
   const double FZ = 2 * ((side ? KFZR : KFZF) * g + (side ? t : -t));
   // front: (v + la*r) ... - sa;  rear: (v - lb*r) ... [(-lb)*r == -(lb*r) exactly]  (:32-33)
-  const double alpha = mpj_atan((v + (side ? -lb : la) * r) / (ux + 0.01)) - (side ? 0.0 : sa);
+  const double alpha = mpj_atan_bl((v + (side ? -lb : la) * r) / (ux + 0.01)) - (side ? 0.0 : sa);
   const double X1 = B * alpha;
-  const double FY = mu * FZ * 1.0 * mpj_sin(C * mpj_atan(X1 - E * (X1 - mpj_atan(X1))));  // (:35-38)
+  const double FY = mu * FZ * 1.0 * mpj_sin_bl(C * mpj_atan_bl(X1 - E * (X1 - mpj_atan_bl(X1))));  // (:35-38)
   const double FYo = __shfl_xor(FY, 1);
   const double FY1 = side ? FYo : FY, FY2 = side ? FY : FYo;
   const double uxc = ux <= 0 ? 0.0 : ux;  // (:40-42)
   double sp, cp;
-  mpj_sincos(psi, &sp, &cp);
+  mpj_sincos_bl(psi, &sp, &cp);
   d[0] = uxc * cp - v * sp;
   d[1] = uxc * sp + v * cp;
   d[2] = (FY1 + FY2) / M - r * uxc;
@@ -140,7 +140,7 @@ __device__ __forceinline__ void philox_normal2(const MppiDev& P, unsigned scene,
   const double u2 = ((double)b2 + 0.5) * 1.1102230246251565e-16;
   const double rr = mpj_sqrt(-2.0 * mpj_log(u1));
   double sn, cs;
-  mpj_sincos(MPJ_TWO_PI * u2, &sn, &cs);
+  mpj_sincos_bl(MPJ_TWO_PI * u2, &sn, &cs);
   z[0] = rr * cs;
   z[1] = rr * sn;
 }

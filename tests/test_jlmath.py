@@ -45,3 +45,20 @@ def test_modpi():
         v = oracle.m("modpi", float(a))
         assert -pi <= v <= pi
         assert abs(math.remainder(v - a, 2 * pi)) < 1e-12
+
+
+def test_branchless_variants_bitidentical():
+    """mpj_atan_bl / mpj_sincos_bl (used in the hot kernels) == the exact FDLIBM routines."""
+    r = np.random.default_rng(9)
+    xs = np.concatenate([r.uniform(-10, 10, 20000), r.uniform(-7.1, 7.1, 20000), r.uniform(-1e-7, 1e-7, 2000),
+                         np.pi / 2 * np.arange(-6, 7) + r.uniform(-1e-9, 1e-9, 13),
+                         np.array([0.0, -0.0, 0.4375, 0.6875, 1.1875, 2.4375, math.pi / 2, math.pi, 3.9, -3.9,
+                                   math.pi / 4, 2.356194490192345, 1e-9, 2e20, np.inf, -np.inf])])
+    for x in xs:
+        x = float(x)
+        a, b = oracle.m("atan_bl", x), oracle.m("atan", x)
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], ("atan", x)
+        if np.isfinite(x):
+            for fb, fe in (("sin_bl", "sin"), ("cos_bl", "cos")):
+                a, b = oracle.m(fb, x), oracle.m(fe, x)
+                assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], (fb, x)
