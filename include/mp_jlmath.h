@@ -539,13 +539,24 @@ MPJ_FN double mpj_log(double x) {
 /* Bit-identical to mpj_atan / mpj_sin / mpj_cos / mpj_sincos (checked on CPU in
  * tests/test_jlmath.py and on the GPU in tests/test_gpu_mppi.py), written with
  * selects instead of branches so a wavefront whose lanes fall in different
- * argument ranges executes ONE instruction stream (no exec-mask serialisation)
- * and independent chains can interleave.  Arguments outside the fast range take
- * the exact branchy routine; on the device that fallback is wave-uniform. */
+ * argument ranges executes ONE straight-line instruction stream (no exec-mask
+ * serialisation) and independent chains can be interleaved by the scheduler.
+ * On the device MPJ_SEL is a forced v_cndmask pair (hipcc otherwise re-forms
+ * branches from nested ternaries).  Arguments outside the fast range of sincos
+ * take the exact routine through a wave-uniform branch. */
 #if defined(__HIP_DEVICE_COMPILE__)
 #define MPJ_ANY(c) __any((int)(c))
+__device__ __forceinline__ double mpj_sel(int c, double t, double f) {
+  const unsigned long long m = __ballot(c);
+  unsigned rl, rh;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(rl) : "v"(__double2loint(f)), "v"(__double2loint(t)), "s"(m));
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(rh) : "v"(__double2hiint(f)), "v"(__double2hiint(t)), "s"(m));
+  return __hiloint2double((int)rh, (int)rl);
+}
+#define MPJ_SEL(c, t, f) mpj_sel((int)(c), (t), (f))
 #else
 #define MPJ_ANY(c) (c)
+#define MPJ_SEL(c, t, f) ((c) ? (t) : (f))
 #endif
 
 MPJ_FN double mpj_atan_bl(double x) {
@@ -557,32 +568,32 @@ MPJ_FN double mpj_atan_bl(double x) {
                aT10 = 1.62858201153657823623e-02;
   const uint32_t hx = mpj_hi(x);
   const uint32_t ix = hx & 0x7fffffffu;
-  if (MPJ_ANY(ix >= 0x44100000u)) return mpj_atan(x); /* |x| >= 2^66 or NaN */
-  const int small = ix < 0x3fdc0000u;
-  const int c0 = ix < 0x3fe60000u, c1 = ix < 0x3ff30000u, c2 = ix < 0x40038000u;
-  const double a = small ? x : mpj_fabs(x);
-  /* (na*a - nb) / (dc + dd*a): id -1 -> x/1, 0 -> (2x-1)/(2+x), 1 -> (x-1)/(1+x),
-   * 2 -> (x-1.5)/(1+1.5x), 3 -> -1/x */
-  const double na = small ? 1.0 : (c0 ? 2.0 : (c1 ? 1.0 : (c2 ? 1.0 : 0.0)));
-  const double nb = small ? 0.0 : (c0 ? 1.0 : (c1 ? 1.0 : (c2 ? 1.5 : 1.0)));
-  const double dc = small ? 1.0 : (c0 ? 2.0 : (c1 ? 1.0 : (c2 ? 1.0 : 0.0)));
-  const double dd = small ? 0.0 : (c0 ? 1.0 : (c1 ? 1.0 : (c2 ? 1.5 : 1.0)));
-  const double hi = small ? 0.0 : (c0 ? 4.63647609000806093515e-01 : (c1 ? 7.85398163397448278999e-01 :
-                    (c2 ? 9.82793723247329054082e-01 : 1.57079632679489655800e+00)));
-  const double lo = small ? 0.0 : (c0 ? 2.26987774529616870924e-17 : (c1 ? 3.06161699786838301793e-17 :
-                    (c2 ? 1.39033110312309984516e-17 : 6.12323399573676603587e-17)));
-  const double ax = (na * a - nb) / (dc + dd * a);
+  const int small = ix < 0x3fdc0000u, c0 = ix < 0x3fe60000u, c1 = ix < 0x3ff30000u, c2 = ix < 0x40038000u;
+  const int id2 = c2 && !c1;
+  /* (na*a - nb) / (na + nb*a): id -1 -> x/1, 0 -> (2x-1)/(2+x), 1 -> (x-1)/(1+x),
+   * 2 -> (x-1.5)/(1+1.5x), 3 -> -1/x == (0*x-1)/(0+1*x).  NaN propagates. */
+  const double a = MPJ_SEL(small, x, mpj_fabs(x));
+  const double na = MPJ_SEL(small, 1.0, MPJ_SEL(c0, 2.0, MPJ_SEL(c2, 1.0, 0.0)));
+  const double nb = MPJ_SEL(small, 0.0, MPJ_SEL(id2, 1.5, 1.0));
+  const double hi = MPJ_SEL(small, 0.0, MPJ_SEL(c0, 4.63647609000806093515e-01, MPJ_SEL(c1,
+                    7.85398163397448278999e-01, MPJ_SEL(c2, 9.82793723247329054082e-01, 1.57079632679489655800e+00))));
+  const double lo = MPJ_SEL(small, 0.0, MPJ_SEL(c0, 2.26987774529616870924e-17, MPJ_SEL(c1,
+                    3.06161699786838301793e-17, MPJ_SEL(c2, 1.39033110312309984516e-17, 6.12323399573676603587e-17))));
+  const double ax = (na * a - nb) / (na + nb * a);
   const double z = ax * ax;
   const double w = z * z;
   const double s1 = z * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT10, aT8), aT6), aT4), aT2), aT0);
   const double s2 = w * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT9, aT7), aT5), aT3), aT1);
   /* id -1: x - x*s == -((x*s - 0) - x) == hi - ((x*s - lo) - x) with hi = lo = 0 */
   const double r = hi - ((ax * (s1 + s2) - lo) - ax);
-  const double rs = (!small && (hx >> 31)) ? -r : r;
-  return ix < 0x3e400000u ? x : rs;
+  const double rs = MPJ_SEL(!small && (hx >> 31), -r, r);
+  /* |x| >= 2^66 (incl. ±Inf, where 0*Inf would be NaN): atanhi[3] + atanlo[3] */
+  const double big = 1.57079632679489655800e+00 + 6.12323399573676603587e-17;
+  const double rb = MPJ_SEL(ix >= 0x44100000u && x == x, MPJ_SEL(hx >> 31, -big, big), rs);
+  return MPJ_SEL(ix < 0x3e400000u, x, rb);
 }
 
-/* sin and cos for |x| <= ~9π/4 without a branch (cw2c reduction, n in {0, ±1..±4}). */
+/* sin and cos for |x| <= ~9π/4 without a divergent branch (cw2c reduction, n in {0, ±1..±4}). */
 MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
   const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
   const double ax = mpj_fabs(x);
@@ -593,18 +604,18 @@ MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
     mpj_sincos(x, so, co);
     return;
   }
-  const double fa = xhp <= 0x4002d97cu ? 1.0 : (xhp <= 0x400f6a7au ? 2.0 : (xhp <= 0x4015fdbcu ? 3.0 : 4.0));
-  const double fn = x > 0.0 ? fa : -fa;
+  const double fa = MPJ_SEL(xhp <= 0x4002d97cu, 1.0, MPJ_SEL(xhp <= 0x400f6a7au, 2.0, MPJ_SEL(xhp <= 0x4015fdbcu, 3.0, 4.0)));
+  const double fn = MPJ_SEL(x > 0.0, fa, -fa);
   double y0, y1;
   mpj_cw2c(x, fn, 0, &y0, &y1);
   const double sk = mpj_sin_k(y0, y1), ck = mpj_cos_k(y0, y1);
-  const double s0 = ax < MPJ_SQRT_EPS ? x : mpj_sin_k0(x);
-  const double c0 = ax < MPJ_SQRT_HALF_EPS ? 1.0 : mpj_cos_k(x, 0.0);
+  const double s0 = MPJ_SEL(ax < MPJ_SQRT_EPS, x, mpj_sin_k0(x));
+  const double c0 = MPJ_SEL(ax < MPJ_SQRT_HALF_EPS, 1.0, mpj_cos_k(x, 0.0));
   const int n = ((int)fn) & 3;
-  const double sr = n == 0 ? sk : (n == 1 ? ck : (n == 2 ? -sk : -ck));
-  const double cr = n == 0 ? ck : (n == 1 ? -sk : (n == 2 ? -ck : sk));
-  *so = small ? s0 : sr;
-  *co = small ? c0 : cr;
+  const double sr = MPJ_SEL(n == 0, sk, MPJ_SEL(n == 1, ck, MPJ_SEL(n == 2, -sk, -ck)));
+  const double cr = MPJ_SEL(n == 0, ck, MPJ_SEL(n == 1, -sk, MPJ_SEL(n == 2, -ck, sk)));
+  *so = MPJ_SEL(small, s0, sr);
+  *co = MPJ_SEL(small, c0, cr);
 }
 
 /* sin only, same fast range. */

@@ -71,6 +71,29 @@ struct PlanArgs {
   int lds_unom, lds_obs, lds_grid;  // offsets (in doubles) into dynamic LDS; lds_grid < 0: grid stays in HBM
 };
 
+// Noise for every (scene, step, rollout), h-major [S][H][K][2] so the rollout's
+// per-step read is one coalesced 16-B load per lane pair.  Philox draws are
+// generated here by the whole GPU (409,600 independent Box–Muller pairs at
+// cfg2) instead of sitting on the rollouts' serial per-step critical path;
+// MP_NOISE_EXTERNAL input [S][K][H][2] is transposed into the same layout.
+__global__ __launch_bounds__(256) void noise_prep_kernel(MppiDev P, int S, const double* ext, double* zh) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)S * P.H * P.K;
+  if (i >= n) return;
+  const int k = (int)(i % P.K);
+  const long long t = i / P.K;
+  const int h = (int)(t % P.H), s = (int)(t / P.H);
+  double z[2];
+  if (P.noise_mode == 0) {
+    const double2 e = *reinterpret_cast<const double2*>(ext + (((size_t)s * P.K + k) * P.H + h) * 2);
+    z[0] = e.x;
+    z[1] = e.y;
+  } else {
+    philox_normal2(P, (unsigned)s, (unsigned)k, (unsigned)h, z);
+  }
+  reinterpret_cast<double2*>(zh)[i] = make_double2(z[0], z[1]);
+}
+
 __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   __shared__ double sh_red[NT / 64];
   __shared__ double sh_e[RPB];
@@ -86,7 +109,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
 
   const double* X0 = A.X0 + 7 * s;
   const double* goal = A.goal + 2 * s;
-  const double* noise = A.noise ? A.noise + (size_t)K * H2 * s : nullptr;
+  const double* noise = A.noise + (size_t)K * H2 * s;  // h-major [H][K][2] (noise_prep_kernel)
   // Stage the scene's read-only inputs in LDS: the rollout loop then issues no
   // global loads, so no s_waitcnt vmcnt ever waits on the (uncoalesced) stream
   // of TrajectoryCollection stores (CDNA4 vmcnt counts stores too).
@@ -119,11 +142,18 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   int feas;
   double c;
   {
-    auto ctrl = [&](int j, double* u) { draw_ctrl(P, noise, unom, (unsigned)s, kk, j, u); };
-    auto store = [&](int j, const double* u) {
-      if (active) ctrl_k[2 * j + side] = u[side];
+    // z for step j+1 is loaded at the top of step j: the wait for it never covers
+    // the TrajectoryCollection stores issued later in the step.
+    const double2* zrow = reinterpret_cast<const double2*>(noise) + kk;
+    double2 zc = zrow[0];
+    auto ctrl = [&](int j, double* u) {
+      const double z[2] = {zc.x, zc.y};
+      if (j + 1 < H) zc = zrow[(size_t)(j + 1) * K];
+      sample_ctrl(P, z, unom + 2 * j, u);
     };
-    double* traj = (A.coll_traj && active) ? A.coll_traj + ((size_t)s * K + k) * (H + 1) * 7 : nullptr;
+    auto store = [&](int j, const double* u) { ctrl_k[2 * j + side] = u[side]; };
+    // inactive pairs (k >= K) recompute rollout K-1 and write identical values
+    double* traj = A.coll_traj ? A.coll_traj + ((size_t)s * K + kk) * (H + 1) * 7 : nullptr;
     c = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas);
   }
   if (active && side == 0) {
@@ -255,7 +285,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   {
     auto ctrl = [&](int j, double* u) { u[0] = Ush[2 * j]; u[1] = Ush[2 * j + 1]; };
     auto store = [&](int, const double*) {};
-    double* traj = (pair == 0) ? A.traj_out + (size_t)s * (H + 1) * 7 : nullptr;
+    double* traj = A.traj_out + (size_t)s * (H + 1) * 7;  // every pair writes the same values
     int f2;
     const double c2 = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &f2);
     if (tid == 0) {
@@ -408,7 +438,16 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   const int pstride = 4 + 2 * H;
   PlanArgs A;
   A.X0 = X0; A.goal = goal; A.unom = U_nom; A.obs = D.n_obs > 0 ? obstacles : nullptr;
-  A.grid = D.gnx > 0 ? grid : nullptr; A.noise = noise;
+  A.grid = D.gnx > 0 ? grid : nullptr;
+  double* zh = (double*)mp_ws(ctx, WS_NOISE, sizeof(double) * (size_t)S * K * H * 2);
+  if (!zh) return MP_ERR_NOMEM;
+  {
+    const long long n = (long long)S * K * H;
+    hipLaunchKernelGGL(noise_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, S, noise,
+                       zh);
+    MP_HIP(ctx, hipGetLastError());
+  }
+  A.noise = zh;
   A.ctrl_all = coll_ctrl ? coll_ctrl : (double*)mp_ws(ctx, WS_IO14, sizeof(double) * (size_t)S * K * 2 * H);
   A.cost_all = coll_cost ? coll_cost : (double*)mp_ws(ctx, WS_MPPI_COST, sizeof(double) * (size_t)S * K);
   A.feas_all = coll_feas ? coll_feas : (unsigned char*)mp_ws(ctx, WS_MPPI_FEAS, (size_t)S * K);

@@ -29,6 +29,14 @@ struct MppiDev {
   unsigned long long seed, offset;
 };
 
+// Exchange a double with the other lane of the pair: DPP quad_perm [1,0,3,2]
+// (one VALU op per 32-bit half, no LDS round trip as __shfl_xor would take).
+__device__ __forceinline__ double pair_swap(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
 // ---------------------------------------------------------------- dynamics
 // VehicleDynamics for a lane pair.  side = lane & 1 (0: front tire, 1: rear).
 __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side) {
@@ -43,9 +51,9 @@ __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, 
   const double alpha = mpj_atan_bl((v + (side ? -lb : la) * r) / (ux + 0.01)) - (side ? 0.0 : sa);
   const double X1 = B * alpha;
   const double FY = mu * FZ * 1.0 * mpj_sin_bl(C * mpj_atan_bl(X1 - E * (X1 - mpj_atan_bl(X1))));  // (:35-38)
-  const double FYo = __shfl_xor(FY, 1);
+  const double FYo = pair_swap(FY);
   const double FY1 = side ? FYo : FY, FY2 = side ? FY : FYo;
-  const double uxc = ux <= 0 ? 0.0 : ux;  // (:40-42)
+  const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);  // (:40-42)
   double sp, cp;
   mpj_sincos_bl(psi, &sp, &cp);
   d[0] = uxc * cp - v * sp;
@@ -63,44 +71,38 @@ __device__ __forceinline__ double run_cost(const double* x, double sr, double ax
   return v * v * 1 + 1 * (r * r) + 5 * (ax * ax) + 3 * (sr * sr) + 2 * (sa * sa) + 10 * (y * y);
 }
 
-// ObstacleEvaluation (MPPIUtils.jl:120-132) + occupancy grid (build extension)
+// ObstacleEvaluation (MPPIUtils.jl:120-132) + occupancy grid (build extension).
+// Branch-free: `c = hit ? c + pen : c` is bit-identical to `if (hit) c = c + pen`.
 __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* x, const double* obs,
                                                 const unsigned char* grid, int* ok) {
   double c = 0.0;
   for (int o = 0; o < P.n_obs; o++) {
     const double dx = x[0] - obs[3 * o], dy = x[1] - obs[3 * o + 1], R = obs[3 * o + 2];
-    if (dx * dx + dy * dy <= R * R) {
-      *ok = 0;
-      c = c + P.obs_pen;
-    }
+    const int hit = dx * dx + dy * dy <= R * R;
+    *ok &= !hit;
+    c = MPJ_SEL(hit, c + P.obs_pen, c);
   }
   if (P.gnx > 0) {
     const double fx = (x[0] - P.gx0) / P.gdx;
     const double fy = (x[1] - P.gy0) / P.gdy;
-    if (fx >= 0.0 && fy >= 0.0 && fx < (double)P.gnx && fy < (double)P.gny) {
-      const int ix = (int)fx, iy = (int)fy;
-      if (grid[iy * P.gnx + ix]) {
-        *ok = 0;
-        c = c + P.obs_pen;
-      }
-    }
+    const int inb = fx >= 0.0 && fy >= 0.0 && fx < (double)P.gnx && fy < (double)P.gny;
+    const int ix = inb ? (int)fx : 0, iy = inb ? (int)fy : 0;
+    const int hit = inb && grid[iy * P.gnx + ix];
+    *ok &= !hit;
+    c = MPJ_SEL(hit, c + P.obs_pen, c);
   }
   return c;
 }
 
-// BoundEvaluation, MPPIUtils.jl:135-151
+// BoundEvaluation, MPPIUtils.jl:135-151 (branch-free, same accumulation order)
 __device__ __forceinline__ double bound_cost(const MppiDev& P, const double* x, int* ok) {
   double c = 0.0;
 #pragma unroll
   for (int i = 0; i < 7; i++) {
-    if (x[i] < P.XL[i]) {
-      *ok = 0;
-      c = c + P.slack * __builtin_fabs(x[i] - P.XL[i]);
-    }
-    if (x[i] > P.XU[i]) {
-      *ok = 0;
-      c = c + P.slack * __builtin_fabs(x[i] - P.XU[i]);
-    }
+    const int lo = x[i] < P.XL[i], hi = x[i] > P.XU[i];
+    *ok &= !(lo | hi);
+    c = MPJ_SEL(lo, c + P.slack * __builtin_fabs(x[i] - P.XL[i]), c);
+    c = MPJ_SEL(hi, c + P.slack * __builtin_fabs(x[i] - P.XU[i]), c);
   }
   return c;
 }
@@ -167,10 +169,19 @@ __device__ __forceinline__ void draw_ctrl(const MppiDev& P, const double* noise_
   sample_ctrl(P, z, unom_s + 2 * h, u);
 }
 
+// A state row of 7 doubles written by the lane pair without divergence: the
+// even lane writes x[0..3] at [0..3], the odd lane x[3..6] at [3..6] (x[3]
+// is written twice with the same value).
+__device__ __forceinline__ void store_state(double* row, const double* x, int side) {
+  double* p = row + 3 * side;
+#pragma unroll
+  for (int i = 0; i < 4; i++) p[i] = MPJ_SEL(side, x[3 + i], x[i]);
+}
+
 // --------------------------------------------------------------- rollout
 // TrajectoryRollout for the lane pair (MPPIUtils.jl:31-57).  `ctrl(j, u)` yields the
-// control of step j.  traj (optional) gets (H+1)x7 states: the even lane stores
-// x[0..3], the odd lane x[4..6].  Returns cost_total; *feas = constraint.
+// control of step j.  traj (optional) gets (H+1)x7 states (store_state).
+// Returns cost_total; *feas = constraint.
 template <class CtrlFn, class StoreFn>
 __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X0, const double* goal,
                                                const double* obs, const unsigned char* grid,
@@ -179,10 +190,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
   double x[7];
 #pragma unroll
   for (int i = 0; i < 7; i++) x[i] = X0[i];
-  if (traj) {
-    if (side == 0) { for (int i = 0; i < 4; i++) traj[i] = x[i]; }
-    else { for (int i = 4; i < 7; i++) traj[i] = x[i]; }
-  }
+  if (traj) store_state(traj, x, side);
   double sum = 0.0;
   int ok_all = 1;
   for (int j = 0; j < P.H; j++) {
@@ -213,11 +221,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     }
     sum = sum + cj;
     ok_all &= okc & okb;
-    if (traj) {
-      double* t = traj + 7 * (j + 1);
-      if (side == 0) { for (int i = 0; i < 4; i++) t[i] = x[i]; }
-      else { for (int i = 4; i < 7; i++) t[i] = x[i]; }
-    }
+    if (traj) store_state(traj + 7 * (j + 1), x, side);
   }
   {  // terminal (:49-54): only the running cost of the extra RK2 step is used
     int okc = 1, okb = 1;

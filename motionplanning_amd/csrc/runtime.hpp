@@ -52,6 +52,7 @@ enum {
   WS_IO14,
   WS_IO15,
   WS_IO16,
+  WS_NOISE,
   WS_ILQR0,
   WS_ILQR1,
   WS_ILQR2,
