@@ -1,12 +1,15 @@
-"""MPPI rollout-step throughput on MI355X (BASELINE.json metric, configs[1]).
+"""MPPI rollout-step throughput on MI355X (BASELINE.json metric).
 
-One step = one MPPIPlan (OptimalControl/MPPI/src/MPPIUtils.jl:169-203) per scene at
-K=8192 rollouts, H=50 horizon steps, 7-state dynamic bicycle, 100x100 occupancy
-grid, device Philox noise, the full TrajectoryCollection (every rollout's
-trajectory and control list) written to HBM, weights + MPPICtrl + final rollout:
-ONE kernel launch (mp_mppi_plan_dev).  Inputs are resident in HBM before the timed
-region.  N>1: one process per GPU, each solves its own scene(s) (weak scaling) and
-the ranks all-gather the optimal controls over RCCL (the north star's exchange step).
+One step = one MPPIPlan (OptimalControl/MPPI/src/MPPIUtils.jl:169-203) for each of
+S scenes per GPU (default 8 = the per-GPU shard of configs[4], "64 scenes sharded
+8xMI355X"); every scene is configs[1]: K=8192 rollouts, H=50 horizon steps, 7-state
+dynamic bicycle, 100x100 occupancy grid, device Philox noise, the full
+TrajectoryCollection (every rollout's trajectory and control list) written to HBM,
+weights + MPPICtrl + final rollout.  Two launches per step (noise, plan).  Inputs
+are resident in HBM before the timed region.  N>1: one process per GPU, each
+solves its own S scenes (weak scaling) and the ranks all-gather the optimal
+controls over RCCL (the north star's exchange step).  The single-scene
+(configs[1] exactly, latency-bound) rate is reported beside it in "single_scene".
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scenes S] [--cpu-seconds T]
 """
@@ -34,40 +37,30 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scenes", type=int, default=1, help="scenes per GPU per step")
+    ap.add_argument("--scenes", type=int, default=8, help="scenes per GPU per step (configs[4] shard)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--rotate", type=int, default=12, help="output buffer sets rotated to defeat the 256 MB MALL")
+    ap.add_argument("--rotate", type=int, default=3, help="output buffer sets rotated (>256 MB MALL at S=8)")
+    ap.add_argument("--no-single", action="store_true", help="skip the single-scene (configs[1]) line")
     return ap.parse_args()
 
 
 def algorithmic_bytes(S, K, H):
-    """HBM bytes one launch must move (full TrajectoryCollection contract), see DESIGN.md §4."""
-    per_rollout = (H * 16  # control list written (types.jl:5)
-                   + (H + 1) * 56  # trajectory written (types.jl:4)
-                   + 8 + 1  # cost + feasibility
-                   + H * 16)  # control list read back for Σ w·u
+    """Compulsory HBM bytes of one mppi_plan_kernel launch: per rollout-step
+    16 B noise read + 16 B control written + 56 B state written; per rollout the initial
+    state row, cost and feasibility flag."""
+    per_rollout = H * (16 + 16 + 56) + 56 + 8 + 1
     return S * K * per_rollout
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-
+def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
+    """Time `steps` plan calls of S scenes; returns (elapsed_s_max, kernel_ms_mean, valid)."""
     from motionplanning_amd import configs
     from motionplanning_amd.abi import MP_NOISE_PHILOX, ptr
-    from motionplanning_amd.context import Context
 
-    ctx = Context(local)
     c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415 + rank)
     p = c["params"]
-    K, H, S = p.K, p.H, a.scenes
+    K, H = p.K, p.H
 
     def t(x, dt=torch.float64):
         return torch.as_tensor(np.ascontiguousarray(x), dtype=dt, device=dev).contiguous()
@@ -78,7 +71,7 @@ def main():
     dun = t(np.zeros((S, H, 2)))
     dgrid = t(np.tile(c["grid"], (S, 1, 1)), torch.uint8)
     sets = []
-    for _ in range(max(1, a.rotate)):
+    for _ in range(max(1, rotate)):
         sets.append(dict(
             U=torch.empty((S, H, 2), dtype=torch.float64, device=dev),
             traj=torch.empty((S, H + 1, 7), dtype=torch.float64, device=dev),
@@ -92,49 +85,63 @@ def main():
             cfeas=torch.empty((S, K), dtype=torch.uint8, device=dev),
         ))
     gathered = torch.empty((world * S, H, 2), dtype=torch.float64, device=dev)
-    stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
-    torch.cuda.set_stream(stream)  # RCCL all_gather is ordered after the plan kernel
 
-    ev = []
-
-    def step(i, timed):
+    def step(i):
         b = sets[i % len(sets)]
         p.offset = i
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
         ctx.check(ctx.lib.mp_mppi_plan_dev(
             ctx.handle, ctypes.byref(p), S, ptr(dX0), ptr(dgoal), ptr(dun), None, ptr(dgrid), None, ptr(b["U"]),
             ptr(b["traj"]), ptr(b["cost"]), ptr(b["feas"]), ptr(b["rc"]), ptr(b["fc"]), ptr(b["ctraj"]),
             ptr(b["cctrl"]), ptr(b["ccost"]), ptr(b["cfeas"])))
-        if timed:
-            e1.record(stream)
-            ev.append((e0, e1))
         if world > 1:
             dist.all_gather_into_tensor(gathered, b["U"])
 
-    for i in range(a.warmup):
-        step(i, False)
+    for i in range(warmup):
+        step(i)
     torch.cuda.synchronize()
+    ms, cnt = ctypes.c_double(), ctypes.c_int32()
+    ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))  # drop warmup events
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i, True)
+    for i in range(steps):
+        step(warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ev]))
+    ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+    kern_ms = ms.value / max(1, cnt.value)
+    ok = all(bool((b["rc"] == K + 1).all().item()) and bool(torch.isfinite(b["cost"]).all().item())
+             for b in sets[: min(len(sets), warmup + steps)])
     if world > 1:
-        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed, kern_ms, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(tt[0]), float(tt[1])
-    ok = bool((sets[0]["rc"] == K + 1).all().item()) and bool(torch.isfinite(sets[0]["cost"]).all().item())
+        elapsed, kern_ms, ok = float(tt[0]), float(tt[1]), tt[2].item() == 0.0
+    return elapsed, kern_ms, ok, K, H, p.feasibility_count
 
-    units = world * S * K * H * a.steps
-    value = units / elapsed
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from motionplanning_amd.context import Context
+
+    ctx = Context(local)
+    ctx.lib.mp_ctx_kernel_timing(ctx.handle, 1)
+    stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
+    torch.cuda.set_stream(stream)  # RCCL all_gather is ordered after the plan kernel
+
+    S = a.scenes
+    elapsed, kern_ms, ok, K, H, fc = run(a, S, ctx, dev, world, rank, a.steps, a.warmup, a.rotate)
+    value = world * S * K * H * a.steps / elapsed
     nbytes = algorithmic_bytes(S, K, H)
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
     out = {
@@ -151,9 +158,10 @@ def main():
         "dtype": "f64",
         "data": "synthetic (seeded Philox noise; cfg1 circles rasterised into a 100x100 grid)",
         "config": {
-            "workload": "configs[1]: MPPI K=8192 H=50 dynamic bicycle, 2-D occupancy-grid cost, full "
-                        "TrajectoryCollection, weights + MPPICtrl + final rollout",
-            "K": K, "H": H, "scenes_per_gpu": S, "feasibility_count": p.feasibility_count,
+            "workload": f"configs[4] per-GPU shard: {S} independent scenes per GPU, each configs[1] (MPPI K=8192 "
+                        "H=50 dynamic bicycle, 2-D occupancy-grid cost, full TrajectoryCollection, weights + "
+                        "MPPICtrl + final rollout)",
+            "K": K, "H": H, "scenes_per_gpu": S, "feasibility_count": fc,
             "parallelism": f"scene-sharded x{world}" + (" + RCCL all_gather(MPPICtrl)" if world > 1 else ""),
         },
         "roofline": {
@@ -163,6 +171,13 @@ def main():
         },
         "valid": ok,
     }
+    if not a.no_single and S != 1:
+        e1, k1, ok1, _, _, _ = run(a, 1, ctx, dev, world, rank, a.steps, a.warmup, 12)
+        out["single_scene"] = {
+            "workload": "configs[1] exactly: one scene per GPU per step (latency-bound serial chain)",
+            "value": world * K * H * a.steps / e1, "ms_per_step": e1 / a.steps * 1e3, "kernel_ms": k1,
+            "roofline_frac": algorithmic_bytes(1, K, H) / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS, "valid": ok1,
+        }
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     if rank == 0:

@@ -52,6 +52,12 @@ int mp_device_count(int* n);
 int mp_ctx_synchronize(mp_ctx* ctx);
 /* The hipStream_t the context launches on (for HIP-event timing). */
 void* mp_ctx_stream(mp_ctx* ctx);
+/* Kernel timing: when enabled, every launch of the dominant kernel of a call
+ * (mppi_plan_kernel, ...) is bracketed by HIP events on the context stream;
+ * mp_ctx_kernel_ms synchronises, returns the summed milliseconds and launch
+ * count since the last query, and resets them. */
+int mp_ctx_kernel_timing(mp_ctx* ctx, int enable);
+int mp_ctx_kernel_ms(mp_ctx* ctx, double* ms_sum, int32_t* count);
 
 /* ---------------------------------------------------------------- MPPI */
 #define MP_NX 7 /* [x, y, v, r, psi, ux, sa]  vehicledynamics.jl:20-26 */

@@ -14,12 +14,17 @@
 #include "mppi_device.hpp"
 #include "runtime.hpp"
 
+#include <cstdlib>
+#include <vector>
+
 using namespace mpk;
 
 namespace {
 
 constexpr int NT = 256;     // threads per block (4 waves)
 constexpr int RPB = NT / 2; // rollouts per block
+constexpr size_t kMaxLds = 150 * 1024;  // dynamic LDS budget per block (160 KiB per CU on gfx950)
+constexpr size_t kCoLds = 76 * 1024;    // budget that keeps two blocks co-resident per CU
 
 __device__ __forceinline__ double block_reduce_min(double v, double* sh) {
   for (int o = 32; o >= 1; o >>= 1) v = nanmin(v, __shfl_xor(v, o));
@@ -69,7 +74,14 @@ struct PlanArgs {
   int nb;
   int pstride;
   int lds_unom, lds_obs, lds_grid;  // offsets (in doubles) into dynamic LDS; lds_grid < 0: grid stays in HBM
+  int lds_ctrl, lds_part;           // control lists [RPB][2H+1] / staged partials (< 0: use HBM)
+  unsigned long long* stamps;       // diagnostic build only (MPGPU_STAMPS=1): [grid][8] s_memrealtime
 };
+
+#define MP_STAMP(i)                                                                  \
+  do {                                                                               \
+    if (A.stamps && threadIdx.x == 0) A.stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 
 // Noise for every (scene, step, rollout), h-major [S][H][K][2] so the rollout's
 // per-step read is one coalesced 16-B load per lane pair.  Philox draws are
@@ -98,23 +110,27 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   __shared__ double sh_red[NT / 64];
   __shared__ double sh_e[RPB];
   __shared__ double sh_q[2][128];
-  __shared__ int sh_last;
-  extern __shared__ double dyn[];  // H*2 (final MPPICtrl) + nb scales
+  __shared__ int sh_last, sh_m, sh_bstar, sh_fc;
+  __shared__ double sh_eta;
+  extern __shared__ double dyn[];
   const int H = P.H, H2 = 2 * H, K = P.K;
   const int s = blockIdx.x / A.nb, b = blockIdx.x % A.nb;
   const int tid = threadIdx.x, pair = tid >> 1, side = tid & 1;
   const int k = b * RPB + pair;
   const bool active = k < K;
   const int kk = active ? k : K - 1;
+  MP_STAMP(0);
 
   const double* X0 = A.X0 + 7 * s;
   const double* goal = A.goal + 2 * s;
   const double* noise = A.noise + (size_t)K * H2 * s;  // h-major [H][K][2] (noise_prep_kernel)
   // Stage the scene's read-only inputs in LDS: the rollout loop then issues no
-  // global loads, so no s_waitcnt vmcnt ever waits on the (uncoalesced) stream
-  // of TrajectoryCollection stores (CDNA4 vmcnt counts stores too).
+  // global loads but the prefetched noise, so no s_waitcnt vmcnt ever waits on
+  // the (uncoalesced) TrajectoryCollection stores (CDNA4 vmcnt counts stores).
   double* unom = dyn + A.lds_unom;
   double* obs = A.obs ? dyn + A.lds_obs : nullptr;
+  double* ush = A.lds_ctrl >= 0 ? dyn + A.lds_ctrl : nullptr;  // [RPB][H2+1] this block's control lists
+  const int ustr = H2 + 1;
   const unsigned char* grid = nullptr;
   {
     const double* gu = A.unom + (size_t)H2 * s;
@@ -136,7 +152,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     }
     __syncthreads();
   }
-  double* ctrl_k = A.ctrl_all + ((size_t)s * K + kk) * H2;
+  double* ctrl_g = A.ctrl_all ? A.ctrl_all + ((size_t)s * K + kk) * H2 : nullptr;
 
   // ---------------- phase 1: the rollout of this lane pair
   int feas;
@@ -151,11 +167,15 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       if (j + 1 < H) zc = zrow[(size_t)(j + 1) * K];
       sample_ctrl(P, z, unom + 2 * j, u);
     };
-    auto store = [&](int j, const double* u) { ctrl_k[2 * j + side] = u[side]; };
+    auto store = [&](int j, const double* u) {
+      if (ush) ush[pair * ustr + 2 * j + side] = u[side];
+      if (ctrl_g) ctrl_g[2 * j + side] = u[side];
+    };
     // inactive pairs (k >= K) recompute rollout K-1 and write identical values
     double* traj = A.coll_traj ? A.coll_traj + ((size_t)s * K + kk) * (H + 1) * 7 : nullptr;
     c = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas);
   }
+  MP_STAMP(1);
   if (active && side == 0) {
     A.cost_all[(size_t)s * K + k] = c;
     A.feas_all[(size_t)s * K + k] = (unsigned char)feas;
@@ -168,7 +188,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   if (side == 0) sh_e[pair] = e;
   const double eta_b = block_reduce_sum(side == 0 ? e : 0.0, sh_red);
   const double fc_b = block_reduce_sum((side == 0 && active && feas) ? 1.0 : 0.0, sh_red);
-  __syncthreads();  // ctrl_all stores of this block -> visible to its own loads below (same CU)
+  __syncthreads();  // control-list stores of this block -> visible to its own loads below (same CU)
   double* part = A.part + ((size_t)s * A.nb + b) * A.pstride;
   {
     // Σ_i e_i u_i[t] over this block's rollouts; two fixed halves per output, summed in order
@@ -178,9 +198,14 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       const int tt = t0 + t;
       double acc = 0.0;
       if (tt < H2) {
-        for (int r = r0; r < r1; r++) {
-          const int kr = b * RPB + r;
-          if (kr < K) acc = acc + sh_e[r] * A.ctrl_all[((size_t)s * K + kr) * H2 + tt];
+        if (ush) {
+          for (int r = r0; r < r1; r++) acc = acc + sh_e[r] * ush[r * ustr + tt];
+        } else {
+          // independent loads: issue 16 before consuming (L2 latency, not a serial chain)
+          const double* cb = A.ctrl_all + ((size_t)s * K + b * RPB) * H2 + tt;
+          const int rmax = min(r1, K - b * RPB);
+#pragma unroll 16
+          for (int r = r0; r < rmax; r++) acc = acc + sh_e[r] * cb[(size_t)r * H2];
         }
       }
       sh_q[q][t] = acc;
@@ -195,6 +220,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     part[2] = fc_b;
   }
   // ---------------- arrival: release (Guideline 16 recipe), ticket
+  MP_STAMP(2);
   __syncthreads();  // every wave's stores done (workgroup release waits vmcnt(0))
   if (tid == 0) {
     __threadfence();  // agent-scope release: write back this XCD's L2
@@ -207,14 +233,23 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     }
   }
   __syncthreads();
+  MP_STAMP(3);
   if (!sh_last) return;
 
   // ---------------- phase 2: combine + final rollout (last block of scene s)
-  double* Ush = dyn;          // [H2]  (phase 1 is done with the staging area below)
-  double* scale = dyn + H2;   // [nb]
-  const double* partS = A.part + (size_t)s * A.nb * A.pstride;
+  double* Ush = dyn;         // [H2]
+  double* scale = dyn + H2;  // [nb]
+  // every partial record of the scene, staged with independent coalesced loads
+  const double* partG = A.part + (size_t)s * A.nb * A.pstride;
+  const double* partS = partG;
+  if (A.lds_part >= 0) {
+    double* pl = dyn + A.lds_part;
+    const int n = A.nb * A.pstride;
+    for (int i = tid; i < n; i += NT) pl[i] = partG[i];
+    __syncthreads();
+    partS = pl;
+  }
   // FeasibilityCount prefix (MPPIUtils.jl:175): m = rollouts actually run
-  __shared__ int sh_m, sh_bstar, sh_fc;
   if (tid == 0) {
     int tot = 0;
     for (int i = 0; i < A.nb; i++) tot += (int)partS[(size_t)i * A.pstride + 2];
@@ -239,7 +274,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   }
   __syncthreads();
   const int m = sh_m, nfull = sh_bstar;  // blocks [0, nfull) complete; [nfull*RPB, m) partial
-  // partial boundary block, recomputed from the stored per-rollout costs / controls
+  // partial boundary block, recomputed from the stored costs and regenerated controls
   double rho_p = __builtin_inf(), eta_p = 0.0;
   const int p0 = nfull * RPB;
   const bool has_p = p0 < m;
@@ -261,7 +296,6 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   __syncthreads();
   const double scale_p = has_p ? mpj_exp(P.nil * (rho_p - rho)) : 0.0;
   // η and MPPICtrl = Σ_b scale_b Σ_i e_i u_i  /  η      (fixed order over blocks)
-  __shared__ double sh_eta;
   if (tid == 0) {
     double eta = 0.0;
     for (int i = 0; i < nfull; i++) eta = eta + partS[(size_t)i * A.pstride + 1] * scale[i];
@@ -270,17 +304,27 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   }
   __syncthreads();
   const double inv_eta = 1.0 / sh_eta;
+  const double* noiseS = A.noise + (size_t)K * H2 * s;
   for (int t = tid; t < H2; t += NT) {
     double acc = 0.0;
+#pragma unroll 8
     for (int i = 0; i < nfull; i++) acc = acc + partS[(size_t)i * A.pstride + 4 + t] * scale[i];
     if (has_p) {
       double ap = 0.0;
-      for (int r = 0; r < m - p0; r++) ap = ap + sh_e[r] * A.ctrl_all[((size_t)s * K + p0 + r) * H2 + t];
+      for (int r = 0; r < m - p0; r++) {
+        const int kr = p0 + r, h = t >> 1;
+        double u[2];
+        const double2 zz = reinterpret_cast<const double2*>(noiseS)[(size_t)h * K + kr];
+        const double z[2] = {zz.x, zz.y};
+        sample_ctrl(P, z, unom + 2 * h, u);
+        ap = ap + sh_e[r] * u[t & 1];
+      }
       acc = acc + ap * scale_p;
     }
     Ush[t] = acc * inv_eta;
   }
   __syncthreads();
+  MP_STAMP(4);
   // final TrajectoryRollout(MPPICtrl) — every pair runs it redundantly, pair 0 writes
   {
     auto ctrl = [&](int j, double* u) { u[0] = Ush[2 * j]; u[1] = Ush[2 * j + 1]; };
@@ -298,6 +342,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     }
   }
   for (int t = tid; t < H2; t += NT) A.U_out[(size_t)s * H2 + t] = Ush[t];
+  MP_STAMP(5);
 }
 
 // ------------------------------------------------------------- mp_rollout
@@ -448,11 +493,10 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     MP_HIP(ctx, hipGetLastError());
   }
   A.noise = zh;
-  A.ctrl_all = coll_ctrl ? coll_ctrl : (double*)mp_ws(ctx, WS_IO14, sizeof(double) * (size_t)S * K * 2 * H);
   A.cost_all = coll_cost ? coll_cost : (double*)mp_ws(ctx, WS_MPPI_COST, sizeof(double) * (size_t)S * K);
   A.feas_all = coll_feas ? coll_feas : (unsigned char*)mp_ws(ctx, WS_MPPI_FEAS, (size_t)S * K);
   A.part = (double*)mp_ws(ctx, WS_MPPI_PART, sizeof(double) * (size_t)S * nb * pstride);
-  if (!A.ctrl_all || !A.cost_all || !A.feas_all || !A.part) return MP_ERR_NOMEM;
+  if (!A.cost_all || !A.feas_all || !A.part) return MP_ERR_NOMEM;
   A.coll_traj = coll_traj;
   int st = mp_ticket_reserve(ctx, S);
   if (st) return st;
@@ -462,7 +506,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   A.rc_out = rc_out; A.fc_out = fc_out;
   A.nb = nb;
   A.pstride = pstride;
-  // dynamic LDS: [phase-2 scratch: 2H + nb] [unom: 2H] [obs: 3 n_obs] [grid bytes]
+  // dynamic LDS: [phase-2: 2H + nb] [unom: 2H] [obs: 3 n_obs] [grid bytes] [control lists | staged partials]
   int off = 2 * H + nb;
   A.lds_unom = off;
   off += 2 * H;
@@ -474,10 +518,67 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     A.lds_grid = off;
     off += (int)((gbytes + 7) / 8);
   }
+  // Control lists / staged partials in LDS only while two blocks still fit per CU
+  // (multi-scene launches need every block co-resident); otherwise the HBM path.
+  const int ctrl_words = RPB * (2 * H + 1), part_words = nb * pstride;
+  A.lds_ctrl = A.lds_part = -1;
+  const bool many = (size_t)S * nb > 256;
+  const size_t budget = many ? kCoLds : kMaxLds;
+  if ((size_t)(off + (ctrl_words > part_words ? ctrl_words : part_words)) * 8 <= budget) {
+    A.lds_ctrl = A.lds_part = off;
+    off += ctrl_words > part_words ? ctrl_words : part_words;
+  } else if ((size_t)(off + part_words) * 8 <= budget) {
+    A.lds_part = off;
+    off += part_words;
+  }
+  // control lists in HBM: the TrajectoryCollection output, or the fallback when LDS is too small
+  A.ctrl_all = coll_ctrl;
+  if (A.lds_ctrl < 0 && !A.ctrl_all) {
+    A.ctrl_all = (double*)mp_ws(ctx, WS_IO14, sizeof(double) * (size_t)S * K * 2 * H);
+    if (!A.ctrl_all) return MP_ERR_NOMEM;
+  }
   const size_t shmem = sizeof(double) * (size_t)off;
-  MP_CHECK(ctx, shmem <= 60 * 1024, "K/H/obstacles too large for one scene (dynamic LDS %zu B)", shmem);
+  MP_CHECK(ctx, shmem <= kMaxLds, "K/H/obstacles too large for one scene (dynamic LDS %zu B)", shmem);
+  static bool attr_set = false;
+  if (!attr_set) {
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kMaxLds));
+    attr_set = true;
+  }
+  A.stamps = nullptr;
+  static const bool stamps_on = getenv("MPGPU_STAMPS") != nullptr;
+  if (stamps_on) {
+    A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA2, sizeof(unsigned long long) * 8 * S * nb);
+    MP_HIP(ctx, hipMemsetAsync(A.stamps, 0, sizeof(unsigned long long) * 8 * S * nb, ctx->stream));
+  }
+  mp_time_begin(ctx);
   hipLaunchKernelGGL(mppi_plan_kernel, dim3(S * nb), dim3(NT), shmem, ctx->stream, D, A);
   MP_HIP(ctx, hipGetLastError());
+  mp_time_end(ctx);
+  if (stamps_on) {
+    std::vector<unsigned long long> h(8 * S * nb);
+    MP_HIP(ctx, hipMemcpyAsync(h.data(), A.stamps, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    unsigned long long t0 = ~0ull, end = 0;
+    double d01 = 0, d12 = 0, d23 = 0;
+    int last = -1;
+    for (int b = 0; b < S * nb; b++) {
+      const unsigned long long* q = &h[8 * b];
+      t0 = q[0] < t0 ? q[0] : t0;
+      d01 += (q[1] - q[0]) / 100.0; d12 += (q[2] - q[1]) / 100.0; d23 += (q[3] - q[2]) / 100.0;
+      if (q[5]) last = b;
+      end = q[5] > end ? q[5] : end;
+      end = q[3] > end ? q[3] : end;
+    }
+    fprintf(stderr, "[stamps us] blocks=%d mean rollout %.2f partial %.2f ticket %.2f", S * nb, d01 / (S * nb),
+            d12 / (S * nb), d23 / (S * nb));
+    if (last >= 0) {
+      const unsigned long long* q = &h[8 * last];
+      fprintf(stderr, " | last block: start+%.2f combine %.2f final-rollout %.2f | total %.2f", (q[0] - t0) / 100.0,
+              (q[4] - q[3]) / 100.0, (q[5] - q[4]) / 100.0, (end - t0) / 100.0);
+    }
+    fprintf(stderr, "\n");
+  }
   return MP_OK;
 }
 

@@ -66,7 +66,51 @@ void* mp_pinned(mp_ctx* ctx, size_t bytes) {
   return ctx->pinned;
 }
 
+static hipEvent_t next_event(mp_ctx* ctx) {
+  if (ctx->ev_used == ctx->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    ctx->ev_pool.push_back(e);
+  }
+  return ctx->ev_pool[ctx->ev_used++];
+}
+
+void mp_time_begin(mp_ctx* ctx) {
+  if (!ctx->timing) return;
+  hipEvent_t e = next_event(ctx);
+  if (e) hipEventRecord(e, ctx->stream);
+}
+
+void mp_time_end(mp_ctx* ctx) {
+  if (!ctx->timing) return;
+  hipEvent_t e = next_event(ctx);
+  if (e) hipEventRecord(e, ctx->stream);
+}
+
 extern "C" {
+
+int mp_ctx_kernel_timing(mp_ctx* ctx, int enable) {
+  if (!ctx) return MP_ERR_INVALID;
+  ctx->timing = enable != 0;
+  return MP_OK;
+}
+
+int mp_ctx_kernel_ms(mp_ctx* ctx, double* ms_sum, int32_t* count) {
+  if (!ctx || !ms_sum || !count) return MP_ERR_INVALID;
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  double t = 0.0;
+  int n = 0;
+  for (size_t i = 0; i + 1 < ctx->ev_used; i += 2) {
+    float ms = 0.f;
+    MP_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev_pool[i], ctx->ev_pool[i + 1]));
+    t += ms;
+    n++;
+  }
+  ctx->ev_used = 0;
+  *ms_sum = t;
+  *count = n;
+  return MP_OK;
+}
 
 const char* mp_version(void) { return MPGPU_VERSION " (gfx950)"; }
 
@@ -116,6 +160,7 @@ int mp_ctx_destroy(mp_ctx* ctx) {
   if (ctx->pinned) hipHostFree(ctx->pinned);
   if (ctx->tickets) hipFree(ctx->tickets);
   if (ctx->flags) hipFree(ctx->flags);
+  for (hipEvent_t e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->ha_states_candi) hipFree(ctx->ha_states_candi);
   if (ctx->ha_paths_candi) hipFree(ctx->ha_paths_candi);
   hipStreamDestroy(ctx->stream);

@@ -28,7 +28,15 @@ struct mp_ctx {
   unsigned int* tickets = nullptr;
   int n_tickets = 0;
   int* flags = nullptr;  // device status flags (NaN seen, ...)
+  // optional HIP-event timing of the dominant kernel
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
 };
+
+// Bracket a kernel launch with timing events when ctx->timing is on.
+void mp_time_begin(mp_ctx* ctx);
+void mp_time_end(mp_ctx* ctx);
 
 // workspace slots
 enum {
