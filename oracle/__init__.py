@@ -62,7 +62,7 @@ def lib():
         ]:
             if hasattr(L, name):
                 f = getattr(L, name)
-                f.restype = _D if name != "or_ilqr_solve" else ctypes.c_int
+                f.restype = {"or_ilqr_solve": ctypes.c_int, "or_ilqr_backward": ctypes.c_int}.get(name, _D)
                 f.argtypes = args
         _lib = L
     return _lib
@@ -148,3 +148,37 @@ def philox_normal2(seed, offset, scene, k, h):
     z = np.zeros(2)
     lib().or_philox_normal2(seed, offset, scene, k, h, ptr(z))
     return z
+
+
+# ----------------------------------------------------------------- iLQR
+def ilqr_rollout(p, x0, U):
+    x0 = np.ascontiguousarray(x0, np.float64)
+    U = np.ascontiguousarray(U, np.float64)
+    X = np.zeros((p.N, 4))
+    J = lib().or_ilqr_rollout(ctypes.byref(p), ptr(x0), ptr(U), ptr(X))
+    return X, J
+
+
+def ilqr_backward(p, X, U):
+    X = np.ascontiguousarray(X, np.float64)
+    U = np.ascontiguousarray(U, np.float64)
+    k = np.zeros((p.N - 1, 2))
+    K = np.zeros((p.N - 1, 4, 2))
+    lib().or_ilqr_backward(ctypes.byref(p), ptr(X), ptr(U), ptr(k), ptr(K))
+    return k, K
+
+
+def ilqr_forward(p, X, U, k, K, alpha):
+    X, U, k, K = (np.ascontiguousarray(a, np.float64) for a in (X, U, k, K))
+    Xn, Un = np.zeros_like(X), np.zeros_like(U)
+    J = lib().or_ilqr_forward(ctypes.byref(p), ptr(X), ptr(U), ptr(k), ptr(K), float(alpha), ptr(Xn), ptr(Un))
+    return Xn, Un, J
+
+
+def ilqr_solve(p, X, U):
+    X = np.array(X, np.float64)
+    U = np.array(U, np.float64)
+    J = ctypes.c_double()
+    it = ctypes.c_int32()
+    flags = lib().or_ilqr_solve(ctypes.byref(p), ptr(X), ptr(U), ctypes.byref(J), ctypes.byref(it))
+    return X, U, J.value, it.value, flags
