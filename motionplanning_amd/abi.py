@@ -123,7 +123,7 @@ SIGNATURES = {
     "mp_vehicle_euler": (ctypes.c_int, [_V, _I, _V, _V, ctypes.c_double, _I, _V]),
     "mp_ilqr_rollout": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
     "mp_ilqr_backward": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
-    "mp_ilqr_forward": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I] + [_V] * 9),
+    "mp_ilqr_forward": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I] + [_V] * 8),
     "mp_ilqr_solve": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
     "mp_ha_set_primitives": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _V, _V]),
     "mp_ha_expand": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I] + [_V] * 7),
