@@ -51,7 +51,10 @@ def test_solve_bitexact(ctx, variant, N, max_iter):
         assert it[b] == ito, (b, it[b], ito)
         assert J[b] == Jo and np.array_equal(X[b], Xo) and np.array_equal(U[b], Uo)
     if variant == ilqr.MP_ILQR_OPTIMALCONTROL:
-        assert ok and 10080 < J[0] < 10100  # x0 of ILQR.jl:12 (restatement value 10093.67)
+        # x0 of ILQR.jl:12 converges (restatement value 10093.67); other random instances may stall
+        # at a stationary point where the reference's unbounded halving would spin (max_ls flag),
+        # identically in the oracle (compared above).
+        assert 10080 < J[0] < 10100 and it[0] == 13
 
 
 def test_cfg3_full_size_one_pass(ctx):
