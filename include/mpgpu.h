@@ -198,6 +198,12 @@ typedef struct mp_ha_params {
   int32_t max_pops;                /* safety cap on search iterations            */
 } mp_ha_params;
 
+/* neighbor_origin (hybrid_astar_utils.jl:483-503) computed by the library (FDLIBM sin/cos,
+ * Euler Δt = 1e-2, n_col = floor(expand_time/Δt)), returned and installed in the context:
+ * states_candi[n_gear*n_steer][3], paths_candi[n_gear*n_steer][n_col][3]. */
+int mp_ha_neighbor_origin(mp_ctx* ctx, const mp_ha_params* p, int32_t n_steer, const double* steer_set,
+                          int32_t n_gear, const double* gear_set, double* states_candi, double* paths_candi);
+
 /* Primitive table of neighbor_origin (hybrid_astar_utils.jl:483-503):
  * states_candi[n_prim][3], paths_candi[n_prim][n_col][3]  (Julia 3×n_prim, 3×n_col×n_prim). */
 int mp_ha_set_primitives(mp_ctx* ctx, const mp_ha_params* p, const double* states_candi,

@@ -182,3 +182,97 @@ def ilqr_solve(p, X, U):
     it = ctypes.c_int32()
     flags = lib().or_ilqr_solve(ctypes.byref(p), ptr(X), ptr(U), ctypes.byref(J), ctypes.byref(it))
     return X, U, J.value, it.value, flags
+
+
+# ----------------------------------------------------------- Hybrid A*
+def _ha():
+    L = lib()
+    if not getattr(L, "_ha_ready", False):
+        P = ctypes.POINTER(HAParams)
+        L.or_ha_neighbor_origin.restype = ctypes.c_int
+        L.or_ha_neighbor_origin.argtypes = [_D, ctypes.c_int, _V, ctypes.c_int, _V, _V, _V]
+        L.or_ha_allpath.restype = ctypes.c_int
+        L.or_ha_allpath.argtypes = [_V, _V, _V]
+        L.or_ha_encode.restype = ctypes.c_int64
+        L.or_ha_encode.argtypes = [P, _V]
+        L.or_ha_regulate.restype = None
+        L.or_ha_regulate.argtypes = [P, _V, _V]
+        L.or_ha_block_free.restype = ctypes.c_int
+        L.or_ha_block_free.argtypes = [P, _V, ctypes.c_int, _V]
+        L.or_ha_convex_free.restype = ctypes.c_int
+        L.or_ha_convex_free.argtypes = [_V, _V]
+        L.or_ha_expand.restype = None
+        L.or_ha_expand.argtypes = [P] + [_V] * 9
+        L.or_ha_rs_connect.restype = ctypes.c_int
+        L.or_ha_rs_connect.argtypes = [P, _V, _V, _V, _V, _V]
+        L.or_ha_rs_heuristic.restype = _D
+        L.or_ha_rs_heuristic.argtypes = [P, _V, _V]
+        L.or_change_basis.restype = None
+        L.or_change_basis.argtypes = [_V, _V, _D, _V]
+        L.or_ha_plan.restype = ctypes.c_int
+        L.or_ha_plan.argtypes = [P] + [_V] * 12
+        L._ha_ready = True
+    return L
+
+
+def ha_neighbor_origin(T, steer_set, gear_set):
+    steer = np.ascontiguousarray(steer_set, np.float64)
+    gear = np.ascontiguousarray(gear_set, np.float64)
+    ncol = int(np.floor(T / 1e-2))
+    n = len(steer) * len(gear)
+    sc = np.zeros((n, 3))
+    pc = np.zeros((n, ncol, 3))
+    _ha().or_ha_neighbor_origin(T, len(steer), ptr(steer), len(gear), ptr(gear), ptr(sc), ptr(pc))
+    return sc, pc
+
+
+def ha_allpath(ns):
+    ns = np.ascontiguousarray(ns, np.float64)
+    cost = np.zeros(48)
+    cmds = np.zeros((48, 5, 3))
+    b = _ha().or_ha_allpath(ptr(ns), ptr(cost), ptr(cmds))
+    return b, cost, cmds
+
+
+def ha_encode(p, s):
+    return _ha().or_ha_encode(ctypes.byref(p), ptr(np.ascontiguousarray(s, np.float64)))
+
+
+def ha_block_free(p, path, walls):
+    path = np.ascontiguousarray(path, np.float64)
+    walls = np.ascontiguousarray(walls, np.float64)
+    return bool(_ha().or_ha_block_free(ctypes.byref(p), ptr(path), path.shape[0], ptr(walls)))
+
+
+def ha_convex_free(p1, p2):
+    return bool(_ha().or_ha_convex_free(ptr(np.ascontiguousarray(p1, np.float64)),
+                                        ptr(np.ascontiguousarray(p2, np.float64))))
+
+
+def ha_expand(p, node, goal, walls, sc, pc):
+    n = p.n_prim
+    nbs, idx, fr, h = np.zeros((n, 3)), np.zeros(n, np.int64), np.zeros(n, np.uint8), np.zeros(n)
+    args = [np.ascontiguousarray(a, np.float64) for a in (node, goal, walls, sc, pc)]
+    _ha().or_ha_expand(ctypes.byref(p), *[ptr(a) for a in args], ptr(nbs), ptr(idx), ptr(fr), ptr(h))
+    return nbs, idx, fr, h
+
+
+def ha_rs_connect(p, node, goal, walls):
+    path = np.zeros((501, 3))
+    ln = np.zeros(1, np.int32)
+    args = [np.ascontiguousarray(a, np.float64) for a in (node, goal, walls)]
+    ok = _ha().or_ha_rs_connect(ctypes.byref(p), *[ptr(a) for a in args], ptr(path), ptr(ln))
+    return bool(ok), path[: ln[0]]
+
+
+def ha_plan(p, start, goal, walls, sc, pc):
+    mp = p.max_pops
+    pops, nn, ns, rl = (np.zeros(1, np.int32) for _ in range(4))
+    seq = np.full(mp, -1, np.int64)
+    states = np.zeros((mp, 3))
+    rs = np.zeros((501, 3))
+    args = [np.ascontiguousarray(a, np.float64) for a in (start, goal, walls, sc, pc)]
+    found = _ha().or_ha_plan(ctypes.byref(p), *[ptr(a) for a in args], ptr(pops), ptr(nn), ptr(seq), ptr(ns),
+                             ptr(states), ptr(rl), ptr(rs))
+    return dict(found=bool(found), pops=int(pops[0]), n_nodes=int(nn[0]), pop_seq=seq[: pops[0]],
+                states=states[: ns[0]], rs_path=rs[: rl[0]])

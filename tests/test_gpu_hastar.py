@@ -1,0 +1,77 @@
+"""GPU parity for the Hybrid A* hot path (mp_ha_*) vs the CPU oracle — BIT-EXACT discrete
+outputs (Encode indices, collision booleans, heuristics, pop order, node counts, paths).
+Parity against Julia itself is unpinned (no reference artifact)."""
+import numpy as np
+import pytest
+
+import oracle
+from motionplanning_amd import hybrid_astar as ha
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(ctx, scene=ha.PERPENDICULAR):
+    h = ha.driver_searcher(scene)
+    p = ha.params_of(h)
+    sc, pc = ha.install_primitives(h, ctx)
+    sco, pco = oracle.ha_neighbor_origin(h.s.expand_time, h.s.steer_set, h.s.gear_set)
+    assert np.array_equal(sc, sco) and np.array_equal(pc, pco)
+    return h, p, sc, pc
+
+
+def test_expand_and_rs_connect_bitexact(ctx):
+    import ctypes
+
+    from motionplanning_amd.abi import ptr
+
+    h, p, sc, pc = _setup(ctx)
+    walls = np.array(h.s.obstacle_list)
+    r = np.random.default_rng(1)
+    B = 64
+    nodes = np.c_[r.choice(np.arange(-5, 10.01, 0.5), B), r.choice(np.arange(0, 10.01, 0.5), B),
+                  r.integers(-12, 13, B) * np.pi / 12]
+    goal = np.tile(h.s.ending_states, (B, 1))
+    W = np.tile(walls, (B, 1, 1))
+    nb, idx = np.zeros((B, 62, 3)), np.zeros((B, 62), np.int64)
+    fr, hh = np.zeros((B, 62), np.uint8), np.zeros((B, 62))
+    ctx.check(ctx.lib.mp_ha_expand(ctx.handle, ctypes.byref(p), B, ptr(nodes), ptr(goal), ptr(W), ptr(nb), ptr(idx),
+                                   ptr(fr), ptr(hh)))
+    ok, path, ln = np.zeros(B, np.uint8), np.zeros((B, 501, 3)), np.zeros(B, np.int32)
+    ctx.check(ctx.lib.mp_ha_rs_connect(ctx.handle, ctypes.byref(p), B, ptr(nodes), ptr(goal), ptr(W), ptr(ok),
+                                       ptr(path), ptr(ln)))
+    n_free = 0
+    for b in range(B):
+        nbo, idxo, fro, ho = oracle.ha_expand(p, nodes[b], goal[b], walls, sc, pc)
+        assert np.array_equal(nb[b], nbo) and np.array_equal(idx[b], idxo) and np.array_equal(fr[b], fro)
+        assert np.array_equal(hh[b][fro == 1], ho[fro == 1])
+        n_free += int(fro.sum())
+        oko, patho = oracle.ha_rs_connect(p, nodes[b], goal[b], walls)
+        assert bool(ok[b]) == oko and ln[b] == len(patho)
+        assert np.array_equal(path[b, : ln[b]], patho)
+    assert 0 < n_free < B * 62  # both branches exercised
+
+
+@pytest.mark.parametrize("scene,pops", [(ha.PERPENDICULAR, 275), (ha.PARALLEL, 120)])
+def test_driver_scene_plan_bitexact(ctx, scene, pops):
+    h, p, sc, pc = _setup(ctx, scene)
+    ha.planHybridAstar_(h, ctx=ctx)
+    ref = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+    assert h.r.found and ref["found"] and h.r.loop_count == ref["pops"] == pops
+    assert h.r.n_nodes == ref["n_nodes"]
+    assert np.array_equal(h.r.pop_sequence, ref["pop_seq"])  # expanded-node set, in pop order
+    assert np.array_equal(h.r.hybrid_astar_states.T, ref["states"])
+    assert np.array_equal(h.r.RSpath_final.T, ref["rs_path"])
+
+
+def test_scenario_batch_lockstep_bitexact(ctx):
+    """BASELINE cfg4 shape (perpendicular + parallel scenarios, seeded starts), 32 scenes in lockstep."""
+    hs = ha.scenario_batch(32, seed=4)
+    _, p, sc, pc = _setup(ctx)
+    ha.plan_batch(hs, ctx=ctx)
+    mism = 0
+    for h in hs:
+        ref = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+        same = (h.r.found == ref["found"] and h.r.loop_count == ref["pops"] and h.r.n_nodes == ref["n_nodes"]
+                and np.array_equal(h.r.pop_sequence, ref["pop_seq"]))
+        mism += not same
+    assert mism == 0

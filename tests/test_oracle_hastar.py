@@ -1,0 +1,80 @@
+"""Hybrid A* oracle (oracle/or_hastar.c): known answers derived from the reference text.
+
+No reference artifact exists for this path: the planner's discrete outputs are
+pinned GPU-vs-restatement bit-exactly (tests/test_gpu_hastar.py); here the restatement is
+checked against hand-derivable answers and the SURVEY's independent-restatement counts.
+"""
+import math
+
+import numpy as np
+
+import oracle
+from motionplanning_amd import hybrid_astar as ha
+
+
+def _rect(b):
+    ox, oy, psi, l, w = b
+    px = np.array([-l, -l, l, l, -l]); py = np.array([w, -w, -w, w, w])
+    c, s = math.cos(psi), math.sin(psi)
+    return np.c_[c * px - s * py + ox, s * px + c * py + oy]
+
+
+def test_collision_detection_demo():
+    """CollisionDetection/main.jl:7-19: the vehicle block beside wall 1 is collision free (prints `true`);
+    the small triangle inside wall 1 collides (`false`)."""
+    walls = ha.PERPENDICULAR["walls"]
+    veh = _rect([5.5, 1.0, 0.0, 1.5, 1.0])
+    assert oracle.ha_convex_free(_rect(walls[0]), veh)
+    cur, eps = (0.0, -1.0), 1e-1
+    tri = np.array([[cur[0], cur[1] + eps], [cur[0] - eps, cur[1]], [cur[0] + eps, cur[1]], [cur[0], cur[1] + eps],
+                    [cur[0], cur[1] + eps]])
+    assert not oracle.ha_convex_free(_rect(walls[0]), tri)
+
+
+def test_rs_straight_ahead():
+    """A goal d straight ahead: LSL with t = v = 0 and u = d is optimal, cost d."""
+    for d in (0.5, 1.0, 3.7):
+        b, cost, cmds = oracle.ha_allpath([d, 0.0, 0.0])
+        assert cost[b] == d
+        assert cmds[b, 1, 0] == d and cmds[b, 1, 2] == 0  # straight segment of length d
+
+
+def test_primitive_table_shape():
+    """neighbor_origin: 62 primitives x 250 columns."""
+    st = ha.driver_settings()
+    sc, pc = oracle.ha_neighbor_origin(2.5, st["steer_set"], st["gear_set"])
+    assert sc.shape == (62, 3) and pc.shape == (62, 250, 3)
+    assert np.array_equal(sc, pc[:, -1])
+    straight = 15  # steer 0 (middle of LinRange(-1/minR, 1/minR, 31)) forward
+    assert abs(sc[straight, 0] - 2.5) < 1e-12 and sc[straight, 1] == 0 and sc[straight, 2] == 0
+
+
+def test_encode_bijection():
+    """Encode over the regulated lattice is a bijection onto 1..31*21*25 (the idea of the
+    prototype's encode/decode round trip, backup_several_prototypes/.../unit_tests.jl:3-26)."""
+    h = ha.driver_searcher()
+    p = ha.params_of(h)
+    seen = set()
+    for x in np.arange(-5, 10.001, 0.5):
+        for y in np.arange(0, 10.001, 0.5):
+            for k in range(-12, 13):
+                s = ha.regulate_states(h.s.resolutions, [x, y, k * math.pi / 12])
+                seen.add(oracle.ha_encode(p, s))
+    assert seen == set(range(1, 31 * 21 * 25 + 1))  # 16,275 cells
+    assert oracle.ha_encode(p, [10.5, 0, 0]) == 0 and oracle.ha_encode(p, [0, -0.5, 0]) == 0
+
+
+def test_driver_scenes_match_survey_probe():
+    """main_hybrid_astar.jl scenes: 275 pops / 1,364 nodes (perpendicular), 120 pops (parallel) —
+    the counts an independent Python restatement reported in SURVEY §3.2."""
+    for scene, pops, nodes in ((ha.PERPENDICULAR, 275, 1364), (ha.PARALLEL, 120, None)):
+        h = ha.driver_searcher(scene)
+        p = ha.params_of(h)
+        sc, pc = oracle.ha_neighbor_origin(h.s.expand_time, h.s.steer_set, h.s.gear_set)
+        r = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+        assert r["found"] and r["pops"] == pops
+        if nodes:
+            assert r["n_nodes"] == nodes
+        # the path ends at the goal pose and starts at the popped node
+        assert np.abs(r["rs_path"][-1, :2] - h.s.ending_states[:2]).max() < 1e-2  # Euler, 100 steps/segment
+        assert np.array_equal(r["rs_path"][0], r["states"][0])
