@@ -20,10 +20,16 @@
 
 namespace {
 
-constexpr int NRS = 48;
 constexpr int MAXW = 16;    // walls per scene held in LDS
 constexpr int MAXPATH = 501;
 #define PI2 (MPJ_PI / 2)
+#ifdef HA_DEBUG
+// phase markers to host-mapped memory (tools/ha_dbg.cpp polls them while the kernel runs)
+__device__ int* g_ha_dbg;
+#define HMARK(ph) __hip_atomic_store(g_ha_dbg + (blockIdx.x * 64 + threadIdx.x), (ph), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+#else
+#define HMARK(ph)
+#endif
 
 struct HaDev {
   double L2, W2, minR, expand_time;
@@ -49,7 +55,7 @@ __device__ __forceinline__ double fin(double t, double u, double v, double cost)
 }
 
 // path1..path12 (ReedsSheppsUtils.jl:48-380); identical operation order to oracle/or_hastar.c
-__device__ double rs_path(int w, const double* s, Cmd* c) {
+__device__ __forceinline__ double rs_path(int w, const double* s, Cmd* c) {
   const double x = s[0], y = s[1], p = s[2];
   double rho, th, t, u, v, a, cost;
   c->n = 0;
@@ -189,50 +195,75 @@ __device__ double rs_path(int w, const double* s, Cmd* c) {
   }
 }
 
-// candidate `id` of allpath (word (id/4)+1, variant id%4: plain, timeflip, reflect, reverse)
-__device__ double rs_candidate(int id, const double* s, double* cm /* [5][3] or null */) {
-  const int w = id / 4 + 1, var = id % 4;
-  double q[3] = {s[0], s[1], s[2]};
-  if (var == 1) { q[0] = -q[0]; q[2] = -q[2]; }
-  else if (var == 2) { q[1] = -q[1]; q[2] = -q[2]; }
-  else if (var == 3) { q[0] = -q[0]; q[1] = -q[1]; }
-  Cmd c;
-  const double cost = rs_path(w, q, &c);
+// Julia findmin order on (cost, candidate id): NaN first (lowest id among NaNs), else the
+// smallest cost, ties to the lowest id.  A total order, so per-lane then cross-lane
+// reduction gives the same winner as allpath's sequential findmin.
+__device__ __forceinline__ bool rs_before(double a, int ia, double b, int ib) {
+  const bool an = a != a, bn = b != b;
+  if (an && bn) return ia < ib;
+  if (an) return true;
+  if (bn) return false;
+  return (a < b) || (a == b && ia < ib);
+}
+
+// allpath + findmin (ReedsSheppsUtils.jl:383-436, hybrid_astar_utils.jl rs_heuristic /
+// RS_connected).  The word loop is wave-uniform (no divergent 12-way switch): lane&3 is
+// the variant (plain, timeflip, reflect, reverse) of candidate id = 4(w-1)+variant.
+// Returns the winning cost in every lane; *best_id = winning id; if cm != nullptr the
+// winner's commands [5][3] (distance, gear, steer) are written to cm (LDS) by one lane.
+__device__ __forceinline__ void rs_variant(const double* s, int var, double* q) {
+  q[0] = s[0]; q[1] = s[1]; q[2] = s[2];
+  if (var == 1) { q[0] = -q[0]; q[2] = -q[2]; }       // timeflip
+  else if (var == 2) { q[1] = -q[1]; q[2] = -q[2]; }  // reflect
+  else if (var == 3) { q[0] = -q[0]; q[1] = -q[1]; }  // reverse
+}
+
+__device__ __forceinline__ double rs_best(const double* s, int lane, int* best_id, double* cm) {
+  double q[3];
+  rs_variant(s, lane & 3, q);
+  double bc = __builtin_inf();
+  int bi = 1 << 20;
+#pragma unroll 1
+  for (int w = 1; w <= 12; w++) {
+    Cmd c;
+    const double cost = rs_path(w, q, &c);
+    const int id = 4 * (w - 1) + (lane & 3);
+    if (rs_before(cost, id, bc, bi)) { bc = cost; bi = id; }
+  }
+#pragma unroll
+  for (int o = 2; o >= 1; o >>= 1) {  // lanes 4j..4j+3 hold identical copies of variants 0..3
+    const double ov = __shfl_xor(bc, o);
+    const int oi = __shfl_xor(bi, o);
+    if (rs_before(ov, oi, bc, bi)) { bc = ov; bi = oi; }
+  }
+  *best_id = bi;
   if (cm) {
-    for (int i = 0; i < 15; i++) cm[i] = 0.0;
-    if (cost < __builtin_inf()) {
-      for (int r = 0; r < c.n; r++) {
-        double ge = c.ge[r], st = c.st[r];
-        if (var == 1 || var == 3) ge = -1 * ge;
-        if (var == 2 || var == 3) st = -1 * st;
-        cm[r * 3 + 0] = c.tr[r];
+    // the winner's commands: re-evaluate its word (wave-uniform), apply the variant's
+    // gear / steer flips exactly as allpath does (-1 * x)
+    const int wv = bi & 3;
+    double qw[3];
+    rs_variant(s, wv, qw);
+    Cmd c;
+    const double cost = rs_path(bi / 4 + 1, qw, &c);
+    const int n = cost < __builtin_inf() ? c.n : 0;
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < 5; r++) {
+        double ge = 0.0, st = 0.0, tr = 0.0;
+        if (r < n) {
+          tr = c.tr[r];
+          ge = c.ge[r];
+          st = c.st[r];
+          if (wv == 1 || wv == 3) ge = -1 * ge;
+          if (wv == 2 || wv == 3) st = -1 * st;
+        }
+        cm[r * 3 + 0] = tr;
         cm[r * 3 + 1] = ge;
         cm[r * 3 + 2] = st;
       }
     }
   }
-  return cost;
-}
-
-// argmin over the 48 candidate costs held by lanes 0..47 (Julia findmin: first NaN, else
-// first minimum).  Returns the winning index in every lane.
-__device__ __forceinline__ int wave_argmin(double c, int lane) {
-  const int valid = lane < NRS;
-  double v = valid ? c : __builtin_inf();
-  int ix = valid ? lane : 1 << 20;
-  // key: NaN < everything; ties -> smaller index
-  for (int o = 32; o >= 1; o >>= 1) {
-    const double ov = __shfl_xor(v, o);
-    const int oi = __shfl_xor(ix, o);
-    const bool on = ov != ov, sn = v != v;
-    bool take;
-    if (on && sn) take = oi < ix;
-    else if (on) take = true;
-    else if (sn) take = false;
-    else take = (ov < v) || (ov == v && oi < ix);
-    if (take) { v = ov; ix = oi; }
-  }
-  return ix;
+  return bc;
 }
 
 __device__ __forceinline__ void change_basis(const double* init, const double* term, double minR, double* out) {
@@ -348,6 +379,7 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
   if (item > 0 && !A.do_exp) return;
   const int s = A.scene_of[slot];
   const int lane = threadIdx.x;
+  HMARK(1);
   const int nw = P.n_walls;
   const double* node = A.node + 3 * s;
   const double* goal = A.goal + 3 * s;
@@ -356,22 +388,24 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
     const double* wl = A.walls + ((size_t)s * nw + i) * 5;
     rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], wp + 10 * i);
   }
+  HMARK(5);
   __syncthreads();
+  HMARK(6);
   if (item == 0) {
     // ------------------------------------------------ RS_connected
     double ns[3];
     change_basis(node, goal, P.minR, ns);
-    double cm[15];
-    const double c = lane < NRS ? rs_candidate(lane, ns, cm) : __builtin_inf();
-    const int best = wave_argmin(c, lane);
-    if (lane == best)
-      for (int i = 0; i < 15; i++) cmd[i] = cm[i];
+    HMARK(7);
+    int best;
+    rs_best(ns, lane, &best, cmd);
+    HMARK(3);
     __syncthreads();
     int nseg = 0;
     for (int i = 0; i < 5; i++) {
       if (cmd[i * 3 + 1] == 0) break;
       nseg++;
     }
+    HMARK(4);
     double* path = A.rs_path + (size_t)s * MAXPATH * 3;
     double sx = node[0], sy = node[1], sp = node[2];
     if (lane == 0) { path_s[0] = sx; path_s[1] = sy; path_s[2] = sp; }
@@ -412,6 +446,7 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
       sx = __shfl(sx, 0);
       sy = __shfl(sy, 0);
       sp = psi_s[100];
+      HMARK(10 + seg);
       __syncthreads();
     }
     const int n = 100 * nseg + 1;
@@ -421,6 +456,7 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
     const int npose = n > 5 ? (n - 1) / 5 + 1 : 1;
     int freep = 1;
     for (int j = lane; j < npose; j += 64) freep &= pose_free(P, path_s + 3 * (j * 5), wp, nw);
+    HMARK(20);
     const int ok = !__any(!freep);
     if (lane == 0) {
       A.rs_ok[s] = (unsigned char)ok;
@@ -460,9 +496,8 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
   // rs_heuristic
   double ns[3];
   change_basis(nb, goal, P.minR, ns);
-  const double c = lane < NRS ? rs_candidate(lane, ns, nullptr) : __builtin_inf();
-  const int best = wave_argmin(c, lane);
-  const double cb = __shfl(c, best);
+  int best;
+  const double cb = rs_best(ns, lane, &best, nullptr);
   if (lane == 0) {
     A.fr[o] = 1;
     A.h[o] = cb * P.minR;
@@ -513,6 +548,13 @@ struct HNode {
 }  // namespace
 
 extern "C" {
+#ifdef HA_DEBUG
+int mp_ha_debug_buf(int* host_mapped) {
+  int* d = nullptr;
+  hipHostGetDevicePointer((void**)&d, host_mapped, 0);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ha_dbg), &d, sizeof d) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int mp_ha_set_primitives(mp_ctx* ctx, const mp_ha_params* p, const double* states_candi, const double* paths_candi) {
   if (!ctx) return MP_ERR_INVALID;

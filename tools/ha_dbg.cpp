@@ -1,0 +1,46 @@
+// Standalone Hybrid A* RS_connected driver for kernel debugging (build with -DHA_DEBUG).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <thread>
+#include <unistd.h>
+
+#include <hip/hip_runtime.h>
+
+#include "../include/mpgpu.h"
+extern "C" int mp_ha_debug_buf(int*);
+
+int main() {
+  mp_ctx* ctx = nullptr;
+  if (mp_ctx_create(0, &ctx)) { printf("ctx: %s\n", mp_last_error(nullptr)); return 1; }
+  mp_ha_params p;
+  memset(&p, 0, sizeof p);
+  p.vehicle_len = 3; p.vehicle_wid = 2; p.minR = 3 / std::tan(M_PI / 6); p.expand_time = 2.5;
+  p.res[0] = 0.5; p.res[1] = 0.5; p.res[2] = M_PI / 12;
+  double sb[6] = {-5, 10, 0, 10, -M_PI, M_PI};
+  memcpy(p.stbound, sb, sizeof sb);
+  p.n_walls = 3; p.n_prim = 62; p.n_col = 250; p.max_pops = 5000;
+  double node[3] = {7, 0, M_PI / 2}, goal[3] = {0, 0.5, M_PI / 2};
+  double walls[15] = {0, -1, 0, 5.5 / 2 + 1, 1, -5.5 / 2, 2.7432 / 2, 0, 1, 2.7432 / 2, 5.5 / 2, 2.7432 / 2, 0, 1, 2.7432 / 2};
+  unsigned char ok = 0;
+  static double path[501 * 3];
+  int len = 0;
+  int* buf = nullptr;
+  hipHostMalloc((void**)&buf, 64 * 64 * sizeof(int), hipHostMallocMapped);
+  memset(buf, 0, 64 * 64 * sizeof(int));
+  printf("dbg buf %d\n", mp_ha_debug_buf(buf));
+  printf("launch\n");
+  fflush(stdout);
+  int st = -99;
+  std::thread th([&] { st = mp_ha_rs_connect(ctx, &p, 1, node, goal, walls, &ok, path, &len); });
+  for (int t = 0; t < 20 && st == -99; t++) usleep(250000);
+  printf("block0 phases:");
+  for (int i = 0; i < 64; i++) printf(" %d", ((volatile int*)buf)[i]);
+  printf("\nst=%d\n", st);
+  fflush(stdout);
+  if (st == -99) _exit(3);
+  th.join();
+  printf("st %d ok %d len %d end %g %g %g\n", st, ok, len, path[3 * (len - 1)], path[3 * (len - 1) + 1], path[3 * (len - 1) + 2]);
+  mp_ctx_destroy(ctx);
+  return 0;
+}
