@@ -85,6 +85,10 @@ typedef struct mp_mppi_params {
   int32_t ctrl_cost;         /* 1: λ·u_nomᵀΣ⁻¹(u−u_nom) term (MPPIUtils.jl:45)  */
   uint64_t seed;             /* Philox key                                      */
   uint64_t offset;           /* Philox counter word (advance per solve)         */
+  int32_t scene_base;        /* global index of this call's scene 0 (Philox     */
+  int32_t reserved;          /*   counter word): a rank planning scenes [a,b)   */
+                             /*   of a sharded batch passes a, so every scene   */
+                             /*   draws the same stream at any world size       */
 } mp_mppi_params;
 
 /*

@@ -68,6 +68,8 @@ class MPPIParams(ctypes.Structure):
         ("ctrl_cost", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("offset", ctypes.c_uint64),
+        ("scene_base", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

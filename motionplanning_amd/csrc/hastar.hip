@@ -504,6 +504,54 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
   }
 }
 
+// allpath over B normalised states: 16 states per wave, lanes 4j..4j+3 = the four variants
+// of state j; the word loop is wave-uniform.  cost[B][48], cmds[B][48][5][3], best[B].
+__global__ __launch_bounds__(64) void allpath_kernel(int B, const double* __restrict__ ns, double* __restrict__ cost,
+                                                     double* __restrict__ cmds, int* __restrict__ best) {
+  const int lane = threadIdx.x, var = lane & 3;
+  const int b = blockIdx.x * 16 + (lane >> 2);
+  const bool live = b < B;
+  double s[3] = {0.0, 0.0, 0.0};
+  if (live) { s[0] = ns[3 * b]; s[1] = ns[3 * b + 1]; s[2] = ns[3 * b + 2]; }
+  double q[3];
+  rs_variant(s, var, q);
+  double bc = __builtin_inf();
+  int bi = 1 << 20;
+#pragma unroll 1
+  for (int w = 1; w <= 12; w++) {
+    Cmd c;
+    const double cst = rs_path(w, q, &c);
+    const int id = 4 * (w - 1) + var;
+    if (rs_before(cst, id, bc, bi)) { bc = cst; bi = id; }
+    if (live) {
+      cost[(size_t)b * 48 + id] = cst;
+      double* o = cmds + ((size_t)b * 48 + id) * 15;
+      const int n = cst < __builtin_inf() ? c.n : 0;
+#pragma unroll
+      for (int r = 0; r < 5; r++) {
+        double tr = 0.0, ge = 0.0, st = 0.0;
+        if (r < n) {
+          tr = c.tr[r];
+          ge = c.ge[r];
+          st = c.st[r];
+          if (var == 1 || var == 3) ge = -1 * ge;
+          if (var == 2 || var == 3) st = -1 * st;
+        }
+        o[3 * r] = tr;
+        o[3 * r + 1] = ge;
+        o[3 * r + 2] = st;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 2; o >= 1; o >>= 1) {
+    const double ov = __shfl_xor(bc, o);
+    const int oi = __shfl_xor(bi, o);
+    if (rs_before(ov, oi, bc, bi)) { bc = ov; bi = oi; }
+  }
+  if (live && var == 0) best[b] = bi;
+}
+
 // ---------------------------------------------------------------- host
 int make_ha(mp_ctx* ctx, const mp_ha_params* p, HaDev* D) {
   MP_CHECK(ctx, p != nullptr, "params is NULL");
@@ -674,9 +722,23 @@ int mp_ha_rs_connect(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double
 int mp_ha_allpath(mp_ctx* ctx, int32_t B, const double* norm_states, double* cost, double* cmds, int32_t* best) {
   if (!ctx) return MP_ERR_INVALID;
   MP_CHECK(ctx, B >= 1 && norm_states && cost && cmds && best, "bad arguments");
-  // allpath is evaluated inside the iteration kernel; this entry point serves the
-  // ReedsSheppsCurves demo surface (main.jl) on the host with the same FDLIBM math.
-  return mp_fail(ctx, MP_ERR_UNSUPPORTED, "mp_ha_allpath: use mp_ha_rs_connect / mp_ha_expand");
+  MP_HIP(ctx, hipSetDevice(ctx->device));
+  int st = MP_OK;
+  const double* dns = mp_upload(ctx, WS_IO0, norm_states, 3 * (size_t)B, &st);
+  double* dcost = mp_alloc_out(ctx, WS_IO1, cost, 48 * (size_t)B, &st);
+  double* dcmds = mp_alloc_out(ctx, WS_IO2, cmds, 48 * 15 * (size_t)B, &st);
+  int32_t* dbest = mp_alloc_out(ctx, WS_IO3, best, (size_t)B, &st);
+  if (st) return st;
+  mp_time_begin(ctx);
+  hipLaunchKernelGGL(allpath_kernel, dim3((unsigned)((B + 15) / 16)), dim3(64), 0, ctx->stream, B, dns, dcost, dcmds,
+                     (int*)dbest);
+  MP_HIP(ctx, hipGetLastError());
+  mp_time_end(ctx);
+  if ((st = mp_download(ctx, cost, (const double*)dcost, 48 * (size_t)B))) return st;
+  if ((st = mp_download(ctx, cmds, (const double*)dcmds, 48 * 15 * (size_t)B))) return st;
+  if ((st = mp_download(ctx, best, (const int32_t*)dbest, (size_t)B))) return st;
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MP_OK;
 }
 
 int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* start, const double* goal,

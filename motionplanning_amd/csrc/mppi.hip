@@ -470,6 +470,7 @@ static int make_dev_params(mp_ctx* ctx, const mp_mppi_params* p, int K, MppiDev*
   D->ctrl_cost = p->ctrl_cost;
   D->seed = p->seed;
   D->offset = p->offset;
+  D->scene_base = p->scene_base;
   return MP_OK;
 }
 

@@ -27,6 +27,7 @@ struct MppiDev {
   double gx0, gy0, gdx, gdy;
   int noise_mode, ctrl_cost;
   unsigned long long seed, offset;
+  int scene_base;
 };
 
 // Exchange a double with the other lane of the pair: DPP quad_perm [1,0,3,2]
@@ -134,7 +135,7 @@ __device__ __forceinline__ void philox4x32(unsigned c0, unsigned c1, unsigned c2
 __device__ __forceinline__ void philox_normal2(const MppiDev& P, unsigned scene, unsigned k, unsigned h,
                                                double* z) {
   unsigned o[4];
-  philox4x32(k, h, scene, (unsigned)P.offset, (unsigned)P.seed,
+  philox4x32(k, h, scene + (unsigned)P.scene_base, (unsigned)P.offset, (unsigned)P.seed,
              (unsigned)(P.seed >> 32) ^ (unsigned)(P.offset >> 32), o);
   const unsigned long long b1 = ((unsigned long long)(o[0] >> 5) << 26) | (unsigned long long)(o[1] >> 6);
   const unsigned long long b2 = ((unsigned long long)(o[2] >> 5) << 26) | (unsigned long long)(o[3] >> 6);

@@ -200,6 +200,28 @@ def planHybridAstar_(h, ctx=None, max_pops=5000):
     return None
 
 
+def changeBasis(init, term, minR):
+    """changeBasis, ReedsSheppsUtils.jl:2-11 (host arithmetic; the device does this inside
+    mp_ha_rs_connect / mp_ha_expand with the library's FDLIBM sin/cos)."""
+    dx, dy = (term[0] - init[0]) / minR, (term[1] - init[1]) / minR
+    c, s = math.cos(init[2]), math.sin(init[2])
+    return np.array([dx * c + dy * s, -dx * s + dy * c, term[2] - init[2]])
+
+
+def allpath(norm_states, ctx=None):
+    """allpath (ReedsSheppsUtils.jl:468-511) for B normalised states on the device.
+    Returns (best[B] 0-based candidate index, cost[B][48], cmds[B][48][5][3]) with cmds rows
+    [distance, gear, steer]; Inf cost (all-zero cmds) where a word is infeasible."""
+    ctx = ctx or default_context()
+    ns = f64(norm_states).reshape(-1, 3)
+    B = ns.shape[0]
+    cost = np.zeros((B, 48))
+    cmds = np.zeros((B, 48, 5, 3))
+    best = np.zeros(B, np.int32)
+    ctx.check(ctx.lib.mp_ha_allpath(ctx.handle, B, ptr(ns), ptr(cost), ptr(cmds), ptr(best)))
+    return best, cost, cmds
+
+
 # ----------------------------------------------------- driver scenes
 def driver_settings():
     """PathPlanning/HybridAstar/main_hybrid_astar.jl:21-29."""

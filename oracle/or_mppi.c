@@ -249,7 +249,7 @@ int or_mppi_plan(const mp_mppi_params* p, int scene, const double* X0, const dou
     for (int h = 0; h < H; h++) {
       double z[2];
       if (noise) { z[0] = noise[((size_t)m * H + h) * 2]; z[1] = noise[((size_t)m * H + h) * 2 + 1]; }
-      else or_philox_normal2(p->seed, p->offset, (uint32_t)scene, (uint32_t)m, (uint32_t)h, z);
+      else or_philox_normal2(p->seed, p->offset, (uint32_t)(scene + p->scene_base), (uint32_t)m, (uint32_t)h, z);
       sample_ctrl(p, L, unom + 2 * h, z, u + 2 * h);
     }
     int feas;
@@ -270,7 +270,7 @@ int or_mppi_plan(const mp_mppi_params* p, int scene, const double* X0, const dou
     for (int h = 0; h < H; h++) {
       double z[2];
       if (noise) { z[0] = noise[((size_t)i * H + h) * 2]; z[1] = noise[((size_t)i * H + h) * 2 + 1]; }
-      else or_philox_normal2(p->seed, p->offset, (uint32_t)scene, (uint32_t)i, (uint32_t)h, z);
+      else or_philox_normal2(p->seed, p->offset, (uint32_t)(scene + p->scene_base), (uint32_t)i, (uint32_t)h, z);
       sample_ctrl(p, L, unom + 2 * h, z, u + 2 * h);
     }
     int feas;

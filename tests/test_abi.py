@@ -27,7 +27,25 @@ def test_version_and_no_device_error():
     assert lib.mp_version().decode().startswith("0.1")
 
 
-def test_struct_sizes_match_header():
-    # natural alignment of the POD structs as laid out by the C compiler
-    assert abi.ctypes.sizeof(abi.MPPIParams) == 4 * 4 + 8 * 2 + 8 * 4 + 8 * 14 + 8 * 4 + 8 * 2 + 4 * 2 + 8 * 4 + 4 * 2 + 8 * 2
-    assert abi.ctypes.sizeof(abi.ILQRParams) == 4 * 2 + 8 * 4 + 4 * 2
+def test_struct_sizes_match_header(tmp_path):
+    """ctypes mirrors vs the C compiler's layout of include/mpgpu.h (sizeof + every offsetof)."""
+    import subprocess
+
+    structs = {"mp_mppi_params": abi.MPPIParams, "mp_ilqr_params": abi.ILQRParams, "mp_ha_params": abi.HAParams}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/mpgpu.h"', "int main(void){"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            cf = {"lambda_": "lambda"}.get(fname, fname)  # Python keyword
+            lines.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {cf}));')
+    lines.append("return 0;}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n") if l)
+    for cname, py in structs.items():
+        assert int(got[cname]) == abi.ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got[f"{cname}.{fname}"]) == getattr(py, fname).offset, (cname, fname)
+

@@ -75,3 +75,17 @@ def test_scenario_batch_lockstep_bitexact(ctx):
                 and np.array_equal(h.r.pop_sequence, ref["pop_seq"]))
         mism += not same
     assert mism == 0
+
+
+def test_allpath_bitexact(ctx):
+    """All 48 Reeds–Shepp candidates (cost + commands) and the findmin winner, vs the oracle."""
+    r = np.random.default_rng(7)
+    ns = np.r_[r.uniform(-4, 4, (509, 3)) * [1, 1, np.pi / 4],
+               [[2.0, 0.0, 0.0], [0.0, 0.0, 0.0], [1e-300, -0.0, 0.0], [3.0, 2.0, np.pi], [-3.0, -2.0, -np.pi]]]
+    best, cost, cmds = ha.allpath(ns, ctx=ctx)
+    for b in range(len(ns)):
+        bo, co, mo = oracle.ha_allpath(ns[b])
+        assert best[b] == bo
+        assert np.array_equal(cost[b], co)
+        assert np.array_equal(cmds[b], mo)
+    assert best[len(ns) - 5] == 0 and cost[len(ns) - 5, 0] == 2.0  # straight ahead: LSL, cost d
