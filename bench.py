@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--rotate", type=int, default=3, help="output buffer sets rotated (>256 MB MALL at S=8)")
     ap.add_argument("--no-single", action="store_true", help="skip the single-scene (configs[1]) line")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
+                    help="rocprofv3 PMC summary (tools/pmc_traffic.py) for roofline.traffic")
+    ap.add_argument("--no-extras", action="store_true", help="skip the iLQR (configs[2]) and Hybrid A* (configs[3]) lines")
     return ap.parse_args()
 
 
@@ -58,8 +61,9 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
     from motionplanning_amd import configs
     from motionplanning_amd.abi import MP_NOISE_PHILOX, ptr
 
-    c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415 + rank)
+    c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415)
     p = c["params"]
+    p.scene_base = rank * S  # global scene ids: rank r plans scenes [rS, (r+1)S) of the job
     K, H = p.K, p.H
 
     def t(x, dt=torch.float64):
@@ -171,6 +175,10 @@ def main():
         },
         "valid": ok,
     }
+    tr = load_traffic(a.traffic, S, K, H)
+    if tr is not None:
+        out["roofline"]["traffic"] = tr["traffic_bytes"]
+        out["roofline"]["traffic_source"] = tr["source"]
     if not a.no_single and S != 1:
         e1, k1, ok1, _, _, _ = run(a, 1, ctx, dev, world, rank, a.steps, a.warmup, 12)
         out["single_scene"] = {
@@ -178,12 +186,121 @@ def main():
             "value": world * K * H * a.steps / e1, "ms_per_step": e1 / a.steps * 1e3, "kernel_ms": k1,
             "roofline_frac": algorithmic_bytes(1, K, H) / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS, "valid": ok1,
         }
+    if not a.no_extras:
+        out["ilqr"] = bench_ilqr(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
+        out["hybrid_astar"] = bench_hastar(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def load_traffic(path, S, K, H):
+    """roofline.traffic: HBM bytes per mppi_plan_kernel launch from a rocprofv3 --pmc run of this
+    same bench command (FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected by tools/pmc_traffic.py);
+    used only if that run had the same S, K, H."""
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    e = d.get("mppi_plan_kernel", {})
+    if "traffic_bytes" not in e or d.get("config") != {"S": S, "K": K, "H": H}:
+        return None
+    return {"traffic_bytes": e["traffic_bytes"], "source": os.path.relpath(path, ROOT)}
+
+
+def _sync_max(x, world, dev):
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def bench_ilqr(ctx, world, rank, cpu=False, reps=5, B=4096, N=100):
+    """configs[2]: one backward Riccati sweep + one forward trial (alpha = 1) over B=4096
+    initial states x H=100 knots per GPU (weak scaling).  Unit: one instance-knot of
+    (backward + forward).  Host buffers in/out (the iLQR entry points take host arrays), so
+    the wall rate includes PCIe; kernel_rate uses the library's HIP-event kernel time."""
+    from motionplanning_amd import ilqr
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    p = ilqr.params(N=N)
+    x0, U = ilqr.cfg3_instances(B, N, seed=3 + rank)
+    X, J = ilqr.ilqr_rollout(p, x0, U, ctx=ctx)
+    ilqr.ilqr_forward(p, X, U, *ilqr.ilqr_backward(p, X, U, ctx=ctx), np.ones(B), ctx=ctx)  # warm-up
+    ms, cnt = ctypes.c_double(), ctypes.c_int32()
+    ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        k, K = ilqr.ilqr_backward(p, X, U, ctx=ctx)
+        Xn, Un, Jn = ilqr.ilqr_forward(p, X, U, k, K, np.ones(B), ctx=ctx)
+    el = _sync_max(time.perf_counter() - t0, world, dev)
+    ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+    kms = _sync_max(ms.value / reps, world, dev)
+    units = B * (N - 1)
+    out = {"metric": "iLQR instance-knots/s (backward Riccati + forward trial), H=100, 4096 instances per GPU",
+           "value": world * units * reps / el, "kernel_rate": world * units / (kms * 1e-3), "kernel_ms": kms,
+           "ms_per_pass": el / reps * 1e3, "dtype": "f64", "scaling": "weak", "valid": bool(np.isfinite(Jn).all()),
+           "bound": "valu-fp64 (FD derivatives: ~130 stage-cost + 48 dynamics evals per knot)"}
+    if cpu:
+        import oracle
+
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 3.0:
+            ko, Ko = oracle.ilqr_backward(p, X[n % B], U[n % B])
+            oracle.ilqr_forward(p, X[n % B], U[n % B], ko, Ko, 1.0)
+            n += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": n * (N - 1) / dt, "unit": "instance-knots/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} instances (backward + forward, H=100) in {dt:.1f} s, scalar C oracle"}
+    return out
+
+
+def bench_hastar(ctx, world, rank, cpu=False):
+    """configs[3]: planHybridAstar! for 256 parking scenarios (128 perpendicular + 128 parallel,
+    seeded starts), sharded across ranks (strong scaling), each rank a lockstep batch search
+    (one fused RS-connect + 62-neighbour expansion launch per iteration).  Unit: one node
+    expansion (pop: RS_connected + FindNewNode over 62 primitives).  Scenarios whose open
+    list empties (or that hit max_pops) end not-found exactly as the reference/oracle does;
+    "found" counts the rest (tests/test_gpu_hastar.py pins the outcomes to the oracle)."""
+    from motionplanning_amd import distributed as D
+    from motionplanning_amd import hybrid_astar as ha
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ha.plan_batch(ha.scenario_batch(4, seed=5), ctx=ctx)  # warm-up
+    hs = ha.scenario_batch(256, seed=4)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g = D.hybrid_astar_sharded(hs, ctx=ctx)
+    el = _sync_max(time.perf_counter() - t0, world, dev)
+    pops = int(g["pops"].sum())
+    out = {"metric": "Hybrid A* node expansions/s (RS_connected + 62-neighbour FindNewNode per pop), 256 scenarios",
+           "value": pops / el, "neighbour_evals_per_s": pops * 62 / el, "ms_total": el * 1e3,
+           "scenarios": len(hs), "found": int(g["found"].sum()), "total_pops": pops, "scaling": "strong",
+           "dtype": "f64", "valid": bool((g["pops"] > 0).all()),
+           "bound": "latency / host search loop (one launch + D2H per iteration)"}
+    if cpu:
+        import oracle
+
+        h0 = hs[0]
+        p = ha.params_of(h0)
+        sc, pc = oracle.ha_neighbor_origin(h0.s.expand_time, h0.s.steer_set, h0.s.gear_set)
+        n, cp, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < 3.0 and n < len(hs):
+            h = hs[n]
+            cp += oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc,
+                                 pc)["pops"]
+            n += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": cp / dt, "unit": "node expansions/s", "cores": 1, "kind": "port",
+                               "sample": f"{n} scenarios ({cp} pops) in {dt:.1f} s, scalar C oracle"}
+    return out
 
 
 def cpu_baseline(budget_s):

@@ -33,6 +33,15 @@ def initial_controls(B, N, u=U_INIT_REF):
     return U
 
 
+def cfg3_instances(B=4096, N=100, seed=3):
+    """BASELINE configs[2] / SURVEY §8d cfg3 initial states x0 = [U(-1,1), 3.6+U(-1,1), 5+U(-1,1),
+    U(-0.2,0.2)] (instance 0 = ILQR.jl:12's x0) and the ILQR.jl:33 initial guess."""
+    r = np.random.default_rng(seed)
+    x0 = np.c_[r.uniform(-1, 1, B), 3.6 + r.uniform(-1, 1, B), 5 + r.uniform(-1, 1, B), r.uniform(-0.2, 0.2, B)]
+    x0[0] = X0_REF
+    return x0, initial_controls(B, N)
+
+
 def ilqr_rollout(p, x0, U, ctx=None):
     ctx = ctx or default_context()
     x0 = f64(x0).reshape(-1, 4)

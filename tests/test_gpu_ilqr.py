@@ -15,11 +15,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _instances(B, N, seed=3):
-    """BASELINE.md cfg3 initial states: x0 = [U(-1,1), 3.6+U(-1,1), 5+U(-1,1), U(-0.2,0.2)]."""
-    r = np.random.default_rng(seed)
-    x0 = np.c_[r.uniform(-1, 1, B), 3.6 + r.uniform(-1, 1, B), 5 + r.uniform(-1, 1, B), r.uniform(-0.2, 0.2, B)]
-    x0[0] = ilqr.X0_REF
-    return x0, ilqr.initial_controls(B, N)
+    return ilqr.cfg3_instances(B, N, seed)
 
 
 @pytest.mark.parametrize("variant,N", [(ilqr.MP_ILQR_OPTIMALCONTROL, 20), (ilqr.MP_ILQR_PARKING, 30)])
