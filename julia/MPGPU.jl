@@ -1,0 +1,341 @@
+"""
+    MPGPU
+
+Julia binding of libmpgpu.so (include/mpgpu.h) for the reference's planner scripts.
+`include("MPGPU.jl")` after the reference's own `include("src/...")` lines and the
+hot-path functions below take over the reference's names on the same searcher objects:
+
+  * `MPPIPlan(mppi::MPPISearcher)`      OptimalControl/MPPI/src/MPPIUtils.jl:169-203
+  * `TrajectoryRollout(mppi, ctrl)`     MPPIUtils.jl:31-57 (batched form: `rollout_batch`)
+  * `planHybridAstar!(ha)`              PathPlanning/HybridAstar/src/hybrid_astar_utils.jl:235-296
+  * `RS_connected`, `FindNewNode` device parts (`ha_rs_connect`, `ha_expand`)
+  * iLQR passes (`ilqr_backward!`, `ilqr_forward!`, `ilqr_solve!`)  OptimalControl/ILQR/ILQR.jl:44-88
+
+Errors: every non-zero status is re-raised as `error(mp_last_error(ctx))`, the style of
+the reference's own validation (MPPI/src/setup.jl:19-38).  Arrays are passed in Julia's
+native column-major layout; each call documents the Julia shape (the C header writes the
+same buffer in reversed, row-major order).
+
+This file cannot be executed in the build container (no Julia toolchain); the same entry
+points are exercised from Python ctypes by tests/ with identical layouts.
+"""
+module MPGPU
+
+export MPPIPlan, planHybridAstar!, mppi_plan_batch, rollout_batch, ha_expand, ha_rs_connect,
+       ha_allpath, ilqr_backward!, ilqr_forward!, ilqr_solve!
+
+const libmpgpu = get(ENV, "MPGPU_LIB", joinpath(@__DIR__, "..", "motionplanning_amd", "lib", "libmpgpu.so"))
+
+const MP_OK = Cint(0)
+const MP_ERR_NUMERIC = Cint(4)
+const MP_NOISE_EXTERNAL = Int32(0)
+const MP_NOISE_PHILOX = Int32(1)
+
+# ------------------------------------------------------------------ context
+const CTX = Ref{Ptr{Cvoid}}(C_NULL)
+
+last_error(c::Ptr{Cvoid}) = unsafe_string(ccall((:mp_last_error, libmpgpu), Cstring, (Ptr{Cvoid},), c))
+
+function check(st::Cint, c::Ptr{Cvoid} = CTX[])
+    st == MP_OK || error("libmpgpu: ", last_error(c))
+    return nothing
+end
+
+"""One context (device + HIP stream + cached workspaces) per process; device = LOCAL_RANK."""
+function ctx(device::Integer = parse(Int, get(ENV, "LOCAL_RANK", "0")))
+    if CTX[] == C_NULL
+        r = Ref{Ptr{Cvoid}}(C_NULL)
+        st = ccall((:mp_ctx_create, libmpgpu), Cint, (Cint, Ref{Ptr{Cvoid}}), device, r)
+        st == MP_OK || error("libmpgpu: ", last_error(Ptr{Cvoid}(C_NULL)))
+        CTX[] = r[]
+        atexit(() -> (ccall((:mp_ctx_destroy, libmpgpu), Cint, (Ptr{Cvoid},), CTX[]); CTX[] = C_NULL))
+    end
+    return CTX[]
+end
+
+# --------------------------------------------------------------------- MPPI
+"""mp_mppi_params, field for field (isbits => C layout)."""
+struct MppiParams
+    K::Int32
+    H::Int32
+    feasibility_count::Int32
+    n_obs::Int32
+    dt::Float64
+    lambda::Float64
+    sigma::NTuple{4,Float64}      # Σ row-major
+    XL::NTuple{7,Float64}
+    XU::NTuple{7,Float64}
+    CL::NTuple{2,Float64}
+    CU::NTuple{2,Float64}
+    slack_penalty::Float64
+    obs_penalty::Float64
+    grid_nx::Int32
+    grid_ny::Int32
+    grid_x0::Float64
+    grid_y0::Float64
+    grid_dx::Float64
+    grid_dy::Float64
+    noise_mode::Int32
+    ctrl_cost::Int32
+    seed::UInt64
+    offset::UInt64
+    scene_base::Int32
+    reserved::Int32
+end
+
+"""MppiParams from an MPPISearcher's settings (MPPI/src/types.jl:10-31, setup.jl:3-59)."""
+function params(mppi; noise_mode = MP_NOISE_PHILOX, seed = 0, offset = 0, grid = nothing)
+    s = mppi.s
+    Σ = Matrix{Float64}(s.Σ)
+    nx, ny, x0, y0, dx, dy = 0, 0, 0.0, 0.0, 0.0, 0.0
+    if grid !== nothing            # (occupancy::Matrix{UInt8} (nx, ny), x0, y0, dx, dy) — build extension
+        occ, x0, y0, dx, dy = grid
+        nx, ny = size(occ)
+    end
+    MppiParams(s.SamplingNumber, s.N, s.FeasibilityCount, length(s.obstacle_list), s.dt, s.lambda,
+               (Σ[1, 1], Σ[1, 2], Σ[2, 1], Σ[2, 2]), Tuple(s.XL), Tuple(s.XU), Tuple(s.CL), Tuple(s.CU),
+               s.SlackPenalty, 100 * 712.5, nx, ny, x0, y0, dx, dy, noise_mode, 1, seed, offset, 0, 0)
+end
+
+"""
+    mppi_plan_batch(p, X0, goal, Unom; obstacles, grid, noise, collect) -> NamedTuple
+
+S scenes in one launch.  Julia shapes: X0 (7, S), goal (2, S), Unom (2, H, S),
+obstacles (3, n_obs, S), grid occupancy (nx, ny, S) UInt8, noise z (2, H, K, S) or
+`nothing` (device Philox).  Returns U (2, H, S), traj (7, H+1, S), cost, feasible,
+rollout_count, feasible_count (S,) and, with `collect`, the TrajectoryCollection arrays
+coll_traj (7, H+1, K, S), coll_ctrl (2, H, K, S), coll_cost (K, S), coll_feas (K, S).
+"""
+function mppi_plan_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Float64}, Unom::Array{Float64,3};
+                         obstacles = nothing, grid = nothing, noise = nothing, collect::Bool = false)
+    S = size(X0, 2); H = Int(p.H); K = Int(p.K)
+    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 25)...)
+    U = zeros(2, H, S); traj = zeros(7, H + 1, S); cost = zeros(S)
+    feas = zeros(Int32, S); rc = zeros(Int32, S); fc = zeros(Int32, S)
+    ct = collect ? zeros(7, H + 1, K, S) : nothing
+    cc = collect ? zeros(2, H, K, S) : nothing
+    ck = collect ? zeros(K, S) : nothing
+    cf = collect ? zeros(UInt8, K, S) : nothing
+    nz(a) = a === nothing ? C_NULL : pointer(a)
+    c = ctx()
+    st = GC.@preserve X0 goal Unom obstacles grid noise U traj cost feas rc fc ct cc ck cf begin
+        ccall((:mp_mppi_plan, libmpgpu), Cint,
+              (Ptr{Cvoid}, Ref{MppiParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+               Ptr{UInt8}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32},
+               Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}),
+              c, p, S, X0, goal, Unom, nz(obstacles), nz(grid), nz(noise), U, traj, cost, feas, rc, fc,
+              nz(ct), nz(cc), nz(ck), nz(cf))
+    end
+    st == MP_ERR_NUMERIC && @warn "MPPIPlan: NaN rollout cost (outputs written)"
+    st == MP_ERR_NUMERIC || check(st, c)
+    return (; U, traj, cost, feasible = feas, rollout_count = rc, feasible_count = fc,
+            coll_traj = ct, coll_ctrl = cc, coll_cost = ck, coll_feas = cf)
+end
+
+const SOLVES = Ref{UInt64}(0)   # per-process solve counter = Philox counter word
+
+"""
+    MPPIPlan(mppi; noise = nothing, seed = 0, collect = true)
+
+Drop-in for MPPIUtils.jl:169-203: mutates `mppi.r.{Traj, Control, Feasibility, cost, time,
+FeasibleTrajCount, RolloutCount}` and `mppi.p.TrajectoryCollection[1:m]`.  `noise` is the
+caller's z (2, N, SamplingNumber) (the draws the reference takes from `MvNormal`); by
+default the device Philox stream keyed by `seed` and a per-call counter is used.
+"""
+function MPPIPlan(mppi; noise = nothing, seed = 0, collect::Bool = true)
+    t1 = time()
+    s = mppi.s
+    p = params(mppi; seed = seed, offset = SOLVES[])
+    SOLVES[] += 1
+    obs = isempty(s.obstacle_list) ? nothing : reshape(reduce(hcat, s.obstacle_list), 3, :, 1)
+    Unom = reshape(permutedims(Matrix{Float64}(s.NominalControl)), 2, s.N, 1)   # N×2 -> (2, N, 1)
+    z = noise === nothing ? nothing : reshape(noise, 2, s.N, s.SamplingNumber, 1)
+    r = mppi_plan_batch(p, reshape(s.X0, 7, 1), reshape(s.goal, 2, 1), Unom; obstacles = obs, noise = z,
+                        collect = collect)
+    mppi.r.Control = permutedims(r.U[:, :, 1])          # N×2
+    mppi.r.Traj = permutedims(r.traj[:, :, 1])          # (N+1)×7
+    mppi.r.Feasibility = r.feasible[1] == 1 ? :Feasible : :InFeasible
+    mppi.r.cost = r.cost[1]
+    mppi.r.RolloutCount = r.rollout_count[1]
+    mppi.r.FeasibleTrajCount = r.feasible_count[1]
+    if collect
+        m = r.rollout_count[1] - 1
+        hold = eltype(mppi.p.TrajectoryCollection)
+        mppi.p.TrajectoryCollection = [hold(permutedims(r.coll_traj[:, :, k, 1]), permutedims(r.coll_ctrl[:, :, k, 1]),
+                                            r.coll_feas[k, 1] == 1, r.coll_cost[k, 1]) for k in 1:m]
+    end
+    mppi.r.time = time() - t1
+    return nothing
+end
+
+"""
+    rollout_batch(p, X0 (7,S), goal (2,S), ctrl (2,H,K,S); Unom, obstacles) -> (traj, cost, feas, argmin)
+
+Batched TrajectoryRollout (MPPIUtils.jl:31-57, DWAUtils.jl:16-42) with given controls.
+"""
+function rollout_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Float64}, ctrl::Array{Float64,4};
+                       Unom = nothing, obstacles = nothing)
+    _, H, K, S = size(ctrl)
+    traj = zeros(7, H + 1, K, S); cost = zeros(K, S); feas = zeros(UInt8, K, S); am = zeros(Int32, S)
+    nz(a) = a === nothing ? C_NULL : pointer(a)
+    c = ctx()
+    st = GC.@preserve X0 goal ctrl Unom obstacles traj cost feas am ccall((:mp_rollout, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{MppiParams}, Int32, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Ptr{Float64},
+         Ptr{Float64}, Ptr{UInt8}, Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Ptr{Int32}),
+        c, p, S, K, X0, goal, ctrl, 2, nz(Unom), nz(obstacles), C_NULL, traj, cost, feas, am)
+    check(st, c)
+    return traj, cost, feas, am .+ 1     # 1-based argmin
+end
+
+# ---------------------------------------------------------------- Hybrid A*
+struct HaParams
+    vehicle_len::Float64
+    vehicle_wid::Float64
+    minR::Float64
+    expand_time::Float64
+    res::NTuple{3,Float64}
+    stbound::NTuple{6,Float64}
+    n_walls::Int32
+    n_prim::Int32
+    n_col::Int32
+    max_pops::Int32
+end
+
+function ha_params(ha; max_pops = 5000)
+    s = ha.s
+    sb = s.stbound                       # 3×2 [min max] per state (setup.jl:27-33)
+    HaParams(s.vehicle_size[1], s.vehicle_size[2], s.minR, s.expand_time, Tuple(s.resolutions),
+             (sb[1, 1], sb[1, 2], sb[2, 1], sb[2, 2], sb[3, 1], sb[3, 2]), length(s.obstacle_list),
+             s.num_neighbors, size(s.paths_candi, 2), max_pops)
+end
+
+"""Install the searcher's own neighbor_origin table (states_candi 3×n, paths_candi 3×n_col×n):
+the device transforms Julia-computed bits (SURVEY §8c)."""
+function ha_install!(ha, p::HaParams)
+    sc = Matrix{Float64}(ha.s.states_candi); pc = Array{Float64,3}(ha.s.paths_candi)
+    c = ctx()
+    check(GC.@preserve sc pc ccall((:mp_ha_set_primitives, libmpgpu), Cint,
+                                   (Ptr{Cvoid}, Ref{HaParams}, Ptr{Float64}, Ptr{Float64}), c, p, sc, pc), c)
+end
+
+walls_of(ha) = reshape(reduce(hcat, ha.s.obstacle_list), 5, :)
+
+"""
+    planHybridAstar!(ha)
+
+Drop-in for hybrid_astar_utils.jl:235-296 (one scenario; `plan_batch!` for many).  Fills
+`ha.r.hybrid_astar_states` (3×n, goal-side first, as the reference's hcat loop),
+`ha.r.RSpath_final` (3×len), `ha.p.loop_count` and `ha.r.planning_time`, then calls the
+reference's own `retrievePath(ha)` when a path was found.
+"""
+planHybridAstar!(ha; retrieve = nothing) = (plan_batch!([ha]; retrieve = retrieve); nothing)
+
+function plan_batch!(has::AbstractVector; retrieve = nothing, max_pops = 5000)
+    t1 = time()
+    h0 = has[1]
+    p = ha_params(h0; max_pops = max_pops)
+    ha_install!(h0, p)
+    B = length(has)
+    start = reduce(hcat, [h.s.starting_states for h in has]); goal = reduce(hcat, [h.s.ending_states for h in has])
+    walls = reshape(reduce(hcat, [walls_of(h) for h in has]), 5, Int(p.n_walls), B)
+    found = zeros(Int32, B); pops = zeros(Int32, B); nn = zeros(Int32, B)
+    seq = fill(Int64(-1), max_pops, B); ns = zeros(Int32, B); states = zeros(3, max_pops, B)
+    rl = zeros(Int32, B); rs = zeros(3, 501, B)
+    c = ctx()
+    st = GC.@preserve start goal walls found pops nn seq ns states rl rs ccall((:mp_ha_plan, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{HaParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32},
+         Ptr{Int32}, Ptr{Int64}, Ptr{Int32}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}),
+        c, p, B, start, goal, walls, found, pops, nn, seq, ns, states, rl, rs)
+    check(st, c)
+    dt = time() - t1
+    for (b, h) in enumerate(has)
+        h.p.loop_count = pops[b]
+        h.r.planning_time = dt
+        if found[b] == 1
+            h.r.hybrid_astar_states = states[:, 1:ns[b], b]
+            h.r.RSpath_final = rs[:, 1:rl[b], b]
+            retrieve === nothing || retrieve(h)     # e.g. Main.retrievePath
+        end
+    end
+    return (; found, pops, n_nodes = nn, pop_sequence = seq)
+end
+
+"""Batched FindNewNode device part for B popped nodes (3, B): neighbour states (3, n, B),
+Encode indices (n, B) (0 = out of bounds), collision-free flags (n, B), rs heuristics (n, B)."""
+function ha_expand(p::HaParams, node::Matrix{Float64}, goal::Matrix{Float64}, walls::Array{Float64,3})
+    B = size(node, 2); n = Int(p.n_prim)
+    nb = zeros(3, n, B); idx = zeros(Int64, n, B); fr = zeros(UInt8, n, B); h = zeros(n, B)
+    c = ctx()
+    check(GC.@preserve node goal walls nb idx fr h ccall((:mp_ha_expand, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{HaParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int64},
+         Ptr{UInt8}, Ptr{Float64}), c, p, B, node, goal, walls, nb, idx, fr, h), c)
+    return nb, idx, fr, h
+end
+
+"""Batched RS_connected: (ok (B,), paths (3, 501, B), lengths (B,))."""
+function ha_rs_connect(p::HaParams, node::Matrix{Float64}, goal::Matrix{Float64}, walls::Array{Float64,3})
+    B = size(node, 2)
+    ok = zeros(UInt8, B); path = zeros(3, 501, B); len = zeros(Int32, B)
+    c = ctx()
+    check(GC.@preserve node goal walls ok path len ccall((:mp_ha_rs_connect, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{HaParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{UInt8}, Ptr{Float64},
+         Ptr{Int32}), c, p, B, node, goal, walls, ok, path, len), c)
+    return ok, path, len
+end
+
+"""allpath (ReedsSheppsUtils.jl:468-511) for normalised states (3, B): best (1-based), cost (48, B),
+cmds (3, 5, 48, B) (rows [distance, gear, steer] of each command)."""
+function ha_allpath(ns::Matrix{Float64})
+    B = size(ns, 2)
+    cost = zeros(48, B); cmds = zeros(3, 5, 48, B); best = zeros(Int32, B)
+    c = ctx()
+    check(GC.@preserve ns cost cmds best ccall((:mp_ha_allpath, libmpgpu), Cint,
+        (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}), c, B, ns, cost, cmds, best), c)
+    return best .+ 1, cost, cmds
+end
+
+# --------------------------------------------------------------------- iLQR
+struct IlqrParams
+    N::Int32
+    variant::Int32        # 0 OptimalControl/ILQR/Cost.jl, 1 PathPlanning/Parking_ILQR/Cost.jl
+    dT::Float64
+    eps::Float64
+    alpha_floor::Float64
+    tol::Float64
+    max_iter::Int32
+    max_ls::Int32
+end
+IlqrParams(N; variant = 0, dT = 0.05, eps = 1e-3, tol = 1e-6, max_iter = 1000, max_ls = 200) =
+    IlqrParams(N, variant, dT, eps, variant == 1 ? 1e-3 : 0.0, tol, max_iter, max_ls)
+
+"""One backward Riccati sweep (ILQR.jl:46-67) for B instances: X (4, N, B), U (2, N, B)
+-> k (2, N-1, B), K (2, 4, N-1, B) (the reference's klist / Klist per instance)."""
+function ilqr_backward!(k, K, p::IlqrParams, X, U)
+    B = size(X, 3); c = ctx()
+    check(GC.@preserve X U k K ccall((:mp_ilqr_backward, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{IlqrParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+        c, p, B, X, U, k, K), c)
+    return k, K
+end
+
+"""One forward trial at step sizes α (B,) (ILQR.jl:72-80) -> (Xnew, Unew, Jnew)."""
+function ilqr_forward!(Xn, Un, Jn, p::IlqrParams, X, U, k, K, α)
+    B = size(X, 3); c = ctx()
+    check(GC.@preserve X U k K α Xn Un Jn ccall((:mp_ilqr_forward, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{IlqrParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+         Ptr{Float64}, Ptr{Float64}, Ptr{Float64}), c, p, B, X, U, k, K, α, Xn, Un, Jn), c)
+    return Xn, Un, Jn
+end
+
+"""The whole ILQR.jl:39-88 loop per instance, in place on X (4, N, B), U (2, N, B)."""
+function ilqr_solve!(X, U, p::IlqrParams)
+    B = size(X, 3); J = zeros(B); it = zeros(Int32, B); c = ctx()
+    st = GC.@preserve X U J it ccall((:mp_ilqr_solve, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{IlqrParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+        c, p, B, X, U, J, it)
+    st == MP_ERR_NUMERIC && @warn "iLQR: some instances hit max_iter / max_ls (results written)"
+    st == MP_ERR_NUMERIC || check(st, c)
+    return J, it
+end
+
+end # module
