@@ -83,8 +83,8 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
             feas=torch.empty(S, dtype=torch.int32, device=dev),
             rc=torch.empty(S, dtype=torch.int32, device=dev),
             fc=torch.empty(S, dtype=torch.int32, device=dev),
-            ctraj=torch.empty((S, K, H + 1, 7), dtype=torch.float64, device=dev),
-            cctrl=torch.empty((S, K, H, 2), dtype=torch.float64, device=dev),
+            ctraj=torch.empty((S, H + 1, 7, K), dtype=torch.float64, device=dev),  # SoA (include/mpgpu.h)
+            cctrl=torch.empty((S, H, K, 2), dtype=torch.float64, device=dev),
             ccost=torch.empty((S, K), dtype=torch.float64, device=dev),
             cfeas=torch.empty((S, K), dtype=torch.uint8, device=dev),
         ))

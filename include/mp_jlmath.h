@@ -47,6 +47,10 @@ MPJ_FN uint32_t mpj_lo(double x) { mpj_du v; v.d = x; return (uint32_t)(v.u & 0x
 MPJ_FN double mpj_from_words(uint32_t hi, uint32_t lo) {
   mpj_du v; v.u = ((uint64_t)hi << 32) | (uint64_t)lo; return v.d;
 }
+MPJ_FN double mpj_flip(double t, uint32_t signbit) { /* -t when signbit == 0x80000000 (exact negation) */
+  return mpj_from_words(mpj_hi(t) ^ signbit, mpj_lo(t));
+}
+
 MPJ_FN double mpj_zero_lo(double x) { mpj_du v; v.d = x; v.u &= 0xffffffff00000000ull; return v.d; }
 MPJ_FN double mpj_fma(double a, double b, double c) { return __builtin_fma(a, b, c); }
 MPJ_FN double mpj_sqrt(double x) { return __builtin_sqrt(x); }
@@ -545,7 +549,11 @@ MPJ_FN double mpj_log(double x) {
  * branches from nested ternaries).  Arguments outside the fast range of sincos
  * take the exact routine through a wave-uniform branch. */
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(MPJ_COUNT_HOT_PATH)
+#define MPJ_ANY(c) 0 /* instruction-count builds only (tools/isa_count.py): slow paths compiled out */
+#else
 #define MPJ_ANY(c) __any((int)(c))
+#endif
 __device__ __forceinline__ double mpj_sel(int c, double t, double f) {
   const unsigned long long m = __ballot(c);
   unsigned rl, rh;
@@ -572,13 +580,13 @@ MPJ_FN double mpj_atan_bl(double x) {
   const int id2 = c2 && !c1;
   /* (na*a - nb) / (na + nb*a): id -1 -> x/1, 0 -> (2x-1)/(2+x), 1 -> (x-1)/(1+x),
    * 2 -> (x-1.5)/(1+1.5x), 3 -> -1/x == (0*x-1)/(0+1*x).  NaN propagates. */
-  const double a = MPJ_SEL(small, x, mpj_fabs(x));
-  const double na = MPJ_SEL(small, 1.0, MPJ_SEL(c0, 2.0, MPJ_SEL(c2, 1.0, 0.0)));
-  const double nb = MPJ_SEL(small, 0.0, MPJ_SEL(id2, 1.5, 1.0));
-  const double hi = MPJ_SEL(small, 0.0, MPJ_SEL(c0, 4.63647609000806093515e-01, MPJ_SEL(c1,
-                    7.85398163397448278999e-01, MPJ_SEL(c2, 9.82793723247329054082e-01, 1.57079632679489655800e+00))));
-  const double lo = MPJ_SEL(small, 0.0, MPJ_SEL(c0, 2.26987774529616870924e-17, MPJ_SEL(c1,
-                    3.06161699786838301793e-17, MPJ_SEL(c2, 1.39033110312309984516e-17, 6.12323399573676603587e-17))));
+  const double a = mpj_fabs(x); /* the odd polynomial makes the |x| < 0.4375 path sign-symmetric */
+  const double na = small ? 1.0 : (c0 ? 2.0 : (c2 ? 1.0 : 0.0));
+  const double nb = small ? 0.0 : (id2 ? 1.5 : 1.0);
+  const double hi = small ? 0.0 : (c0 ? 4.63647609000806093515e-01 : (c1 ?
+                    7.85398163397448278999e-01 : (c2 ? 9.82793723247329054082e-01 : 1.57079632679489655800e+00)));
+  const double lo = small ? 0.0 : (c0 ? 2.26987774529616870924e-17 : (c1 ?
+                    3.06161699786838301793e-17 : (c2 ? 1.39033110312309984516e-17 : 6.12323399573676603587e-17)));
   const double ax = (na * a - nb) / (na + nb * a);
   const double z = ax * ax;
   const double w = z * z;
@@ -586,7 +594,7 @@ MPJ_FN double mpj_atan_bl(double x) {
   const double s2 = w * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT9, aT7), aT5), aT3), aT1);
   /* id -1: x - x*s == -((x*s - 0) - x) == hi - ((x*s - lo) - x) with hi = lo = 0 */
   const double r = hi - ((ax * (s1 + s2) - lo) - ax);
-  const double rs = MPJ_SEL(!small && (hx >> 31), -r, r);
+  const double rs = mpj_flip(r, hx & 0x80000000u);
   /* |x| >= 2^66 (incl. ±Inf, where 0*Inf would be NaN): atanhi[3] + atanlo[3] */
   const double big = 1.57079632679489655800e+00 + 6.12323399573676603587e-17;
   const double rb = MPJ_SEL(ix >= 0x44100000u && x == x, MPJ_SEL(hx >> 31, -big, big), rs);
@@ -604,16 +612,27 @@ MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
     mpj_sincos(x, so, co);
     return;
   }
-  const double fa = MPJ_SEL(xhp <= 0x4002d97cu, 1.0, MPJ_SEL(xhp <= 0x400f6a7au, 2.0, MPJ_SEL(xhp <= 0x4015fdbcu, 3.0, 4.0)));
-  const double fn = MPJ_SEL(x > 0.0, fa, -fa);
+  /* |n| = 1..4 by range (e_rem_pio2.c), Cody–Waite with fn = ±|n| */
+  const int na = 1 + (xhp > 0x4002d97cu) + (xhp > 0x400f6a7au) + (xhp > 0x4015fdbcu);
+  const int ni = x > 0.0 ? na : -na;
   double y0, y1;
-  mpj_cw2c(x, fn, 0, &y0, &y1);
-  const double sk = mpj_sin_k(y0, y1), ck = mpj_cos_k(y0, y1);
-  const double s0 = MPJ_SEL(ax < MPJ_SQRT_EPS, x, mpj_sin_k0(x));
-  const double c0 = MPJ_SEL(ax < MPJ_SQRT_HALF_EPS, 1.0, mpj_cos_k(x, 0.0));
-  const int n = ((int)fn) & 3;
-  const double sr = MPJ_SEL(n == 0, sk, MPJ_SEL(n == 1, ck, MPJ_SEL(n == 2, -sk, -ck)));
-  const double cr = MPJ_SEL(n == 0, ck, MPJ_SEL(n == 1, -sk, MPJ_SEL(n == 2, -ck, sk)));
+  mpj_cw2c(x, (double)ni, 0, &y0, &y1);
+  /* one sin and one cos kernel: the |x| < π/4 path is sin_k0(x) / cos_k(x, 0), the
+   * reduced path sin_k(y0, y1) / cos_k(y0, y1); both share z, w, r, v of their argument */
+  const double xa = MPJ_SEL(small, x, y0), ya = MPJ_SEL(small, 0.0, y1);
+  const double z = xa * xa, w = z * z;
+  const double r = mpj_fma(z, mpj_fma(z, MPJ_S4, MPJ_S3), MPJ_S2) + z * w * mpj_fma(z, MPJ_S6, MPJ_S5);
+  const double v = z * xa;
+  const double sk0 = xa + v * (MPJ_S1 + z * r);                          /* mpj_sin_k0(x) */
+  const double sk = xa - ((z * (0.5 * ya - v * r) - ya) - v * MPJ_S1);   /* mpj_sin_k(y0, y1) */
+  const double ck = mpj_cos_k(xa, ya);
+  const double s0 = MPJ_SEL(ax < MPJ_SQRT_EPS, x, sk0);
+  const double c0 = MPJ_SEL(ax < MPJ_SQRT_HALF_EPS, 1.0, ck);
+  /* n&3: 0 -> (s, c), 1 -> (c, -s), 2 -> (-s, -c), 3 -> (-c, s) */
+  const int n = ni & 3;
+  const double ts = MPJ_SEL(n & 1, ck, sk), tc = MPJ_SEL(n & 1, sk, ck);
+  const double sr = mpj_flip(ts, (uint32_t)(n & 2) << 30);
+  const double cr = mpj_flip(tc, (uint32_t)((n + 1) & 2) << 30);
   *so = MPJ_SEL(small, s0, sr);
   *co = MPJ_SEL(small, c0, cr);
 }

@@ -109,7 +109,10 @@ typedef struct mp_mppi_params {
  *      rollout_count_out[S] MPPI.r.RolloutCount (= m + 1, reference off-by-one)
  *      feasible_count_out[S] MPPI.r.FeasibleTrajCount
  * optional (NULL to skip) — MPPI.p.TrajectoryCollection[1:K] (types.jl:3-8):
- *      coll_traj[S][K][H+1][7], coll_ctrl[S][K][H][2], coll_cost[S][K], coll_feas[S][K]
+ *      coll_traj[S][H+1][7][K], coll_ctrl[S][H][K][2], coll_cost[S][K], coll_feas[S][K]
+ *      — structure of arrays, rollout index k fastest (Julia (K, 7, H+1, S) and
+ *      (2, K, H, S)): holder k's Trajectory is coll_traj[s][:, :, k] transposed, and a
+ *      wavefront's per-step stores for 32 consecutive rollouts are full 128-B lines.
  *      (all K rollouts are written; the planner uses the first m = rollout_count-1).
  * Returns MP_ERR_NUMERIC (after writing outputs) if any rollout cost was NaN.
  */

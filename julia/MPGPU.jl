@@ -104,7 +104,8 @@ S scenes in one launch.  Julia shapes: X0 (7, S), goal (2, S), Unom (2, H, S),
 obstacles (3, n_obs, S), grid occupancy (nx, ny, S) UInt8, noise z (2, H, K, S) or
 `nothing` (device Philox).  Returns U (2, H, S), traj (7, H+1, S), cost, feasible,
 rollout_count, feasible_count (S,) and, with `collect`, the TrajectoryCollection arrays
-coll_traj (7, H+1, K, S), coll_ctrl (2, H, K, S), coll_cost (K, S), coll_feas (K, S).
+(structure of arrays, rollout index first) coll_traj (K, 7, H+1, S), coll_ctrl (2, K, H, S),
+coll_cost (K, S), coll_feas (K, S).
 """
 function mppi_plan_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Float64}, Unom::Array{Float64,3};
                          obstacles = nothing, grid = nothing, noise = nothing, collect::Bool = false)
@@ -112,8 +113,8 @@ function mppi_plan_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Float6
     p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 25)...)
     U = zeros(2, H, S); traj = zeros(7, H + 1, S); cost = zeros(S)
     feas = zeros(Int32, S); rc = zeros(Int32, S); fc = zeros(Int32, S)
-    ct = collect ? zeros(7, H + 1, K, S) : nothing
-    cc = collect ? zeros(2, H, K, S) : nothing
+    ct = collect ? zeros(K, 7, H + 1, S) : nothing
+    cc = collect ? zeros(2, K, H, S) : nothing
     ck = collect ? zeros(K, S) : nothing
     cf = collect ? zeros(UInt8, K, S) : nothing
     nz(a) = a === nothing ? C_NULL : pointer(a)
@@ -161,7 +162,7 @@ function MPPIPlan(mppi; noise = nothing, seed = 0, collect::Bool = true)
     if collect
         m = r.rollout_count[1] - 1
         hold = eltype(mppi.p.TrajectoryCollection)
-        mppi.p.TrajectoryCollection = [hold(permutedims(r.coll_traj[:, :, k, 1]), permutedims(r.coll_ctrl[:, :, k, 1]),
+        mppi.p.TrajectoryCollection = [hold(permutedims(r.coll_traj[k, :, :, 1]), permutedims(r.coll_ctrl[:, k, :, 1]),
                                             r.coll_feas[k, 1] == 1, r.coll_cost[k, 1]) for k in 1:m]
     end
     mppi.r.time = time() - t1

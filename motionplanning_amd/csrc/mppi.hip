@@ -14,6 +14,7 @@
 #include "mppi_device.hpp"
 #include "runtime.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -58,11 +59,11 @@ struct PlanArgs {
   const double* obs;
   const unsigned char* grid;
   const double* noise;
-  double* ctrl_all;    // [S][K][H][2]
+  double* ctrl_all;    // [S][H][K][2]  (rollout index fastest: coalesced per-step stores)
   double* cost_all;    // [S][K]
   unsigned char* feas_all;  // [S][K]
   double* part;        // [S][nb][pstride]
-  double* coll_traj;   // [S][K][H+1][7] or null
+  double* coll_traj;   // [S][H+1][7][K] or null
   unsigned* tickets;
   int* flags;
   double* U_out;
@@ -80,7 +81,17 @@ struct PlanArgs {
 
 #define MP_STAMP(i)                                                                  \
   do {                                                                               \
-    if (A.stamps && threadIdx.x == 0) A.stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (A.stamps && threadIdx.x == 0) A.stamps[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+// per-wave phase-1 end time [8 + w] and HW_ID (SIMD placement) [20 + w], diagnostic build only
+#define MP_STAMP_WAVE()                                                              \
+  do {                                                                               \
+    if (A.stamps && (threadIdx.x & 63) == 0) {                                       \
+      unsigned hwid;                                                                 \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));             \
+      A.stamps[blockIdx.x * 32 + 8 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime(); \
+      A.stamps[blockIdx.x * 32 + 20 + (threadIdx.x >> 6)] = hwid;                    \
+    }                                                                                \
   } while (0)
 
 // Noise for every (scene, step, rollout), h-major [S][H][K][2] so the rollout's
@@ -106,10 +117,13 @@ __global__ __launch_bounds__(256) void noise_prep_kernel(MppiDev P, int S, const
   reinterpret_cast<double2*>(zh)[i] = make_double2(z[0], z[1]);
 }
 
-__global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
+// BT threads per block (4 or 8 waves), BT/2 rollouts per block.
+template <int BT>
+__global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
+  constexpr int NT = BT, RPB = BT / 2, NQ = BT / 128;
   __shared__ double sh_red[NT / 64];
   __shared__ double sh_e[RPB];
-  __shared__ double sh_q[2][128];
+  __shared__ double sh_q[NQ][128];
   __shared__ int sh_last, sh_m, sh_bstar, sh_fc;
   __shared__ double sh_eta;
   extern __shared__ double dyn[];
@@ -152,7 +166,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     }
     __syncthreads();
   }
-  double* ctrl_g = A.ctrl_all ? A.ctrl_all + ((size_t)s * K + kk) * H2 : nullptr;
+  double* ctrl_g = A.ctrl_all ? A.ctrl_all + ((size_t)s * H * K + kk) * 2 + side : nullptr;
 
   // ---------------- phase 1: the rollout of this lane pair
   int feas;
@@ -169,13 +183,14 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     };
     auto store = [&](int j, const double* u) {
       if (ush) ush[pair * ustr + 2 * j + side] = u[side];
-      if (ctrl_g) ctrl_g[2 * j + side] = u[side];
+      if (ctrl_g) ctrl_g[(size_t)j * K * 2] = u[side];
     };
     // inactive pairs (k >= K) recompute rollout K-1 and write identical values
-    double* traj = A.coll_traj ? A.coll_traj + ((size_t)s * K + kk) * (H + 1) * 7 : nullptr;
+    const TrajOut traj{A.coll_traj ? A.coll_traj + (size_t)s * (H + 1) * 7 * K + kk : nullptr, 7LL * K, (long long)K};
     c = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas);
   }
   MP_STAMP(1);
+  MP_STAMP_WAVE();
   if (active && side == 0) {
     A.cost_all[(size_t)s * K + k] = c;
     A.feas_all[(size_t)s * K + k] = (unsigned char)feas;
@@ -193,7 +208,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   {
     // Σ_i e_i u_i[t] over this block's rollouts; two fixed halves per output, summed in order
     const int t = tid % 128, q = tid / 128;
-    const int r0 = q * (RPB / 2), r1 = r0 + RPB / 2;
+    const int r0 = q * (RPB / NQ), r1 = r0 + RPB / NQ;
     for (int t0 = 0; t0 < H2; t0 += 128) {  // block-uniform trip count: barriers are safe
       const int tt = t0 + t;
       double acc = 0.0;
@@ -202,15 +217,20 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
           for (int r = r0; r < r1; r++) acc = acc + sh_e[r] * ush[r * ustr + tt];
         } else {
           // independent loads: issue 16 before consuming (L2 latency, not a serial chain)
-          const double* cb = A.ctrl_all + ((size_t)s * K + b * RPB) * H2 + tt;
+          const double* cb = A.ctrl_all + (((size_t)s * H + (tt >> 1)) * K + (size_t)b * RPB) * 2 + (tt & 1);
           const int rmax = min(r1, K - b * RPB);
 #pragma unroll 16
-          for (int r = r0; r < rmax; r++) acc = acc + sh_e[r] * cb[(size_t)r * H2];
+          for (int r = r0; r < rmax; r++) acc = acc + sh_e[r] * cb[(size_t)r * 2];
         }
       }
       sh_q[q][t] = acc;
       __syncthreads();
-      if (q == 0 && tt < H2) part[4 + tt] = sh_q[0][t] + sh_q[1][t];
+      if (q == 0 && tt < H2) {
+        double v = sh_q[0][t];
+#pragma unroll
+        for (int i = 1; i < NQ; i++) v = v + sh_q[i][t];
+        part[4 + tt] = v;
+      }
       __syncthreads();
     }
   }
@@ -329,7 +349,7 @@ __global__ __launch_bounds__(NT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   {
     auto ctrl = [&](int j, double* u) { u[0] = Ush[2 * j]; u[1] = Ush[2 * j + 1]; };
     auto store = [&](int, const double*) {};
-    double* traj = A.traj_out + (size_t)s * (H + 1) * 7;  // every pair writes the same values
+    const TrajOut traj{A.traj_out + (size_t)s * (H + 1) * 7, 7, 1};  // every pair writes the same values
     int f2;
     const double c2 = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &f2);
     if (tid == 0) {
@@ -363,7 +383,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(MppiDev P, int K, const dou
     u[1] = q[1];
   };
   auto store = [&](int, const double*) {};
-  double* tr = (traj && active) ? traj + ((size_t)s * K + k) * (H + 1) * 7 : nullptr;
+  const TrajOut tr{(traj && active) ? traj + ((size_t)s * K + k) * (H + 1) * 7 : nullptr, 7, 1};
   int f;
   const double c = rollout_pair(P, X0 + 7 * s, goal + 2 * s, obs ? obs + (size_t)3 * P.n_obs * s : nullptr,
                                 grid ? grid + (size_t)P.gnx * P.gny * s : nullptr,
@@ -480,7 +500,12 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                        int32_t* rc_out, int32_t* fc_out, double* coll_traj, double* coll_ctrl,
                        double* coll_cost, uint8_t* coll_feas) {
   const int K = D.K, H = D.H;
-  const int nb = (K + RPB - 1) / RPB;
+  // 8-wave blocks once the launch fills every CU with one (the dispatcher then places
+  // exactly two waves per SIMD; with 4-wave blocks, two per CU, it can stack 3 + 1 and
+  // the slowest SIMD sets the end time), else 4-wave blocks for more CUs at small S.
+  const int BT = (size_t)S * ((K + 255) / 256) >= 256 ? 512 : 256;
+  const int RPBh = BT / 2;
+  const int nb = (K + RPBh - 1) / RPBh;
   const int pstride = 4 + 2 * H;
   PlanArgs A;
   A.X0 = X0; A.goal = goal; A.unom = U_nom; A.obs = D.n_obs > 0 ? obstacles : nullptr;
@@ -521,9 +546,9 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   }
   // Control lists / staged partials in LDS only while two blocks still fit per CU
   // (multi-scene launches need every block co-resident); otherwise the HBM path.
-  const int ctrl_words = RPB * (2 * H + 1), part_words = nb * pstride;
+  const int ctrl_words = RPBh * (2 * H + 1), part_words = nb * pstride;
   A.lds_ctrl = A.lds_part = -1;
-  const bool many = (size_t)S * nb > 256;
+  const bool many = (size_t)S * nb > 256;  // more blocks than CUs: keep two per CU resident
   const size_t budget = many ? kCoLds : kMaxLds;
   if ((size_t)(off + (ctrl_words > part_words ? ctrl_words : part_words)) * 8 <= budget) {
     A.lds_ctrl = A.lds_part = off;
@@ -542,29 +567,34 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   MP_CHECK(ctx, shmem <= kMaxLds, "K/H/obstacles too large for one scene (dynamic LDS %zu B)", shmem);
   static bool attr_set = false;
   if (!attr_set) {
-    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kMaxLds));
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kMaxLds));
     attr_set = true;
   }
   A.stamps = nullptr;
   static const bool stamps_on = getenv("MPGPU_STAMPS") != nullptr;
   if (stamps_on) {
-    A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA2, sizeof(unsigned long long) * 8 * S * nb);
+    A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA2, sizeof(unsigned long long) * 32 * S * nb);
     MP_HIP(ctx, hipMemsetAsync(A.stamps, 0, sizeof(unsigned long long) * 8 * S * nb, ctx->stream));
   }
   mp_time_begin(ctx);
-  hipLaunchKernelGGL(mppi_plan_kernel, dim3(S * nb), dim3(NT), shmem, ctx->stream, D, A);
+  if (BT == 512)
+    hipLaunchKernelGGL(mppi_plan_kernel<512>, dim3(S * nb), dim3(512), shmem, ctx->stream, D, A);
+  else
+    hipLaunchKernelGGL(mppi_plan_kernel<256>, dim3(S * nb), dim3(256), shmem, ctx->stream, D, A);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
   if (stamps_on) {
-    std::vector<unsigned long long> h(8 * S * nb);
+    std::vector<unsigned long long> h(32 * S * nb);
     MP_HIP(ctx, hipMemcpyAsync(h.data(), A.stamps, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     unsigned long long t0 = ~0ull, end = 0;
     double d01 = 0, d12 = 0, d23 = 0;
     int last = -1;
     for (int b = 0; b < S * nb; b++) {
-      const unsigned long long* q = &h[8 * b];
+      const unsigned long long* q = &h[32 * b];
       t0 = q[0] < t0 ? q[0] : t0;
       d01 += (q[1] - q[0]) / 100.0; d12 += (q[2] - q[1]) / 100.0; d23 += (q[3] - q[2]) / 100.0;
       if (q[5]) last = b;
@@ -573,8 +603,38 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     }
     fprintf(stderr, "[stamps us] blocks=%d mean rollout %.2f partial %.2f ticket %.2f", S * nb, d01 / (S * nb),
             d12 / (S * nb), d23 / (S * nb));
+    {  // spread: block start times and phase-1 end times (percentiles)
+      std::vector<double> st, en;
+      for (int b = 0; b < S * nb; b++) {
+        st.push_back((h[32 * b] - t0) / 100.0);
+        en.push_back((h[32 * b + 1] - t0) / 100.0);
+      }
+      std::sort(st.begin(), st.end());
+      std::sort(en.begin(), en.end());
+      const int n = S * nb;
+      fprintf(stderr, " | start p0/50/90/100 %.1f %.1f %.1f %.1f | p1-end p0/50/90/100 %.1f %.1f %.1f %.1f", st[0],
+              st[n / 2], st[n * 9 / 10], st[n - 1], en[0], en[n / 2], en[n * 9 / 10], en[n - 1]);
+      // per-wave ends and SIMD placement
+      std::vector<double> we;
+      int hist[9] = {0};  // max waves on one SIMD within a block
+      for (int b = 0; b < n; b++) {
+        int cnt[4] = {0, 0, 0, 0}, mx = 0;
+        for (int w = 0; w < 8; w++) {
+          const unsigned long long tw = h[32 * b + 8 + w];
+          if (!tw) continue;
+          we.push_back((tw - t0) / 100.0);
+          const int simd = (int)((h[32 * b + 20 + w] >> 4) & 3);
+          mx = std::max(mx, ++cnt[simd]);
+        }
+        hist[mx]++;
+      }
+      std::sort(we.begin(), we.end());
+      const int m = (int)we.size();
+      fprintf(stderr, " | wave-end p0/50/90/100 %.1f %.1f %.1f %.1f | blocks by max waves/SIMD 1:%d 2:%d 3:%d 4:%d",
+              we[0], we[m / 2], we[m * 9 / 10], we[m - 1], hist[1], hist[2], hist[3], hist[4]);
+    }
     if (last >= 0) {
-      const unsigned long long* q = &h[8 * last];
+      const unsigned long long* q = &h[32 * last];
       fprintf(stderr, " | last block: start+%.2f combine %.2f final-rollout %.2f | total %.2f", (q[0] - t0) / 100.0,
               (q[4] - q[3]) / 100.0, (q[5] - q[4]) / 100.0, (end - t0) / 100.0);
     }

@@ -170,28 +170,38 @@ __device__ __forceinline__ void draw_ctrl(const MppiDev& P, const double* noise_
   sample_ctrl(P, z, unom_s + 2 * h, u);
 }
 
-// A state row of 7 doubles written by the lane pair without divergence: the
-// even lane writes x[0..3] at [0..3], the odd lane x[3..6] at [3..6] (x[3]
-// is written twice with the same value).
-__device__ __forceinline__ void store_state(double* row, const double* x, int side) {
-  double* p = row + 3 * side;
+// Where a rollout's states go: state i of step j at p[j*rs + i*cs].  AoS rows
+// (rs = 7, cs = 1: traj_out, mp_rollout) or the structure-of-arrays
+// TrajectoryCollection (rs = 7K, cs = K, p offset by the rollout index k), whose
+// per-step stores from a wavefront's 32 consecutive rollouts are full 128-B lines.
+struct TrajOut {
+  double* p;
+  long long rs, cs;
+};
+
+// The even lane of the pair stores x[0..3], the odd lane x[4..6].
+__device__ __forceinline__ void store_state(const TrajOut& T, int j, const double* x, int side) {
+  double* q = T.p + (long long)j * T.rs;
 #pragma unroll
-  for (int i = 0; i < 4; i++) p[i] = MPJ_SEL(side, x[3 + i], x[i]);
+  for (int i = 0; i < 4; i++) {
+    const double v = MPJ_SEL(side, x[4 + i < 7 ? 4 + i : 6], x[i]);
+    if (!side || i < 3) q[(long long)(side ? 4 + i : i) * T.cs] = v;
+  }
 }
 
 // --------------------------------------------------------------- rollout
 // TrajectoryRollout for the lane pair (MPPIUtils.jl:31-57).  `ctrl(j, u)` yields the
-// control of step j.  traj (optional) gets (H+1)x7 states (store_state).
+// control of step j.  traj.p (optional) gets the H+1 states (store_state).
 // Returns cost_total; *feas = constraint.
 template <class CtrlFn, class StoreFn>
 __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X0, const double* goal,
                                                const double* obs, const unsigned char* grid,
                                                const double* unom, int side, CtrlFn ctrl, StoreFn store,
-                                               double* traj, int* feas) {
+                                               const TrajOut& traj, int* feas) {
   double x[7];
 #pragma unroll
   for (int i = 0; i < 7; i++) x[i] = X0[i];
-  if (traj) store_state(traj, x, side);
+  if (traj.p) store_state(traj, 0, x, side);
   double sum = 0.0;
   int ok_all = 1;
   for (int j = 0; j < P.H; j++) {
@@ -222,7 +232,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     }
     sum = sum + cj;
     ok_all &= okc & okb;
-    if (traj) store_state(traj + 7 * (j + 1), x, side);
+    if (traj.p) store_state(traj, j + 1, x, side);
   }
   {  // terminal (:49-54): only the running cost of the extra RK2 step is used
     int okc = 1, okb = 1;

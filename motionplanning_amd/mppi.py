@@ -179,13 +179,17 @@ def mppi_plan_batch(p: MPPIParams, X0, goal, U_nom, obstacles=None, grid=None, n
                feasible_count=np.zeros(S, np.int32))
     coll = {}
     if collect:
-        coll = dict(traj=np.zeros((S, K, H + 1, 7)), ctrl=np.zeros((S, K, H, 2)), cost=np.zeros((S, K)),
+        # device layout: structure of arrays, rollout index fastest (include/mpgpu.h)
+        coll = dict(traj_soa=np.zeros((S, H + 1, 7, K)), ctrl_soa=np.zeros((S, H, K, 2)), cost=np.zeros((S, K)),
                     feas=np.zeros((S, K), np.uint8))
     st = ctx.lib.mp_mppi_plan(ctx.handle, ctypes.byref(p), S, ptr(X0), ptr(goal), ptr(U_nom), ptr(obstacles),
                               ptr(grid), ptr(noise), ptr(out["U"]), ptr(out["traj"]), ptr(out["cost"]),
                               ptr(out["feasible"]), ptr(out["rollout_count"]), ptr(out["feasible_count"]),
-                              ptr(coll.get("traj")), ptr(coll.get("ctrl")), ptr(coll.get("cost")),
+                              ptr(coll.get("traj_soa")), ptr(coll.get("ctrl_soa")), ptr(coll.get("cost")),
                               ptr(coll.get("feas")))
+    if collect:  # reference-shaped views: traj (S, K, H+1, 7), ctrl (S, K, H, 2)
+        coll["traj"] = coll["traj_soa"].transpose(0, 3, 1, 2)
+        coll["ctrl"] = coll["ctrl_soa"].transpose(0, 2, 1, 3)
     out["nan"] = st == MP_ERR_NUMERIC
     if st != MP_ERR_NUMERIC:
         ctx.check(st)

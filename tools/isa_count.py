@@ -1,0 +1,94 @@
+"""Static instruction census of the MPPI rollout step (the hot loop of mppi_plan_kernel).
+
+Compiles csrc/mppi.hip for gfx950 with -DMPJ_COUNT_HOT_PATH (the wave-uniform slow paths
+of the branch-free libm compiled out, so the loop body is the hot straight-line path) and
+counts the instructions of the largest loop of the kernel by class.
+
+  python tools/isa_count.py [--kernel mppi_plan_kernel] [--extra -DFOO]
+"""
+import argparse
+import collections
+import os
+import re
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def classify(op):
+    if re.match(r"v_(add|sub)_f64|v_add_f64", op):
+        return "f64 add"
+    if op.startswith("v_mul_f64"):
+        return "f64 mul"
+    if op.startswith(("v_fma_f64", "v_fmac_f64")):
+        return "f64 fma"
+    if op.startswith(("v_div_", "v_rcp_f64", "v_rsq_f64", "v_sqrt_f64")):
+        return "f64 div/rcp/sqrt"
+    if op.startswith("v_cndmask"):
+        return "v_cndmask"
+    if op.startswith(("v_mov", "v_accvgpr")):
+        return "v_mov"
+    if op.startswith(("v_readlane", "v_writelane", "v_readfirstlane")):
+        return "v_read/writelane"
+    if op.startswith("v_cmp"):
+        return "v_cmp"
+    if op.startswith(("v_ldexp", "v_frexp", "v_rndne", "v_trunc", "v_floor", "v_fract", "v_cvt")):
+        return "f64 misc"
+    if op.startswith("v_"):
+        return "other VALU"
+    if op.startswith(("ds_",)):
+        return "LDS"
+    if op.startswith(("global_", "buffer_", "flat_", "scratch_")):
+        return "VMEM"
+    if op.startswith("s_waitcnt") or op.startswith("s_nop"):
+        return "s_waitcnt/nop"
+    if op.startswith("s_"):
+        return "SALU/branch"
+    return "other"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="mppi_plan_kernel")
+    ap.add_argument("--src", default=os.path.join(ROOT, "motionplanning_amd", "csrc", "mppi.hip"))
+    ap.add_argument("--extra", action="append", default=[])
+    ap.add_argument("--top", type=int, default=0)
+    a = ap.parse_args()
+    with tempfile.TemporaryDirectory() as td:
+        asm = os.path.join(td, "k.s")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                        "--cuda-device-only", "-S", "-DMPJ_COUNT_HOT_PATH", "-I" + os.path.join(ROOT, "include"),
+                        *a.extra, "-o", asm, a.src], check=True, capture_output=True)
+        lines = open(asm).read().split("\n")
+    # kernels: every symbol containing the name; take the one with the biggest body
+    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + a.kernel + r"\S*:", l)]
+    best = None
+    for s0 in starts:
+        e0 = next(i for i in range(s0, len(lines)) if lines[i].startswith(".Lfunc_end"))
+        body = lines[s0:e0]
+        heads = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l and l.startswith(".LBB")]
+        for h in heads:
+            lab = body[h].split(":")[0]
+            back = [j for j, l in enumerate(body) if re.search(r"s_(cbranch_\w+|branch)\s+" + re.escape(lab) + r"$", l.strip())]
+            if not back:
+                continue
+            seg = body[h:max(back) + 1]
+            ins = [l.strip().split()[0] for l in seg if l.strip() and not l.strip().startswith((";", ".")) and
+                   not l.startswith(".")]
+            if best is None or len(ins) > len(best[1]):
+                best = (lines[s0].split(":")[0], ins)
+    name, ins = best
+    c = collections.Counter(classify(op) for op in ins)
+    valu = sum(v for k, v in c.items() if k.startswith(("f64", "v_", "other VALU")))
+    nbr = sum(1 for op in ins if op.startswith("s_cbranch"))
+    print(f"{name[:60]}: largest loop body {len(ins)} instructions, VALU {valu}, conditional branches {nbr}")
+    for k, v in c.most_common():
+        print(f"  {k:20s} {v:6d}")
+    if a.top:
+        for op, v in collections.Counter(ins).most_common(a.top):
+            print(f"    {op:28s} {v}")
+
+
+if __name__ == "__main__":
+    main()
