@@ -601,6 +601,43 @@ MPJ_FN double mpj_atan_bl(double x) {
   return MPJ_SEL(ix < 0x3e400000u, x, rb);
 }
 
+/* atan_bl with the range constants {na, nb, hi, lo} fetched from a 5-row table indexed by
+ * the FDLIBM range (0: |x| < 0.4375, 1..4: the four reductions) instead of select trees —
+ * on the device the table lives in LDS (mpj_atan_tab_init fills it).  Same operations on
+ * the same operands as mpj_atan_bl / mpj_atan, so the same bits. */
+MPJ_FN void mpj_atan_tab_init(double* tab) {
+  const double t[20] = {1.0, 0.0, 0.0, 0.0,
+                        2.0, 1.0, 4.63647609000806093515e-01, 2.26987774529616870924e-17,
+                        1.0, 1.0, 7.85398163397448278999e-01, 3.06161699786838301793e-17,
+                        1.0, 1.5, 9.82793723247329054082e-01, 1.39033110312309984516e-17,
+                        0.0, 1.0, 1.57079632679489655800e+00, 6.12323399573676603587e-17};
+  for (int i = 0; i < 20; i++) tab[i] = t[i];
+}
+MPJ_FN double mpj_atan_tab(double x, const double* tab) {
+  const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+               aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+               aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+               aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+               aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+               aT10 = 1.62858201153657823623e-02;
+  const uint32_t hx = mpj_hi(x);
+  const uint32_t ix = hx & 0x7fffffffu;
+  const int id = (ix >= 0x3fdc0000u) + (ix >= 0x3fe60000u) + (ix >= 0x3ff30000u) + (ix >= 0x40038000u);
+  const double* t = tab + 4 * id;
+  const double na = t[0], nb = t[1], hi = t[2], lo = t[3];
+  const double a = mpj_fabs(x);
+  const double ax = (na * a - nb) / (na + nb * a);
+  const double z = ax * ax;
+  const double w = z * z;
+  const double s1 = z * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT10, aT8), aT6), aT4), aT2), aT0);
+  const double s2 = w * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT9, aT7), aT5), aT3), aT1);
+  const double r = hi - ((ax * (s1 + s2) - lo) - ax);
+  const double rs = mpj_flip(r, hx & 0x80000000u);
+  const double big = 1.57079632679489655800e+00 + 6.12323399573676603587e-17;
+  const double rb = MPJ_SEL(ix >= 0x44100000u && x == x, MPJ_SEL(hx >> 31, -big, big), rs);
+  return MPJ_SEL(ix < 0x3e400000u, x, rb);
+}
+
 /* sin and cos for |x| <= ~9π/4 without a divergent branch (cw2c reduction, n in {0, ±1..±4}). */
 MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
   const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;

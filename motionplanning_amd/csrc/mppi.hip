@@ -126,6 +126,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   __shared__ double sh_q[NQ][128];
   __shared__ int sh_last, sh_m, sh_bstar, sh_fc;
   __shared__ double sh_eta;
+  __shared__ double atab[20];  // mpj_atan_tab range constants
   extern __shared__ double dyn[];
   const int H = P.H, H2 = 2 * H, K = P.K;
   const int s = blockIdx.x / A.nb, b = blockIdx.x % A.nb;
@@ -148,6 +149,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   const unsigned char* grid = nullptr;
   {
     const double* gu = A.unom + (size_t)H2 * s;
+    if (tid == 0) mpj_atan_tab_init(atab);
     for (int i = tid; i < H2; i += NT) unom[i] = gu[i];
     if (A.obs) {
       const double* go = A.obs + (size_t)3 * P.n_obs * s;
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     };
     // inactive pairs (k >= K) recompute rollout K-1 and write identical values
     const TrajOut traj{A.coll_traj ? A.coll_traj + (size_t)s * (H + 1) * 7 * K + kk : nullptr, 7LL * K, (long long)K};
-    c = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas);
+    c = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas, atab);
   }
   MP_STAMP(1);
   MP_STAMP_WAVE();
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     auto store = [&](int, const double*) {};
     const TrajOut traj{A.traj_out + (size_t)s * (H + 1) * 7, 7, 1};  // every pair writes the same values
     int f2;
-    const double c2 = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &f2);
+    const double c2 = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &f2, atab);
     if (tid == 0) {
       A.cost_out[s] = c2;
       A.feas_out[s] = f2;
@@ -373,6 +375,9 @@ __global__ __launch_bounds__(NT) void rollout_kernel(MppiDev P, int K, const dou
   const int H = P.H;
   const int s = blockIdx.x / nb, b = blockIdx.x % nb;
   const int tid = threadIdx.x, pair = tid >> 1, side = tid & 1;
+  __shared__ double atab[20];
+  if (tid == 0) mpj_atan_tab_init(atab);
+  __syncthreads();
   const int k = b * RPB + pair;
   const bool active = k < K;
   const int kk = active ? k : K - 1;
@@ -387,7 +392,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(MppiDev P, int K, const dou
   int f;
   const double c = rollout_pair(P, X0 + 7 * s, goal + 2 * s, obs ? obs + (size_t)3 * P.n_obs * s : nullptr,
                                 grid ? grid + (size_t)P.gnx * P.gny * s : nullptr,
-                                unom ? unom + (size_t)2 * H * s : nullptr, side, cf, store, tr, &f);
+                                unom ? unom + (size_t)2 * H * s : nullptr, side, cf, store, tr, &f, atab);
   if (active && side == 0) {
     cost[(size_t)s * K + k] = c;
     feas[(size_t)s * K + k] = (unsigned char)f;
@@ -426,11 +431,14 @@ __global__ __launch_bounds__(64) void euler_kernel(int n, double* states, const 
   const int tid = blockIdx.x * 64 + threadIdx.x;
   const int v = tid >> 1, side = tid & 1;
   const int vv = v < n ? v : n - 1;
+  __shared__ double atab[20];
+  if (threadIdx.x == 0) mpj_atan_tab_init(atab);
+  __syncthreads();
   double x[7], d[7];
   for (int i = 0; i < 7; i++) x[i] = states[7 * vv + i];
   const double sr = ctrl[2 * vv], ax = ctrl[2 * vv + 1];
   for (int t = 0; t < nsteps; t++) {
-    dyn_pair(x, sr, ax, d, side);
+    dyn_pair(x, sr, ax, d, side, atab);
     for (int i = 0; i < 7; i++) x[i] = x[i] + d[i] * dt;
     if (his && v < n && side == 0)
       for (int i = 0; i < 7; i++) his[((size_t)v * nsteps + t) * 7 + i] = x[i];

@@ -40,7 +40,8 @@ __device__ __forceinline__ double pair_swap(double v) {
 
 // ---------------------------------------------------------------- dynamics
 // VehicleDynamics for a lane pair.  side = lane & 1 (0: front tire, 1: rear).
-__device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side) {
+// atab: the mpj_atan_tab range table (LDS).
+__device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side, const double* atab) {
   const double la = 1.56, lb = 1.64, M = 2020.0, Izz = 4095.0, g = 9.81, mu = 0.8;
   const double KFZF = 1018.28 / 2, KFZR = 963.34 / 2, KFZX = 186.22;
   const double B = -10.4 / mu, C = 1.3, E = 0.1556;
@@ -49,9 +50,9 @@ __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, 
   // front: 2*(KFZF*g - t);  rear: 2*(KFZR*g + t)   (vehicledynamics.jl:30-31)
   const double FZ = 2 * ((side ? KFZR : KFZF) * g + (side ? t : -t));
   // front: (v + la*r) ... - sa;  rear: (v - lb*r) ... [(-lb)*r == -(lb*r) exactly]  (:32-33)
-  const double alpha = mpj_atan_bl((v + (side ? -lb : la) * r) / (ux + 0.01)) - (side ? 0.0 : sa);
+  const double alpha = mpj_atan_tab((v + (side ? -lb : la) * r) / (ux + 0.01), atab) - (side ? 0.0 : sa);
   const double X1 = B * alpha;
-  const double FY = mu * FZ * 1.0 * mpj_sin_bl(C * mpj_atan_bl(X1 - E * (X1 - mpj_atan_bl(X1))));  // (:35-38)
+  const double FY = mu * FZ * 1.0 * mpj_sin_bl(C * mpj_atan_tab(X1 - E * (X1 - mpj_atan_tab(X1, atab)), atab));  // (:35-38)
   const double FYo = pair_swap(FY);
   const double FY1 = side ? FYo : FY, FY2 = side ? FY : FYo;
   const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);  // (:40-42)
@@ -81,7 +82,7 @@ __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* 
     const double dx = x[0] - obs[3 * o], dy = x[1] - obs[3 * o + 1], R = obs[3 * o + 2];
     const int hit = dx * dx + dy * dy <= R * R;
     *ok &= !hit;
-    c = MPJ_SEL(hit, c + P.obs_pen, c);
+    c = (hit ? c + P.obs_pen : c);
   }
   if (P.gnx > 0) {
     const double fx = (x[0] - P.gx0) / P.gdx;
@@ -90,7 +91,7 @@ __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* 
     const int ix = inb ? (int)fx : 0, iy = inb ? (int)fy : 0;
     const int hit = inb && grid[iy * P.gnx + ix];
     *ok &= !hit;
-    c = MPJ_SEL(hit, c + P.obs_pen, c);
+    c = (hit ? c + P.obs_pen : c);
   }
   return c;
 }
@@ -102,8 +103,10 @@ __device__ __forceinline__ double bound_cost(const MppiDev& P, const double* x, 
   for (int i = 0; i < 7; i++) {
     const int lo = x[i] < P.XL[i], hi = x[i] > P.XU[i];
     *ok &= !(lo | hi);
-    c = MPJ_SEL(lo, c + P.slack * __builtin_fabs(x[i] - P.XL[i]), c);
-    c = MPJ_SEL(hi, c + P.slack * __builtin_fabs(x[i] - P.XU[i]), c);
+    const double vl = c + P.slack * __builtin_fabs(x[i] - P.XL[i]);
+    c = lo ? vl : c;
+    const double vh = c + P.slack * __builtin_fabs(x[i] - P.XU[i]);
+    c = hi ? vh : c;
   }
   return c;
 }
@@ -197,7 +200,7 @@ template <class CtrlFn, class StoreFn>
 __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X0, const double* goal,
                                                const double* obs, const unsigned char* grid,
                                                const double* unom, int side, CtrlFn ctrl, StoreFn store,
-                                               const TrajOut& traj, int* feas) {
+                                               const TrajOut& traj, int* feas, const double* atab) {
   double x[7];
 #pragma unroll
   for (int i = 0; i < 7; i++) x[i] = X0[i];
@@ -216,10 +219,10 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     }
     const double pc = run_cost(x, u[0], u[1]);
     double k1[7], k2[7], x2[7];
-    dyn_pair(x, u[0], u[1], k1, side);
+    dyn_pair(x, u[0], u[1], k1, side, atab);
 #pragma unroll
     for (int i = 0; i < 7; i++) x2[i] = x[i] + k1[i] * P.dt;
-    dyn_pair(x2, u[0], u[1], k2, side);
+    dyn_pair(x2, u[0], u[1], k2, side, atab);
 #pragma unroll
     for (int i = 0; i < 7; i++) x[i] = x[i] + P.dt * (k1[i] + k2[i]) / 2;
     double cj = pc + cb + cc;

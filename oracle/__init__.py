@@ -32,7 +32,7 @@ def lib():
         if not os.path.exists(LIB):
             build()
         L = ctypes.CDLL(LIB)
-        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "sin_bl", "cos_bl"]:
+        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "atan_tab", "sin_bl", "cos_bl"]:
             f = getattr(L, "or_m_" + n)
             f.restype = _D
             f.argtypes = [_D]
@@ -44,7 +44,7 @@ def lib():
         L.or_rollout.argtypes = [ctypes.POINTER(MPPIParams), _V, _V, _V, ctypes.c_int64, _V, _V, _V, _V,
                                  ctypes.POINTER(ctypes.c_int)]
         L.or_mppi_plan.restype = ctypes.c_int
-        L.or_mppi_plan.argtypes = [ctypes.POINTER(MPPIParams), ctypes.c_int] + [_V] * 15
+        L.or_mppi_plan.argtypes = [ctypes.POINTER(MPPIParams), ctypes.c_int] + [_V] * 16
         L.or_dwa_plan.restype = ctypes.c_int
         L.or_dwa_plan.argtypes = [ctypes.POINTER(MPPIParams), _V, _V, ctypes.c_int, _V, _V, _V, _V]
         L.or_vehicle_euler.restype = None

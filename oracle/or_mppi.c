@@ -345,5 +345,11 @@ double or_m_exp(double x) { return mpj_exp(x); }
 double or_m_log(double x) { return mpj_log(x); }
 double or_m_modpi(double x) { return mpj_modpi(x); }
 double or_m_atan_bl(double x) { return mpj_atan_bl(x); }
+double or_m_atan_tab(double x) {
+  static double tab[20];
+  static int ready = 0;
+  if (!ready) { mpj_atan_tab_init(tab); ready = 1; }
+  return mpj_atan_tab(x, tab);
+}
 double or_m_sin_bl(double x) { return mpj_sin_bl(x); }
 double or_m_cos_bl(double x) { double s, c; mpj_sincos_bl(x, &s, &c); return c; }

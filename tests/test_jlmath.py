@@ -56,8 +56,10 @@ def test_branchless_variants_bitidentical():
                                    math.pi / 4, 2.356194490192345, 1e-9, 2e20, np.inf, -np.inf])])
     for x in xs:
         x = float(x)
-        a, b = oracle.m("atan_bl", x), oracle.m("atan", x)
-        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], ("atan", x)
+        b = oracle.m("atan", x)
+        for fa in ("atan_bl", "atan_tab"):
+            a = oracle.m(fa, x)
+            assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], (fa, x)
         if np.isfinite(x):
             for fb, fe in (("sin_bl", "sin"), ("cos_bl", "cos")):
                 a, b = oracle.m(fb, x), oracle.m(fe, x)

@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--src", default=os.path.join(ROOT, "motionplanning_amd", "csrc", "mppi.hip"))
     ap.add_argument("--extra", action="append", default=[])
     ap.add_argument("--top", type=int, default=0)
+    ap.add_argument("--inst", default="ILi512E", help="substring selecting the template instance")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         asm = os.path.join(td, "k.s")
@@ -62,7 +63,7 @@ def main():
                         *a.extra, "-o", asm, a.src], check=True, capture_output=True)
         lines = open(asm).read().split("\n")
     # kernels: every symbol containing the name; take the one with the biggest body
-    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + a.kernel + r"\S*:", l)]
+    starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + a.kernel + r"\S*:", l) and a.inst in l]
     best = None
     for s0 in starts:
         e0 = next(i for i in range(s0, len(lines)) if lines[i].startswith(".Lfunc_end"))
