@@ -550,9 +550,11 @@ MPJ_FN double mpj_log(double x) {
  * take the exact routine through a wave-uniform branch. */
 #if defined(__HIP_DEVICE_COMPILE__)
 #if defined(MPJ_COUNT_HOT_PATH)
-#define MPJ_ANY(c) 0 /* instruction-count builds only (tools/isa_count.py): slow paths compiled out */
+#define MPJ_ANY(c) 0  /* instruction-count builds only (tools/isa_count.py): slow paths compiled out, */
+#define MPJ_ANYG(c) 1 /* general paths of the optional wave-uniform fast paths kept                   */
 #else
-#define MPJ_ANY(c) __any((int)(c))
+#define MPJ_ANY(c) __any((int)(c))  /* wave-uniform: some lane needs the exact slow path */
+#define MPJ_ANYG(c) __any((int)(c)) /* wave-uniform: some lane needs the general path    */
 #endif
 __device__ __forceinline__ double mpj_sel(int c, double t, double f) {
   const unsigned long long m = __ballot(c);
@@ -564,6 +566,7 @@ __device__ __forceinline__ double mpj_sel(int c, double t, double f) {
 #define MPJ_SEL(c, t, f) mpj_sel((int)(c), (t), (f))
 #else
 #define MPJ_ANY(c) (c)
+#define MPJ_ANYG(c) (c)
 #define MPJ_SEL(c, t, f) ((c) ? (t) : (f))
 #endif
 
@@ -623,9 +626,9 @@ MPJ_FN double mpj_atan_tab(double x, const double* tab) {
   const uint32_t hx = mpj_hi(x);
   const uint32_t ix = hx & 0x7fffffffu;
   const int id = (ix >= 0x3fdc0000u) + (ix >= 0x3fe60000u) + (ix >= 0x3ff30000u) + (ix >= 0x40038000u);
+  const double a = mpj_fabs(x);
   const double* t = tab + 4 * id;
   const double na = t[0], nb = t[1], hi = t[2], lo = t[3];
-  const double a = mpj_fabs(x);
   const double ax = (na * a - nb) / (na + nb * a);
   const double z = ax * ax;
   const double w = z * z;

@@ -135,6 +135,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   const bool active = k < K;
   const int kk = active ? k : K - 1;
   MP_STAMP(0);
+  __builtin_amdgcn_s_setprio(3);
 
   const double* X0 = A.X0 + 7 * s;
   const double* goal = A.goal + 2 * s;
@@ -182,6 +183,15 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       const double z[2] = {zc.x, zc.y};
       if (j + 1 < H) zc = zrow[(size_t)(j + 1) * K];
       sample_ctrl(P, z, unom + 2 * j, u);
+      // Self-balancing issue priority: a wave's priority drops by one per quarter of the
+      // horizon it has completed, so the waves sharing a SIMD (oldest-first arbitration
+      // otherwise lets one run ahead and leaves the other to finish alone) end together.
+      if ((4 * j) % H < 4 && j > 0) {
+        const int q = (4 * j) / H;
+        if (q == 1) __builtin_amdgcn_s_setprio(2);
+        else if (q == 2) __builtin_amdgcn_s_setprio(1);
+        else if (q == 3) __builtin_amdgcn_s_setprio(0);
+      }
     };
     auto store = [&](int j, const double* u) {
       if (ush) ush[pair * ustr + 2 * j + side] = u[side];
@@ -347,7 +357,12 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   }
   __syncthreads();
   MP_STAMP(4);
-  // final TrajectoryRollout(MPPICtrl) — every pair runs it redundantly, pair 0 writes
+  // final TrajectoryRollout(MPPICtrl) on wave 0 only (its 32 pairs run it redundantly, all write
+  // the same values): the other waves leave, so the serial tail owns its SIMD instead of
+  // sharing it with an identical copy
+  for (int t = tid; t < H2; t += NT) A.U_out[(size_t)s * H2 + t] = Ush[t];
+  if (tid >= 64) return;
+  __builtin_amdgcn_s_setprio(3);  // the serial tail first on its SIMD
   {
     auto ctrl = [&](int j, double* u) { u[0] = Ush[2 * j]; u[1] = Ush[2 * j + 1]; };
     auto store = [&](int, const double*) {};
@@ -363,7 +378,6 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       if (c2 != c2 || rho != rho) atomicOr(A.flags, 1);
     }
   }
-  for (int t = tid; t < H2; t += NT) A.U_out[(size_t)s * H2 + t] = Ush[t];
   MP_STAMP(5);
 }
 

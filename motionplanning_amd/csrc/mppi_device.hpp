@@ -60,8 +60,12 @@ __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, 
   mpj_sincos_bl(psi, &sp, &cp);
   d[0] = uxc * cp - v * sp;
   d[1] = uxc * sp + v * cp;
-  d[2] = (FY1 + FY2) / M - r * uxc;
-  d[3] = (FY1 * la - FY2 * lb) / Izz;
+  // the two force divisions (:45-46) split across the pair: even lane (FY1+FY2)/M, odd lane
+  // (FY1*la - FY2*lb)/Izz, exchanged with one DPP swap (same operands, same bits)
+  const double q = (side ? FY1 * la - FY2 * lb : FY1 + FY2) / (side ? Izz : M);
+  const double qo = pair_swap(q);
+  d[2] = (side ? qo : q) - r * uxc;
+  d[3] = side ? q : qo;
   d[4] = r;
   d[5] = ax;
   d[6] = sr;
@@ -76,7 +80,7 @@ __device__ __forceinline__ double run_cost(const double* x, double sr, double ax
 // ObstacleEvaluation (MPPIUtils.jl:120-132) + occupancy grid (build extension).
 // Branch-free: `c = hit ? c + pen : c` is bit-identical to `if (hit) c = c + pen`.
 __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* x, const double* obs,
-                                                const unsigned char* grid, int* ok) {
+                                                const unsigned char* grid, int* ok, int side) {
   double c = 0.0;
   for (int o = 0; o < P.n_obs; o++) {
     const double dx = x[0] - obs[3 * o], dy = x[1] - obs[3 * o + 1], R = obs[3 * o + 2];
@@ -85,8 +89,10 @@ __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* 
     c = (hit ? c + P.obs_pen : c);
   }
   if (P.gnx > 0) {
-    const double fx = (x[0] - P.gx0) / P.gdx;
-    const double fy = (x[1] - P.gy0) / P.gdy;
+    // cell coordinates: even lane divides x, odd lane y, one DPP swap
+    const double f = (side ? x[1] - P.gy0 : x[0] - P.gx0) / (side ? P.gdy : P.gdx);
+    const double fo = pair_swap(f);
+    const double fx = side ? fo : f, fy = side ? f : fo;
     const int inb = fx >= 0.0 && fy >= 0.0 && fx < (double)P.gnx && fy < (double)P.gny;
     const int ix = inb ? (int)fx : 0, iy = inb ? (int)fy : 0;
     const int hit = inb && grid[iy * P.gnx + ix];
@@ -98,16 +104,18 @@ __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* 
 
 // BoundEvaluation, MPPIUtils.jl:135-151 (branch-free, same accumulation order)
 __device__ __forceinline__ double bound_cost(const MppiDev& P, const double* x, int* ok) {
+  int viol = 0;
   double c = 0.0;
 #pragma unroll
   for (int i = 0; i < 7; i++) {
     const int lo = x[i] < P.XL[i], hi = x[i] > P.XU[i];
-    *ok &= !(lo | hi);
+    viol |= lo | hi;
     const double vl = c + P.slack * __builtin_fabs(x[i] - P.XL[i]);
     c = lo ? vl : c;
     const double vh = c + P.slack * __builtin_fabs(x[i] - P.XU[i]);
     c = hi ? vh : c;
   }
+  *ok &= !viol;
   return c;
 }
 
@@ -214,7 +222,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     int okc = 1, okb = 1;
     double cc = 0.0, cb = 0.0;
     if (j > 0) {
-      cc = obstacle_cost(P, x, obs, grid, &okc);
+      cc = obstacle_cost(P, x, obs, grid, &okc, side);
       cb = bound_cost(P, x, &okb);
     }
     const double pc = run_cost(x, u[0], u[1]);
@@ -240,7 +248,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
   {  // terminal (:49-54): only the running cost of the extra RK2 step is used
     int okc = 1, okb = 1;
     const double pc = run_cost(x, 0.0, 0.0);
-    const double cc = obstacle_cost(P, x, obs, grid, &okc);
+    const double cc = obstacle_cost(P, x, obs, grid, &okc, side);
     const double cb = bound_cost(P, x, &okb);
     sum = sum + (pc + cb + cc);
     ok_all &= okc & okb;
