@@ -548,7 +548,10 @@ MPJ_FN double mpj_log(double x) {
  * On the device MPJ_SEL is a forced v_cndmask pair (hipcc otherwise re-forms
  * branches from nested ternaries).  Arguments outside the fast range of sincos
  * take the exact routine through a wave-uniform branch. */
-#if defined(__HIP_DEVICE_COMPILE__)
+/* MPJ_LANE_SAFE (set by kernels whose callers run these routines under divergent control
+ * flow, e.g. hastar.hip): no wave-level operations at all — per-lane slow-path branches and
+ * plain selects — so the result never depends on which lanes are active. */
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MPJ_LANE_SAFE)
 #if defined(MPJ_COUNT_HOT_PATH)
 #define MPJ_ANY(c) 0  /* instruction-count builds only (tools/isa_count.py): slow paths compiled out, */
 #define MPJ_ANYG(c) 1 /* general paths of the optional wave-uniform fast paths kept                   */
@@ -700,6 +703,17 @@ MPJ_FN double mpj_modpi(double a) {
   if (a < -MPJ_PI) a = a + MPJ_TWO_PI;
   else if (a > MPJ_PI) a = a - MPJ_TWO_PI;
   return a;
+}
+/* mpj_modpi without the fmod loop: for |a| < 4π, fmod(a, 2π) is a or a ∓ 2π exactly
+ * (Sterbenz), the rest is selects; |a| >= 4π and NaN take mpj_modpi (wave-uniform). */
+MPJ_FN double mpj_modpi_bl(double a) {
+  const double aa = mpj_fabs(a);
+  if (MPJ_ANY(!(aa < 2 * MPJ_TWO_PI))) return mpj_modpi(a);
+  double r = MPJ_SEL(aa >= MPJ_TWO_PI, a - __builtin_copysign(MPJ_TWO_PI, a), a);
+  r = MPJ_SEL(r == 0.0, 0.0, r);          /* copysign(0, 2π) */
+  r = MPJ_SEL(r < 0.0, r + MPJ_TWO_PI, r); /* Julia mod: result in [0, 2π] */
+  r = MPJ_SEL(r > MPJ_PI, r - MPJ_TWO_PI, r);
+  return MPJ_SEL(aa <= MPJ_PI, a, r);
 }
 /* Julia isless(a, b) for Float64: NaN sorts last, -0.0 < 0.0. */
 MPJ_FN int mpj_isless(double a, double b) {

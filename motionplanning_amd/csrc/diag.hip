@@ -4,6 +4,9 @@
 
 namespace {
 __global__ void math_kernel(int fn, long long n, const double* x, const double* y, double* out) {
+  __shared__ double atab[20];
+  if (threadIdx.x == 0) mpj_atan_tab_init(atab);
+  __syncthreads();
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const double a = x[i];
@@ -20,6 +23,12 @@ __global__ void math_kernel(int fn, long long n, const double* x, const double* 
     case 8: r = mpj_log(a); break;
     case 9: r = mpj_modpi(a); break;
     case 10: r = mpj_sqrt(a); break;
+    // branch-free device variants used by the hot kernels (must equal the exact routines)
+    case 11: r = mpj_modpi_bl(a); break;
+    case 12: r = mpj_atan_bl(a); break;
+    case 13: r = mpj_atan_tab(a, atab); break;
+    case 14: { double s, c; mpj_sincos_bl(a, &s, &c); r = s; break; }
+    case 15: { double s, c; mpj_sincos_bl(a, &s, &c); r = c; break; }
   }
   out[i] = r;
 }
@@ -27,7 +36,7 @@ __global__ void math_kernel(int fn, long long n, const double* x, const double* 
 
 extern "C" int mp_math_eval(mp_ctx* ctx, int32_t fn, int64_t n, const double* x, const double* y, double* out) {
   if (!ctx) return MP_ERR_INVALID;
-  MP_CHECK(ctx, fn >= 0 && fn <= 10 && n >= 0 && x && out && (fn != 4 || y), "bad mp_math_eval arguments");
+  MP_CHECK(ctx, fn >= 0 && fn <= 15 && n >= 0 && x && out && (fn != 4 || y), "bad mp_math_eval arguments");
   if (n == 0) return MP_OK;
   MP_HIP(ctx, hipSetDevice(ctx->device));
   int st = MP_OK;

@@ -6,15 +6,20 @@
 //                     Julia-argmin across the wave, the optimal command's 100-steps-per-
 //                     segment Euler path (heading recurrence and x/y running sums on one
 //                     lane, trigonometry on all lanes), then the SAT sweep of its poses.
-//   block (s, 1+k)    FindNewNode neighbour k: transform + regulate + Encode, the 50-pose
-//                     SAT collision sweep across lanes, and for a collision-free neighbour
-//                     the 48-candidate rs_heuristic across lanes.
+//   block (s, 1+g)    FindNewNode for neighbours 16g..16g+15: transform + regulate + Encode
+//                     on 16 lanes, the (neighbour, pose) SAT collision sweep across all
+//                     lanes, then the 48-candidate rs_heuristic of all 16 neighbours at once
+//                     (lanes 4j..4j+3 = the four variants of neighbour j, word loop uniform).
 // The open list / Dict bookkeeping of planHybridAstar! runs on the host (mp_ha_plan).
 #include <algorithm>
 #include <cmath>
+#include <queue>
 #include <unordered_map>
 #include <vector>
 
+// the libm routines run under divergent control flow here (per-lane early returns, partial
+// pose loops): lane-safe variants, no wave-level ballots inside them
+#define MPJ_LANE_SAFE 1
 #include "../../include/mp_jlmath.h"
 #include "runtime.hpp"
 
@@ -22,13 +27,21 @@ namespace {
 
 constexpr int MAXW = 16;    // walls per scene held in LDS
 constexpr int MAXPATH = 501;
+constexpr int NBG = 16;     // neighbours per expansion block (4 lanes = 4 RS variants each)
 #define PI2 (MPJ_PI / 2)
 #ifdef HA_DEBUG
 // phase markers to host-mapped memory (tools/ha_dbg.cpp polls them while the kernel runs)
 __device__ int* g_ha_dbg;
 #define HMARK(ph) __hip_atomic_store(g_ha_dbg + (blockIdx.x * 64 + threadIdx.x), (ph), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+// phase timestamps (s_memtime) of block b at [b][16] after the 64x64 marker area
+#define HTIME(i)                                                                                   \
+  do {                                                                                             \
+    if (threadIdx.x == 0)                                                                          \
+      reinterpret_cast<unsigned long long*>(g_ha_dbg + 64 * 64)[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define HMARK(ph)
+#define HTIME(i)
 #endif
 
 struct HaDev {
@@ -49,71 +62,92 @@ struct Cmd {
   double tr[5], ge[5], st[5];
 };
 
+// The two polar forms every RS word starts from (ReedsSheppsUtils.jl path1..12):
+// A = polar(x - sin p, y - 1 + cos p), B = polar(x + sin p, y - 1 - cos p).  Computed once
+// per candidate variant instead of once per word (same operands, same bits).
+struct RsPre {
+  double p, rA, tA, rB, tB;
+};
+__device__ __forceinline__ RsPre rs_pre(const double* q) {
+  double sp, cp;
+  mpj_sincos_bl(q[2], &sp, &cp);
+  RsPre R;
+  R.p = q[2];
+  polar(q[0] - sp, q[1] - 1 + cp, &R.rA, &R.tA);
+  polar(q[0] + sp, q[1] - 1 - cp, &R.rB, &R.tB);
+  return R;
+}
+
 __device__ __forceinline__ double fin(double t, double u, double v, double cost) {
   if ((t < 0) || (v < 0) || (u < 0)) return __builtin_inf();
   return cost;
 }
 
 // path1..path12 (ReedsSheppsUtils.jl:48-380); identical operation order to oracle/or_hastar.c
-__device__ __forceinline__ double rs_path(int w, const double* s, Cmd* c) {
-  const double x = s[0], y = s[1], p = s[2];
+__device__ __forceinline__ double rs_path(int w, const RsPre& R, Cmd* c) {
+  const double p = R.p;
   double rho, th, t, u, v, a, cost;
   c->n = 0;
   switch (w) {
     case 1:
-      polar(x - mpj_sin(p), y - 1 + mpj_cos(p), &u, &t);
-      v = mpj_modpi(p - t);
+      u = R.rA;
+      t = R.tA;
+      v = mpj_modpi_bl(p - t);
       cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
       c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
       c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->st[0] = 1; c->st[1] = 0; c->st[2] = 1;
       return fin(t, u, v, cost);
     case 2:
-      polar(x + mpj_sin(p), y - 1 - mpj_cos(p), &rho, &th);
+      rho = R.rB;
+      th = R.tB;
       if (!(rho >= 2)) return __builtin_inf();
       u = mpj_sqrt(rho * rho - 4);
-      t = mpj_modpi(th + mpj_atan2(2, u));
-      v = mpj_modpi(t - p);
+      t = mpj_modpi_bl(th + mpj_atan2(2, u));
+      v = mpj_modpi_bl(t - p);
       cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
       c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
       c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->st[0] = 1; c->st[1] = 0; c->st[2] = -1;
       return fin(t, u, v, cost);
     case 3:
     case 4:
-      polar(x - mpj_sin(p), y - 1 + mpj_cos(p), &rho, &th);
+      rho = R.rA;
+      th = R.tA;
       if (!(rho <= 4)) return __builtin_inf();
       a = mpj_acos(rho / 4);
-      t = mpj_modpi(th + PI2 + a);
-      u = mpj_modpi(MPJ_PI - 2 * a);
-      v = (w == 3) ? mpj_modpi(p - t - u) : mpj_modpi(t + u - p);
+      t = mpj_modpi_bl(th + PI2 + a);
+      u = mpj_modpi_bl(MPJ_PI - 2 * a);
+      v = (w == 3) ? mpj_modpi_bl(p - t - u) : mpj_modpi_bl(t + u - p);
       cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
       c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
       c->st[0] = 1; c->st[1] = -1; c->st[2] = 1;
       c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = (w == 3) ? 1 : -1;
       return fin(t, u, v, cost);
     case 5:
-      polar(x - mpj_sin(p), y - 1 + mpj_cos(p), &rho, &th);
+      rho = R.rA;
+      th = R.tA;
       if (!(rho <= 4)) return __builtin_inf();
       u = mpj_acos(1 - (rho * rho) / 8);
       a = mpj_asin(2 * mpj_sin(u) / rho);
-      t = mpj_modpi(th + PI2 - a);
-      v = mpj_modpi(t - p - u);
+      t = mpj_modpi_bl(th + PI2 - a);
+      v = mpj_modpi_bl(t - p - u);
       cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
       c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
       c->st[0] = 1; c->st[1] = -1; c->st[2] = 1; c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = -1;
       return fin(t, u, v, cost);
     case 6:
-      polar(x + mpj_sin(p), y - 1 - mpj_cos(p), &rho, &th);
+      rho = R.rB;
+      th = R.tB;
       if (!(rho <= 4)) return __builtin_inf();
       if (rho <= 2) {
         a = mpj_acos((rho + 2) / 4);
-        t = mpj_modpi(th + PI2 + a);
-        u = mpj_modpi(a);
-        v = mpj_modpi(p - t + 2 * u);
+        t = mpj_modpi_bl(th + PI2 + a);
+        u = mpj_modpi_bl(a);
+        v = mpj_modpi_bl(p - t + 2 * u);
       } else {
         a = mpj_acos((rho - 2) / 4);
-        t = mpj_modpi(th + PI2 - a);
-        u = mpj_modpi(MPJ_PI - a);
-        v = mpj_modpi(p - t + 2 * u);
+        t = mpj_modpi_bl(th + PI2 - a);
+        u = mpj_modpi_bl(MPJ_PI - a);
+        v = mpj_modpi_bl(p - t + 2 * u);
       }
       cost = __builtin_fabs(t) + 2 * __builtin_fabs(u) + __builtin_fabs(v);
       c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = u; c->tr[3] = v;
@@ -121,13 +155,14 @@ __device__ __forceinline__ double rs_path(int w, const double* s, Cmd* c) {
       c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = -1; c->ge[3] = -1;
       return fin(t, u, v, cost);
     case 7: {
-      polar(x + mpj_sin(p), y - 1 - mpj_cos(p), &rho, &th);
+      rho = R.rB;
+      th = R.tB;
       const double u1 = (20 - rho * rho) / 16;
       if (!((rho <= 6) && (0 <= u1) && (u1 <= 1))) return __builtin_inf();
       u = mpj_acos(u1);
       a = mpj_asin(2 * mpj_sin(u) / rho);
-      t = mpj_modpi(th + PI2 + a);
-      v = mpj_modpi(t - p);
+      t = mpj_modpi_bl(th + PI2 + a);
+      v = mpj_modpi_bl(t - p);
       cost = __builtin_fabs(t) + 2 * __builtin_fabs(u) + __builtin_fabs(v);
       c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = u; c->tr[3] = v;
       c->st[0] = 1; c->st[1] = -1; c->st[2] = 1; c->st[3] = -1;
@@ -135,58 +170,63 @@ __device__ __forceinline__ double rs_path(int w, const double* s, Cmd* c) {
       return fin(t, u, v, cost);
     }
     case 8:
-      polar(x - mpj_sin(p), y - 1 + mpj_cos(p), &rho, &th);
+      rho = R.rA;
+      th = R.tA;
       if (!(rho >= 2)) return __builtin_inf();
       u = mpj_sqrt(rho * rho - 4) - 2;
       a = mpj_atan2(2, u + 2);
-      t = mpj_modpi(th + PI2 + a);
-      v = mpj_modpi(t - p + PI2);
+      t = mpj_modpi_bl(th + PI2 + a);
+      v = mpj_modpi_bl(t - p + PI2);
       cost = __builtin_fabs(t) + PI2 + __builtin_fabs(u) + __builtin_fabs(v);
       c->n = 4; c->tr[0] = t; c->tr[1] = PI2; c->tr[2] = u; c->tr[3] = v;
       c->st[0] = 1; c->st[1] = -1; c->st[2] = 0; c->st[3] = 1;
       c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = -1; c->ge[3] = -1;
       return fin(t, u, v, cost);
     case 9:
-      polar(x - mpj_sin(p), y - 1 + mpj_cos(p), &rho, &th);
+      rho = R.rA;
+      th = R.tA;
       if (!(rho >= 2)) return __builtin_inf();
       u = mpj_sqrt(rho * rho - 4) - 2;
       a = mpj_atan2(u + 2, 2);
-      t = mpj_modpi(th + PI2 - a);
-      v = mpj_modpi(t - p - PI2);
+      t = mpj_modpi_bl(th + PI2 - a);
+      v = mpj_modpi_bl(t - p - PI2);
       cost = __builtin_fabs(t) + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
       c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = PI2; c->tr[3] = v;
       c->st[0] = 1; c->st[1] = 0; c->st[2] = -1; c->st[3] = 1;
       c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->ge[3] = -1;
       return fin(t, u, v, cost);
     case 10:
-      polar(x + mpj_sin(p), y - 1 - mpj_cos(p), &rho, &th);
+      rho = R.rB;
+      th = R.tB;
       if (!(rho >= 2)) return __builtin_inf();
-      t = mpj_modpi(th + PI2);
+      t = mpj_modpi_bl(th + PI2);
       u = rho - 2;
-      v = mpj_modpi(p - t - PI2);
+      v = mpj_modpi_bl(p - t - PI2);
       cost = __builtin_fabs(t) + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
       c->n = 4; c->tr[0] = t; c->tr[1] = PI2; c->tr[2] = u; c->tr[3] = v;
       c->st[0] = 1; c->st[1] = -1; c->st[2] = 0; c->st[3] = -1;
       c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = -1; c->ge[3] = -1;
       return fin(t, u, v, cost);
     case 11:
-      polar(x + mpj_sin(p), y - 1 - mpj_cos(p), &rho, &th);
+      rho = R.rB;
+      th = R.tB;
       if (!(rho >= 2)) return __builtin_inf();
-      t = mpj_modpi(th);
+      t = mpj_modpi_bl(th);
       u = rho - 2;
-      v = mpj_modpi(p - t - PI2);
+      v = mpj_modpi_bl(p - t - PI2);
       cost = __builtin_fabs(t) + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
       c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = PI2; c->tr[3] = v;
       c->st[0] = 1; c->st[1] = 0; c->st[2] = 1; c->st[3] = -1;
       c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->ge[3] = -1;
       return fin(t, u, v, cost);
     default:
-      polar(x + mpj_sin(p), y - 1 - mpj_cos(p), &rho, &th);
+      rho = R.rB;
+      th = R.tB;
       if (!(rho >= 4)) return __builtin_inf();
       u = mpj_sqrt(rho * rho - 4) - 4;
       a = mpj_atan2(2, u + 4);
-      t = mpj_modpi(th + PI2 + a);
-      v = mpj_modpi(t - p);
+      t = mpj_modpi_bl(th + PI2 + a);
+      v = mpj_modpi_bl(t - p);
       cost = __builtin_fabs(t) + PI2 + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
       c->n = 5; c->tr[0] = t; c->tr[1] = PI2; c->tr[2] = u; c->tr[3] = PI2; c->tr[4] = v;
       c->st[0] = 1; c->st[1] = -1; c->st[2] = 0; c->st[3] = 1; c->st[4] = -1;
@@ -221,12 +261,13 @@ __device__ __forceinline__ void rs_variant(const double* s, int var, double* q) 
 __device__ __forceinline__ double rs_best(const double* s, int lane, int* best_id, double* cm) {
   double q[3];
   rs_variant(s, lane & 3, q);
+  const RsPre R = rs_pre(q);
   double bc = __builtin_inf();
   int bi = 1 << 20;
 #pragma unroll 1
   for (int w = 1; w <= 12; w++) {
     Cmd c;
-    const double cost = rs_path(w, q, &c);
+    const double cost = rs_path(w, R, &c);
     const int id = 4 * (w - 1) + (lane & 3);
     if (rs_before(cost, id, bc, bi)) { bc = cost; bi = id; }
   }
@@ -244,7 +285,7 @@ __device__ __forceinline__ double rs_best(const double* s, int lane, int* best_i
     double qw[3];
     rs_variant(s, wv, qw);
     Cmd c;
-    const double cost = rs_path(bi / 4 + 1, qw, &c);
+    const double cost = rs_path(bi / 4 + 1, rs_pre(qw), &c);
     const int n = cost < __builtin_inf() ? c.n : 0;
     if (lane == 0) {
 #pragma unroll
@@ -269,7 +310,8 @@ __device__ __forceinline__ double rs_best(const double* s, int lane, int* best_i
 __device__ __forceinline__ void change_basis(const double* init, const double* term, double minR, double* out) {
   const double p0 = init[2], pg = term[2];
   const double dx = (term[0] - init[0]) / minR, dy = (term[1] - init[1]) / minR;
-  const double s0 = mpj_sin(p0), c0 = mpj_cos(p0);
+  double s0, c0;
+  mpj_sincos_bl(p0, &s0, &c0);
   out[0] = dx * c0 + dy * s0;
   out[1] = -dx * s0 + dy * c0;
   out[2] = pg - p0;
@@ -285,6 +327,8 @@ __device__ __forceinline__ void rect_pts(double ox, double oy, double c, double 
   }
 }
 
+// SeparatingAxisTheorem (CollisionDetection/src/utils.jl:37-62).  The fifth point of each
+// polygon repeats the first, so projecting 4 points gives the same min/max.
 __device__ __forceinline__ int sat(const double* base, const double* other) {
   for (int e = 0; e < 4; e++) {
     const double bx = base[2 * e], by = base[2 * e + 1];
@@ -292,7 +336,7 @@ __device__ __forceinline__ int sat(const double* base, const double* other) {
     const double nx = -vy, ny = vx;
     double mnb = 0, mxb = 0, mno = 0, mxo = 0;
 #pragma unroll
-    for (int j = 0; j < 5; j++) {
+    for (int j = 0; j < 4; j++) {
       const double db = (base[2 * j] - bx) * nx + (base[2 * j + 1] - by) * ny;
       const double dq = (other[2 * j] - bx) * nx + (other[2 * j + 1] - by) * ny;
       if (j == 0 || db < mnb) mnb = db;
@@ -305,34 +349,78 @@ __device__ __forceinline__ int sat(const double* base, const double* other) {
   return 0;
 }
 
-// vehicle pose q=[x,y,ψ] (rear axle) against all walls (corners in LDS); 1 = free
-__device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const double* wp, int nw) {
-  const double x = q[0] + P.L2 * mpj_cos(q[2]), y = q[1] + P.L2 * mpj_sin(q[2]);
-  const double yaw = mpj_modpi(q[2]);
+// SAT with a wall as the base polygon, its pose-independent part precomputed once per block:
+// per edge [bx, by, nx, ny, min, max] of the wall's own projections (same operations).
+__device__ __forceinline__ void sat_base_pre(const double* base, double* pre /* [4][6] */) {
+  for (int e = 0; e < 4; e++) {
+    const double bx = base[2 * e], by = base[2 * e + 1];
+    const double vx = base[2 * e + 2] - bx, vy = base[2 * e + 3] - by;
+    const double nx = -vy, ny = vx;
+    double mnb = 0, mxb = 0;
+    for (int j = 0; j < 4; j++) {
+      const double db = (base[2 * j] - bx) * nx + (base[2 * j + 1] - by) * ny;
+      if (j == 0 || db < mnb) mnb = db;
+      if (j == 0 || db > mxb) mxb = db;
+    }
+    double* o = pre + 6 * e;
+    o[0] = bx; o[1] = by; o[2] = nx; o[3] = ny; o[4] = mnb; o[5] = mxb;
+  }
+}
+__device__ __forceinline__ int sat_pre(const double* pre, const double* other) {
+  for (int e = 0; e < 4; e++) {
+    const double* o = pre + 6 * e;
+    const double bx = o[0], by = o[1], nx = o[2], ny = o[3], mnb = o[4], mxb = o[5];
+    double mno = 0, mxo = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const double dq = (other[2 * j] - bx) * nx + (other[2 * j + 1] - by) * ny;
+      if (j == 0 || dq < mno) mno = dq;
+      if (j == 0 || dq > mxo) mxo = dq;
+    }
+    if ((mxo <= mnb) || (mxb <= mno)) return 1;
+  }
+  return 0;
+}
+
+// vehicle pose q=[x,y,ψ] (rear axle) against all walls (corners wp and SAT tables wpre in
+// LDS); 1 = free
+__device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const double* wp, const double* wpre,
+                                         int nw) {
+  double sq, cq;
+  mpj_sincos_bl(q[2], &sq, &cq);
+  const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
+  const double yaw = mpj_modpi_bl(q[2]);
+  double sy = sq, cy = cq;
+  if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);  // |ψ| > π: the wrapped yaw's own sin/cos
   double vp[10];
-  rect_pts(x, y, mpj_cos(yaw), mpj_sin(yaw), P.L2, P.W2, vp);
+  rect_pts(x, y, cy, sy, P.L2, P.W2, vp);
   for (int i = 0; i < nw; i++)
-    if (!(sat(wp + 10 * i, vp) && sat(vp, wp + 10 * i))) return 0;
+    if (!(sat_pre(wpre + 24 * i, vp) && sat(vp, wp + 10 * i))) return 0;
   return 1;
 }
 
-__device__ __forceinline__ void transform1(const double* node, const double* q, double* o) {
-  const double th = node[2], c = mpj_cos(th), s = mpj_sin(th);
+// transform (hybrid_astar_utils.jl:459-481) with the node's cos/sin given
+__device__ __forceinline__ void transform_cs(const double* node, double c, double s, const double* q, double* o) {
   o[0] = q[0] * c - q[1] * s + node[0];
   o[1] = q[0] * s + q[1] * c + node[1];
-  o[2] = q[2] + th;
+  o[2] = q[2] + node[2];
+}
+__device__ __forceinline__ void transform1(const double* node, const double* q, double* o) {
+  double s, c;
+  mpj_sincos_bl(node[2], &s, &c);
+  transform_cs(node, c, s, q, o);
 }
 
 __device__ __forceinline__ void regulate(const HaDev& P, const double* s, double* o) {
   o[0] = mpj_round(s[0] / P.res[0]) * P.res[0];
   o[1] = mpj_round(s[1] / P.res[1]) * P.res[1];
-  const double psi = mpj_modpi(s[2]);
+  const double psi = mpj_modpi_bl(s[2]);
   o[2] = mpj_round(psi / P.res[2]) * P.res[2];
 }
 
 __device__ __forceinline__ long long encode(const HaDev& P, const double* s) {
   const double* b = P.sb;
-  double x = s[0], y = s[1], psi = mpj_modpi(s[2]);
+  double x = s[0], y = s[1], psi = mpj_modpi_bl(s[2]);
   x = __builtin_fmax(__builtin_fmin(x, b[1]), b[0]);
   y = __builtin_fmax(__builtin_fmin(y, b[3]), b[2]);
   psi = __builtin_fmax(__builtin_fmin(psi, b[5]), b[4]);
@@ -364,15 +452,54 @@ struct IterArgs {
   long long* idx;        // [B][n_prim]
   unsigned char* fr;     // [B][n_prim]
   double* h;             // [B][n_prim]
+  // record mode (mp_ha_plan): all per-iteration outputs of active slot i packed in one record
+  // at rec + i*rb (h[n_prim] | nb[n_prim][3] | idx[n_prim] | len | ok | fr[n_prim]), so one
+  // D2H copy of n_active records returns an iteration's results; rs_path by slot as well
+  char* rec;
+  int rb;
 };
+
+// output addressing: per scene (array mode) or per active slot (record mode)
+struct OutRef {
+  double* h;
+  double* nb;
+  long long* idx;
+  int* len;
+  unsigned char* ok;
+  unsigned char* fr;
+  double* path;
+};
+__device__ __forceinline__ OutRef out_ref(const IterArgs& A, int s, int slot, int n_prim) {
+  OutRef r;
+  if (A.rec) {
+    char* q = A.rec + (size_t)slot * A.rb;
+    r.h = (double*)q;
+    r.nb = r.h + n_prim;
+    r.idx = (long long*)(r.nb + 3 * n_prim);
+    r.len = (int*)(r.idx + n_prim);
+    r.ok = (unsigned char*)(r.len + 1);
+    r.fr = r.ok + 1;
+    r.path = A.rs_path + (size_t)slot * MAXPATH * 3;
+  } else {
+    r.h = A.h ? A.h + (size_t)s * n_prim : nullptr;
+    r.nb = A.nb ? A.nb + (size_t)s * n_prim * 3 : nullptr;
+    r.idx = A.idx ? A.idx + (size_t)s * n_prim : nullptr;
+    r.len = A.rs_len ? A.rs_len + s : nullptr;
+    r.ok = A.rs_ok ? A.rs_ok + s : nullptr;
+    r.fr = A.fr ? A.fr + (size_t)s * n_prim : nullptr;
+    r.path = A.rs_path ? A.rs_path + (size_t)s * MAXPATH * 3 : nullptr;
+  }
+  return r;
+}
 
 __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
   __shared__ double wp[MAXW * 10];
+  __shared__ double wpre[MAXW * 24];
   __shared__ double cmd[15];
   __shared__ double psi_s[101], ix_s[101], iy_s[101];
   __shared__ double path_s[MAXPATH * 3];
   __shared__ int sh_best;
-  const int per = 1 + P.n_prim;
+  const int per = 1 + (P.n_prim + NBG - 1) / NBG;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
   if (slot >= A.n_active) return;
   if (item == 0 && !A.do_rs) return;
@@ -380,6 +507,7 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
   const int s = A.scene_of[slot];
   const int lane = threadIdx.x;
   HMARK(1);
+  HTIME(0);
   const int nw = P.n_walls;
   const double* node = A.node + 3 * s;
   const double* goal = A.goal + 3 * s;
@@ -387,18 +515,22 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
   for (int i = lane; i < nw; i += 64) {
     const double* wl = A.walls + ((size_t)s * nw + i) * 5;
     rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], wp + 10 * i);
+    sat_base_pre(wp + 10 * i, wpre + 24 * i);
   }
   HMARK(5);
   __syncthreads();
   HMARK(6);
+  HTIME(1);
   if (item == 0) {
     // ------------------------------------------------ RS_connected
     double ns[3];
     change_basis(node, goal, P.minR, ns);
     HMARK(7);
+    HTIME(2);
     int best;
     rs_best(ns, lane, &best, cmd);
     HMARK(3);
+    HTIME(3);
     __syncthreads();
     int nseg = 0;
     for (int i = 0; i < 5; i++) {
@@ -406,7 +538,8 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
       nseg++;
     }
     HMARK(4);
-    double* path = A.rs_path + (size_t)s * MAXPATH * 3;
+    const OutRef R = out_ref(A, s, slot, P.n_prim);
+    double* path = R.path;
     double sx = node[0], sy = node[1], sp = node[2];
     if (lane == 0) { path_s[0] = sx; path_s[1] = sy; path_s[2] = sp; }
     for (int seg = 0; seg < nseg; seg++) {
@@ -425,7 +558,7 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
       // per-step increments (trigonometry on all lanes)
       for (int k = lane; k < 100; k += 64) {
         double sn, cs;
-        mpj_sincos(psi_s[k], &sn, &cs);
+        mpj_sincos_bl(psi_s[k], &sn, &cs);
         double d0 = v * cs, d1 = v * sn;
         d0 = d0 * P.minR;
         d1 = d1 * P.minR;
@@ -434,6 +567,7 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
       }
       __syncthreads();
       if (lane == 0) {
+#pragma unroll 10
         for (int k = 0; k < 100; k++) {
           sx = sx + ix_s[k];
           sy = sy + iy_s[k];
@@ -447,6 +581,7 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
       sy = __shfl(sy, 0);
       sp = psi_s[100];
       HMARK(10 + seg);
+      HTIME(4 + seg);
       __syncthreads();
     }
     const int n = 100 * nseg + 1;
@@ -455,52 +590,66 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
     // block_collision_check on poses 1:5:end (or the first column only)
     const int npose = n > 5 ? (n - 1) / 5 + 1 : 1;
     int freep = 1;
-    for (int j = lane; j < npose; j += 64) freep &= pose_free(P, path_s + 3 * (j * 5), wp, nw);
+    for (int j = lane; j < npose; j += 64) freep &= pose_free(P, path_s + 3 * (j * 5), wp, wpre, nw);
     HMARK(20);
+    HTIME(10);
     const int ok = !__any(!freep);
     if (lane == 0) {
-      A.rs_ok[s] = (unsigned char)ok;
-      A.rs_len[s] = n;
+      *R.ok = (unsigned char)ok;
+      *R.len = n;
     }
     return;
   }
-  // -------------------------------------------------- FindNewNode neighbour k
-  const int k = item - 1;
-  double t[3], nb[3];
-  transform1(node, A.sc + 3 * k, t);
-  regulate(P, t, nb);
-  const long long ix = encode(P, nb);
-  const size_t o = (size_t)s * P.n_prim + k;
-  if (lane == 0) {
-    A.nb[3 * o] = nb[0];
-    A.nb[3 * o + 1] = nb[1];
-    A.nb[3 * o + 2] = nb[2];
-    A.idx[o] = ix;
+  // ------------------------------- FindNewNode, neighbours k0 .. k0+15 (one 16-wide group)
+  const int k0 = (item - 1) * NBG, nk = min(NBG, P.n_prim - k0);
+  __shared__ double g_nb[NBG][3];
+  __shared__ long long g_ix[NBG];
+  __shared__ int g_free[NBG];
+  if (lane < nk) {  // transform + regulate_states + Encode (hybrid_astar_utils.jl:396-405)
+    const int k = k0 + lane;
+    double t[3], nb[3];
+    transform1(node, A.sc + 3 * k, t);
+    regulate(P, t, nb);
+    const long long ix = encode(P, nb);
+    const OutRef R = out_ref(A, s, slot, P.n_prim);
+    R.nb[3 * k] = nb[0];
+    R.nb[3 * k + 1] = nb[1];
+    R.nb[3 * k + 2] = nb[2];
+    R.idx[k] = ix;
+    g_nb[lane][0] = nb[0];
+    g_nb[lane][1] = nb[1];
+    g_nb[lane][2] = nb[2];
+    g_ix[lane] = ix;
+    g_free[lane] = 1;
   }
-  if (ix == 0) {
-    if (lane == 0) { A.fr[o] = 0; A.h[o] = 0.0; }
-    return;
-  }
-  // dg_cost -> block_collision_check on primitive poses 1:5:n_col
+  HTIME(11);
+  __syncthreads();
+  // dg_cost -> block_collision_check on primitive poses 1:5:n_col, (neighbour, pose) pairs on lanes
   const int npose = P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1;
-  int freep = 1;
-  for (int j = lane; j < npose; j += 64) {
+  double nsn, ncs;
+  mpj_sincos_bl(node[2], &nsn, &ncs);
+  for (int t = lane; t < nk * npose; t += 64) {
+    const int j = t / npose, jp = t - j * npose;
+    if (g_ix[j] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
     double q[3];
-    transform1(node, A.pc + ((size_t)k * P.n_col + j * 5) * 3, q);
-    freep &= pose_free(P, q, wp, nw);
+    transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + j) * P.n_col + jp * 5) * 3, q);
+    if (!pose_free(P, q, wp, wpre, nw)) g_free[j] = 0;  // benign race: every writer stores 0
   }
-  if (__any(!freep)) {
-    if (lane == 0) { A.fr[o] = 0; A.h[o] = 0.0; }
-    return;
-  }
-  // rs_heuristic
+  HTIME(12);
+  __syncthreads();
+  // rs_heuristic for all 16 neighbours at once: lanes 4j..4j+3 = the variants of neighbour j
+  const int j = lane >> 2;
+  const int jj = j < nk ? j : 0;
   double ns[3];
-  change_basis(nb, goal, P.minR, ns);
+  change_basis(g_nb[jj], goal, P.minR, ns);
   int best;
   const double cb = rs_best(ns, lane, &best, nullptr);
-  if (lane == 0) {
-    A.fr[o] = 1;
-    A.h[o] = cb * P.minR;
+  HTIME(13);
+  if ((lane & 3) == 0 && j < nk) {
+    const OutRef R = out_ref(A, s, slot, P.n_prim);
+    const int fr = g_ix[j] != 0 && g_free[j];
+    R.fr[k0 + j] = (unsigned char)fr;
+    R.h[k0 + j] = fr ? cb * P.minR : 0.0;
   }
 }
 
@@ -515,12 +664,13 @@ __global__ __launch_bounds__(64) void allpath_kernel(int B, const double* __rest
   if (live) { s[0] = ns[3 * b]; s[1] = ns[3 * b + 1]; s[2] = ns[3 * b + 2]; }
   double q[3];
   rs_variant(s, var, q);
+  const RsPre R = rs_pre(q);
   double bc = __builtin_inf();
   int bi = 1 << 20;
 #pragma unroll 1
   for (int w = 1; w <= 12; w++) {
     Cmd c;
-    const double cst = rs_path(w, q, &c);
+    const double cst = rs_path(w, R, &c);
     const int id = 4 * (w - 1) + var;
     if (rs_before(cst, id, bc, bi)) { bc = cst; bi = id; }
     if (live) {
@@ -580,7 +730,8 @@ int need_prims(mp_ctx* ctx, const mp_ha_params* p) {
 int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
   if (A.n_active <= 0) return MP_OK;
   mp_time_begin(ctx);
-  hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(A.n_active * (1 + D.n_prim))), dim3(64), 0, ctx->stream, D, A);
+  hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(A.n_active * (1 + (D.n_prim + NBG - 1) / NBG))), dim3(64), 0,
+                     ctx->stream, D, A);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
   return MP_OK;
@@ -757,43 +908,68 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * (size_t)B, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
-  double* dnode = (double*)mp_ws(ctx, WS_IO0, sizeof(double) * 3 * B);
-  int* dso = (int*)mp_ws(ctx, WS_IO1, sizeof(int) * B);
-  A.rs_ok = (unsigned char*)mp_ws(ctx, WS_IO2, B);
+  // one packed input region (nodes, scene map) and per-slot output records, mirrored in
+  // pinned host memory: one H2D and one D2H copy (n_active records) per search iteration
+  const size_t in_bytes = sizeof(double) * 3 * B + sizeof(int) * B;
+  const int rb = (int)((sizeof(double) * 5 * np + sizeof(int) + 1 + np + 15) & ~(size_t)15);
+  const size_t out_bytes = (size_t)B * rb;
+  char* din = (char*)mp_ws(ctx, WS_IO0, in_bytes);
+  char* dout = (char*)mp_ws(ctx, WS_IO1, out_bytes);
   A.rs_path = (double*)mp_ws(ctx, WS_IO3, sizeof(double) * B * MAXPATH * 3);
-  A.rs_len = (int*)mp_ws(ctx, WS_IO4, sizeof(int) * B);
-  A.nb = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 3 * np * B);
-  A.idx = (long long*)mp_ws(ctx, WS_IO6, sizeof(long long) * np * B);
-  A.fr = (unsigned char*)mp_ws(ctx, WS_IO7, (size_t)np * B);
-  A.h = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * np * B);
-  if (st || !dnode || !dso || !A.rs_ok || !A.rs_path || !A.rs_len || !A.nb || !A.idx || !A.fr || !A.h)
-    return st ? st : MP_ERR_NOMEM;
+  if (st || !din || !dout || !A.rs_path) return st ? st : MP_ERR_NOMEM;
+  double* dnode = (double*)din;
+  int* dso = (int*)(din + sizeof(double) * 3 * B);
+  A.rec = dout;
+  A.rb = rb;
   A.node = dnode;
   A.scene_of = dso;
   A.sc = ctx->ha_states_candi;
   A.pc = ctx->ha_paths_candi;
   A.do_rs = 1;
   A.do_exp = 1;
-  // pinned staging: nodes + scene map in, results out
-  const size_t in_bytes = sizeof(double) * 3 * B + sizeof(int) * B;
-  const size_t out_bytes = (size_t)B * (1 + sizeof(int) + sizeof(double) * 3 * np + sizeof(long long) * np + np +
-                                        sizeof(double) * np);
+  // pinned staging with the same packing
   char* pin = (char*)mp_pinned(ctx, in_bytes + out_bytes + 64);
   if (!pin) return mp_fail(ctx, MP_ERR_NOMEM, "pinned staging allocation failed");
   double* h_node = (double*)pin;
   int* h_so = (int*)(pin + sizeof(double) * 3 * B);
-  char* q = pin + in_bytes;
-  unsigned char* h_ok = (unsigned char*)q; q += B;
-  int* h_len = (int*)q; q += sizeof(int) * B;
-  double* h_nb = (double*)q; q += sizeof(double) * 3 * np * B;
-  long long* h_idx = (long long*)q; q += sizeof(long long) * np * B;
-  unsigned char* h_fr = (unsigned char*)q; q += (size_t)np * B;
-  double* h_h = (double*)q;
+  char* hout = pin + ((in_bytes + 63) & ~(size_t)63);
 
-  // per-scene search state (planHybridAstar!, hybrid_astar_utils.jl:235-296)
-  std::vector<std::vector<HNode>> nodes(B);
-  std::vector<std::unordered_map<long long, int>> dict(B);
-  std::vector<std::vector<int>> open(B);
+  // per-scene search state (planHybridAstar!, hybrid_astar_utils.jl:235-296).
+  // The reference re-sorts its open list every iteration with a stable sort on f
+  // (`sort!` + `popfirst!`, :242-244) and scans it linearly for membership (InOpen,
+  // :298-305).  The same order is kept here in a binary heap keyed by (f, seq): f by
+  // Julia `isless`, seq = the node's rank in the list order that the stable sort
+  // preserves among equal f — nodes already in the list keep their seq; at the end of an
+  // iteration the nodes whose f decreased in place get fresh seqs in their previous list
+  // order, then the nodes appended by push! (in push order).  Membership is a flag.
+  struct OpenKey {
+    double f;
+    long long seq;
+    int id;
+  };
+  struct After {  // priority_queue comparator: true if a comes after b
+    bool operator()(const OpenKey& a, const OpenKey& c) const {
+      if (mpj_isless(a.f, c.f)) return false;
+      if (mpj_isless(c.f, a.f)) return true;
+      return a.seq > c.seq;
+    }
+  };
+  struct Scene {
+    std::vector<HNode> nd;
+    std::vector<long long> seq;       // current key seq per node
+    std::vector<unsigned char> in_open;
+    std::vector<int> dict;  // nodes_collection: Encode index (1..ncell) -> node id, -1 = absent
+    int get(long long i) const { return (i >= 0 && i < (long long)dict.size()) ? dict[i] : -1; }
+    std::priority_queue<OpenKey, std::vector<OpenKey>, After> open;
+    long long ctr = 0;
+    size_t n_open = 0;
+  };
+  std::vector<Scene> sc(B);
+  // Encode range: 1 .. xnum*ynum*pnum (hybrid_astar_utils.jl:316-350)
+  const long long ncell = (long long)(mpj_round((p->stbound[1] - p->stbound[0]) / p->res[0]) + 1) *
+                          (long long)(mpj_round((p->stbound[3] - p->stbound[2]) / p->res[1]) + 1) *
+                          (long long)(mpj_round((p->stbound[5] - p->stbound[4]) / p->res[2]) + 1);
+  MP_CHECK(ctx, ncell > 0 && ncell < (1LL << 31), "state lattice too large (%lld cells)", ncell);
   std::vector<int> done(B, 0), cur(B, -1), loop(B, 0);
   std::vector<long long> start_index(B);
   for (int b = 0; b < B; b++) {
@@ -812,56 +988,69 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     long long si = (long long)((xid - 1) * ynum * pnum + (yid - 1) * pnum + pid);
     if (s0[0] < sbd[0] || s0[0] > sbd[1] || s0[1] < sbd[2] || s0[1] > sbd[3]) si = 0;
     start_index[b] = si;
-    nodes[b].push_back(HNode{-1, {s0[0], s0[1], s0[2]}, si, 0, 0, 0});
-    dict[b][si] = 0;
-    open[b].push_back(0);
+    Scene& S = sc[b];
+    S.nd.push_back(HNode{-1, {s0[0], s0[1], s0[2]}, si, 0, 0, 0});
+    S.seq.push_back(S.ctr);
+    S.in_open.push_back(1);
+    S.dict.assign((size_t)ncell + 1, -1);
+    if (si >= 0 && si <= ncell) S.dict[si] = 0;
+    S.open.push(OpenKey{0.0, S.ctr++, 0});
+    S.n_open = 1;
   }
-  auto less_f = [](const std::vector<HNode>& nd) {
-    return [&nd](int a, int c) { return (bool)mpj_isless(nd[a].f, nd[c].f); };
-  };
   std::vector<int> act;
+  std::vector<std::pair<OpenKey, int>> changed;  // (pre-iteration key, id) of in-place f updates
+  std::vector<int> appended;
   for (;;) {
     act.clear();
     for (int b = 0; b < B; b++) {
       if (done[b]) continue;
-      if (open[b].empty() || loop[b] >= mp) { done[b] = 1; continue; }
+      Scene& S = sc[b];
+      if (S.n_open == 0 || loop[b] >= mp) { done[b] = 1; continue; }
       loop[b]++;
-      std::stable_sort(open[b].begin(), open[b].end(), less_f(nodes[b]));
-      cur[b] = open[b].front();
-      open[b].erase(open[b].begin());
-      pop_seq[(size_t)b * mp + loop[b] - 1] = nodes[b][cur[b]].index;
+      for (;;) {  // popfirst! of the sorted list: the least live key
+        const OpenKey k = S.open.top();
+        S.open.pop();
+        if (S.in_open[k.id] && S.seq[k.id] == k.seq) { cur[b] = k.id; break; }
+      }
+      S.in_open[cur[b]] = 0;
+      S.n_open--;
+      pop_seq[(size_t)b * mp + loop[b] - 1] = S.nd[cur[b]].index;
       const int slot = (int)act.size();
       act.push_back(b);
-      for (int r = 0; r < 3; r++) h_node[3 * b + r] = nodes[b][cur[b]].st[r];
+      for (int r = 0; r < 3; r++) h_node[3 * b + r] = S.nd[cur[b]].st[r];
       h_so[slot] = b;
     }
     if (act.empty()) break;
     const int na = (int)act.size();
-    MP_HIP(ctx, hipMemcpyAsync(dnode, h_node, sizeof(double) * 3 * B, hipMemcpyHostToDevice, ctx->stream));
-    MP_HIP(ctx, hipMemcpyAsync(dso, h_so, sizeof(int) * na, hipMemcpyHostToDevice, ctx->stream));
+    MP_HIP(ctx, hipMemcpyAsync(din, h_node, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     A.n_active = na;
     if ((st = launch_iter(ctx, D, A))) return st;
-    MP_HIP(ctx, hipMemcpyAsync(h_ok, A.rs_ok, B, hipMemcpyDeviceToHost, ctx->stream));
-    MP_HIP(ctx, hipMemcpyAsync(h_len, A.rs_len, sizeof(int) * B, hipMemcpyDeviceToHost, ctx->stream));
-    MP_HIP(ctx, hipMemcpyAsync(h_nb, A.nb, sizeof(double) * 3 * np * B, hipMemcpyDeviceToHost, ctx->stream));
-    MP_HIP(ctx, hipMemcpyAsync(h_idx, A.idx, sizeof(long long) * np * B, hipMemcpyDeviceToHost, ctx->stream));
-    MP_HIP(ctx, hipMemcpyAsync(h_fr, A.fr, (size_t)np * B, hipMemcpyDeviceToHost, ctx->stream));
-    MP_HIP(ctx, hipMemcpyAsync(h_h, A.h, sizeof(double) * np * B, hipMemcpyDeviceToHost, ctx->stream));
+    MP_HIP(ctx, hipMemcpyAsync(hout, dout, (size_t)na * rb, hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    for (int b : act) {
-      std::vector<HNode>& nd = nodes[b];
-      if (h_ok[b]) {  // termination (:259-271)
+    for (int slot = 0; slot < na; slot++) {
+      const int b = act[slot];
+      const char* rq = hout + (size_t)slot * rb;  // this slot's record (see IterArgs::rec)
+      const double* h_h = (const double*)rq;
+      const double* h_nb = h_h + np;
+      const long long* h_idx = (const long long*)(h_nb + 3 * np);
+      const int h_len = *(const int*)(h_idx + np);
+      const unsigned char h_ok = *(const unsigned char*)((const int*)(h_idx + np) + 1);
+      const unsigned char* h_fr = (const unsigned char*)((const int*)(h_idx + np) + 1) + 1;
+      Scene& S = sc[b];
+      std::vector<HNode>& nd = S.nd;
+      if (h_ok) {  // termination (:259-271)
         found[b] = 1;
         done[b] = 1;
-        rs_len[b] = h_len[b];
-        MP_HIP(ctx, hipMemcpy(rs_path + (size_t)b * MAXPATH * 3, A.rs_path + (size_t)b * MAXPATH * 3,
-                              sizeof(double) * 3 * h_len[b], hipMemcpyDeviceToHost));
+        rs_len[b] = h_len;
+        MP_HIP(ctx, hipMemcpy(rs_path + (size_t)b * MAXPATH * 3, A.rs_path + (size_t)slot * MAXPATH * 3,
+                              sizeof(double) * 3 * h_len, hipMemcpyDeviceToHost));
         int c = cur[b], ns = 0;
         double* so = states_out + (size_t)b * mp * 3;
         for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
         ns++;
         while (nd[c].parent >= 0 && nd[c].index != start_index[b] && ns < mp) {
-          c = dict[b][nd[c].parent];
+          c = S.get(nd[c].parent);
+          if (c < 0) break;
           for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
           ns++;
         }
@@ -869,41 +1058,63 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         continue;
       }
       // FindNewNode bookkeeping (:418-446), neighbours in order
+      changed.clear();
+      appended.clear();
       const HNode cn = nd[cur[b]];
       for (int k = 0; k < np; k++) {
-        const size_t o = (size_t)b * np + k;
+        const size_t o = (size_t)k;
         if (h_idx[o] == 0 || !h_fr[o]) continue;
         const double tg = cn.g + p->expand_time;
         double th = std::fmax(h_h[o], 0.0);
         if (h_h[o] != h_h[o]) th = h_h[o];
         const double tf = tg + th;
-        auto it = dict[b].find(h_idx[o]);
+        const int hit = S.get(h_idx[o]);
         int id;
         bool upd = false;
-        if (it != dict[b].end()) {
-          id = it->second;
+        if (hit >= 0) {
+          id = hit;
           if (tg < nd[id].g) {
+            if (S.in_open[id] == 1) {  // first in-place update this iteration: remember the list position
+              changed.push_back({OpenKey{nd[id].f, S.seq[id], id}, id});
+              S.in_open[id] = 3;
+            }
             nd[id].g = tg; nd[id].h = th; nd[id].f = tf; nd[id].parent = cn.index;
             upd = true;
           }
         } else {
           id = (int)nd.size();
           nd.push_back(HNode{cn.index, {h_nb[3 * o], h_nb[3 * o + 1], h_nb[3 * o + 2]}, h_idx[o], tg, th, tf});
-          dict[b][h_idx[o]] = id;
+          S.seq.push_back(-1);
+          S.in_open.push_back(0);
+          if (h_idx[o] > 0 && h_idx[o] <= ncell) S.dict[h_idx[o]] = id;
           upd = true;
         }
-        if (upd) {
-          bool in = false;
-          for (int qd : open[b])
-            if (nd[qd].index == nd[id].index) { in = true; break; }
-          if (!in) open[b].push_back(id);
+        if (upd && !S.in_open[id]) {  // !InOpen -> push! (appended at the list end)
+          S.in_open[id] = 2;            // 2: appended this iteration
+          appended.push_back(id);
+          S.n_open++;
         }
+      }
+      // re-key: in-place updates in their previous list order (first update's old key), then appends
+      std::sort(changed.begin(), changed.end(), [](const std::pair<OpenKey, int>& u, const std::pair<OpenKey, int>& v) {
+        return After()(v.first, u.first);
+      });
+      for (const auto& ck : changed) {
+        const int id = ck.second;
+        S.in_open[id] = 1;
+        S.seq[id] = S.ctr++;
+        S.open.push(OpenKey{nd[id].f, S.seq[id], id});
+      }
+      for (int id : appended) {
+        S.in_open[id] = 1;
+        S.seq[id] = S.ctr++;
+        S.open.push(OpenKey{nd[id].f, S.seq[id], id});
       }
     }
   }
   for (int b = 0; b < B; b++) {
     pops[b] = loop[b];
-    n_nodes[b] = (int)nodes[b].size();
+    n_nodes[b] = (int)sc[b].nd.size();
   }
   return MP_OK;
 }

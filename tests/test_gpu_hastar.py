@@ -63,9 +63,11 @@ def test_driver_scene_plan_bitexact(ctx, scene, pops):
     assert np.array_equal(h.r.RSpath_final.T, ref["rs_path"])
 
 
-def test_scenario_batch_lockstep_bitexact(ctx):
-    """BASELINE cfg4 shape (perpendicular + parallel scenarios, seeded starts), 32 scenes in lockstep."""
-    hs = ha.scenario_batch(32, seed=4)
+@pytest.mark.parametrize("n,seed", [(32, 4), (96, 11)])
+def test_scenario_batch_lockstep_bitexact(ctx, n, seed):
+    """BASELINE cfg4 shape (perpendicular + parallel scenarios, seeded starts) in lockstep: found flag, pop
+    count, node count and the full pop sequence identical to the oracle's sort-every-iteration open list."""
+    hs = ha.scenario_batch(n, seed=seed)
     _, p, sc, pc = _setup(ctx)
     ha.plan_batch(hs, ctx=ctx)
     mism = 0

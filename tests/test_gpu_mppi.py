@@ -155,23 +155,26 @@ def test_plant_replay_mppi_csv(ctx):
 
 
 def test_jlmath_bitexact(ctx):
-    import ctypes
-
+    """Every device libm routine (exact FDLIBM restatements and the branch-free variants of the hot
+    kernels) equals the CPU build bit for bit, incl. range edges and the kπ/2 Cody-Waite points."""
     from motionplanning_amd.abi import ptr
 
     r = np.random.default_rng(0)
     ranges = {0: (-30, 30), 1: (-30, 30), 2: (-1.5, 1.5), 3: (-60, 60), 4: (-5, 5), 5: (-1, 1), 6: (-1, 1),
-              7: (-700, 700), 8: (1e-300, 1e4), 9: (-40, 40), 10: (0, 1e6)}
+              7: (-700, 700), 8: (1e-300, 1e4), 9: (-40, 40), 10: (0, 1e6), 11: (-15, 15), 12: (-60, 60),
+              13: (-60, 60), 14: (-10, 10), 15: (-10, 10)}
     names = {0: "sin", 1: "cos", 2: "tan", 3: "atan", 4: "atan2", 5: "asin", 6: "acos", 7: "exp", 8: "log",
-             9: "modpi"}
+             9: "modpi", 11: "modpi", 12: "atan", 13: "atan", 14: "sin", 15: "cos"}
+    edges = np.array([0.0, -0.0, 1e-300, -1e-300, 0.4375, 0.6875, 1.1875, 2.4375, np.pi / 4, np.pi / 2, np.pi,
+                      2 * np.pi, 3 * np.pi / 4, 4 * np.pi, -4 * np.pi, 1e5, -1e5] +  # |x| < 2^20 pi/2 (Cody-Waite domain)
+                     [np.nextafter(k * np.pi / 2, d) for k in range(-6, 7) for d in (-np.inf, np.inf)])
     for fn, (lo, hi) in ranges.items():
-        x = r.uniform(lo, hi, 20000)
-        y = r.uniform(-5, 5, 20000)
+        x = np.r_[r.uniform(lo, hi, 20000), edges if fn in (11, 12, 13, 14, 15) else []]
+        y = r.uniform(-5, 5, len(x))
         out = np.zeros_like(x)
         ctx.check(ctx.lib.mp_math_eval(ctx.handle, fn, len(x), ptr(x), ptr(y), ptr(out)))
         if fn == 10:
             assert np.array_equal(out, np.sqrt(x))
             continue
         cpu = np.array([oracle.m(names[fn], a, b) if fn == 4 else oracle.m(names[fn], a) for a, b in zip(x, y)])
-        assert np.array_equal(out, cpu), names[fn]
-    del ctypes
+        assert np.array_equal(out.view(np.int64), cpu.view(np.int64)), (fn, names[fn], x[out.view(np.int64) != cpu.view(np.int64)][:5])

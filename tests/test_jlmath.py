@@ -64,3 +64,16 @@ def test_branchless_variants_bitidentical():
             for fb, fe in (("sin_bl", "sin"), ("cos_bl", "cos")):
                 a, b = oracle.m(fb, x), oracle.m(fe, x)
                 assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], (fb, x)
+
+
+def test_modpi_branchless_bitidentical():
+    """mpj_modpi_bl (device fast path, no fmod loop) == mpj_modpi (Julia modπ)."""
+    r = np.random.default_rng(5)
+    tp = 2 * math.pi
+    xs = np.concatenate([r.uniform(-15, 15, 20000), r.uniform(-1e3, 1e3, 2000),
+                         [k * math.pi for k in range(-6, 7)] + [k * tp for k in range(-3, 4)],
+                         [np.nextafter(k * math.pi, d) for k in range(-5, 6) for d in (-np.inf, np.inf)],
+                         [0.0, -0.0, 1e-300, -1e-300, 4 * math.pi, -4 * math.pi, np.inf, -np.inf]])
+    for x in xs:
+        a, b = oracle.m("modpi_bl", float(x)), oracle.m("modpi", float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), x

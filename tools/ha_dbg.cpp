@@ -26,8 +26,8 @@ int main() {
   static double path[501 * 3];
   int len = 0;
   int* buf = nullptr;
-  hipHostMalloc((void**)&buf, 64 * 64 * sizeof(int), hipHostMallocMapped);
-  memset(buf, 0, 64 * 64 * sizeof(int));
+  hipHostMalloc((void**)&buf, 1 << 20, hipHostMallocMapped);
+  memset(buf, 0, 1 << 20);
   printf("dbg buf %d\n", mp_ha_debug_buf(buf));
   printf("launch\n");
   fflush(stdout);
@@ -40,7 +40,32 @@ int main() {
   fflush(stdout);
   if (st == -99) _exit(3);
   th.join();
+  {
+    const unsigned long long* t = reinterpret_cast<const unsigned long long*>(buf + 64 * 64);
+    printf("RS block phase cycles from start:");
+    for (int i = 1; i <= 10; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
+    printf("\n");
+  }
   printf("st %d ok %d len %d end %g %g %g\n", st, ok, len, path[3 * (len - 1)], path[3 * (len - 1) + 1], path[3 * (len - 1) + 2]);
+  {  // expand of the same node: block 1 (neighbours 0..15) phase times
+    double sc[62 * 3], pc[62 * 250 * 3];
+    double steer[31], gear[2] = {1, -1};
+    for (int i = 0; i < 31; i++) {
+      const double t = i / 30.0, a = -1 / p.minR, b = 1 / p.minR;
+      steer[i] = (1 - t) * a + t * b;
+    }
+    printf("prims %d\n", mp_ha_neighbor_origin(ctx, &p, 31, steer, 2, gear, sc, pc));
+    memset(buf, 0, 1 << 20);
+    double nb[62 * 3], hh[62];
+    int64_t idx[62];
+    uint8_t fr[62];
+    printf("expand %d\n", mp_ha_expand(ctx, &p, 1, node, goal, walls, nb, idx, fr, hh));
+    const unsigned long long* t = reinterpret_cast<const unsigned long long*>(buf + 64 * 64);
+    for (int blk = 1; blk <= 4; blk++)
+      printf("expand block %d: walls %lld encode %lld collision %lld heuristic %lld\n", blk,
+             (long long)(t[blk * 16 + 1] - t[blk * 16]), (long long)(t[blk * 16 + 11] - t[blk * 16 + 1]),
+             (long long)(t[blk * 16 + 12] - t[blk * 16 + 11]), (long long)(t[blk * 16 + 13] - t[blk * 16 + 12]));
+  }
   mp_ctx_destroy(ctx);
   return 0;
 }
