@@ -644,6 +644,44 @@ MPJ_FN double mpj_atan_tab(double x, const double* tab) {
   return MPJ_SEL(ix < 0x3e400000u, x, rb);
 }
 
+/* mpj_atan2 with the branch-free atan core (bit-identical: mpj_atan_bl == mpj_atan). */
+MPJ_FN double mpj_atan2_bl(double y, double x) {
+  const double pi_o_4 = 7.8539816339744827900E-01, pi_o_2 = 1.5707963267948965580E+00,
+               pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+  if (mpj_isnan(x) || mpj_isnan(y)) return x + y;
+  uint32_t hx = mpj_hi(x), lx = mpj_lo(x), hy = mpj_hi(y), ly = mpj_lo(y);
+  int32_t ix = (int32_t)(hx & 0x7fffffffu), iy = (int32_t)(hy & 0x7fffffffu);
+  if (hx == 0x3ff00000u && lx == 0) return mpj_atan_bl(y);
+  int m = (int)(((hy >> 31) & 1) | ((hx >> 30) & 2));
+  if ((iy | (int32_t)ly) == 0) {
+    if (m == 0 || m == 1) return y;
+    return m == 2 ? pi : -pi;
+  }
+  if ((ix | (int32_t)lx) == 0) return (hy >> 31) ? -pi_o_2 : pi_o_2;
+  if (ix == 0x7ff00000) {
+    if (iy == 0x7ff00000) {
+      if (m == 0) return pi_o_4;
+      if (m == 1) return -pi_o_4;
+      if (m == 2) return 3.0 * pi_o_4;
+      return -3.0 * pi_o_4;
+    }
+    if (m == 0) return 0.0;
+    if (m == 1) return -0.0;
+    if (m == 2) return pi;
+    return -pi;
+  }
+  if (iy == 0x7ff00000) return (hy >> 31) ? -pi_o_2 : pi_o_2;
+  int32_t k = (iy - ix) >> 20;
+  double z;
+  if (k > 60) { z = pi_o_2 + 0.5 * pi_lo; m &= 1; }
+  else if ((hx >> 31) && k < -60) z = 0.0;
+  else z = mpj_atan_bl(mpj_fabs(y / x));
+  if (m == 0) return z;
+  if (m == 1) return -z;
+  if (m == 2) return pi - (z - pi_lo);
+  return (z - pi_lo) - pi;
+}
+
 /* sin and cos for |x| <= ~9π/4 without a divergent branch (cw2c reduction, n in {0, ±1..±4}). */
 MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
   const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;

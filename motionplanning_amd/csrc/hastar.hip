@@ -12,6 +12,12 @@
 //                     (lanes 4j..4j+3 = the four variants of neighbour j, word loop uniform).
 // The open list / Dict bookkeeping of planHybridAstar! runs on the host (mp_ha_plan).
 #include <algorithm>
+#include <atomic>
+#include <functional>
+#include <thread>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <queue>
 #include <unordered_map>
@@ -54,7 +60,7 @@ struct HaDev {
 // ------------------------------------------------------------ Reeds–Shepp
 __device__ __forceinline__ void polar(double a, double b, double* r, double* th) {
   *r = mpj_sqrt(a * a + b * b);
-  *th = mpj_atan2(b, a);
+  *th = mpj_atan2_bl(b, a);
 }
 
 struct Cmd {
@@ -83,156 +89,109 @@ __device__ __forceinline__ double fin(double t, double u, double v, double cost)
   return cost;
 }
 
-// path1..path12 (ReedsSheppsUtils.jl:48-380); identical operation order to oracle/or_hastar.c
-__device__ __forceinline__ double rs_path(int w, const RsPre& R, Cmd* c) {
+// Reeds–Shepp words path1..path12 (ReedsSheppsUtils.jl:48-380): rs_word below.
+
+// One Reeds–Shepp word w (wave-uniform) as ONE straight-line program: each transcendental
+// (sqrt, acos, sin, asin, atan2) and the three modπ appear once, guarded by uniform branches
+// on w, with word-selected operands — the same operations on the same operands as the
+// reference words and oracle/or_hastar.c rs_path (bit-identical), but one copy of the code
+// instead of twelve inlined word bodies (which overflowed the instruction cache).
+__constant__ signed char kRsGe[12][5] = {{1, 1, 1}, {1, 1, 1}, {1, -1, 1}, {1, -1, -1}, {1, 1, -1},
+                                         {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, -1, -1}, {1, 1, 1, -1},
+                                         {1, -1, -1, -1}, {1, 1, 1, -1}, {1, -1, -1, -1, 1}};
+__constant__ signed char kRsSt[12][5] = {{1, 0, 1}, {1, 0, -1}, {1, -1, 1}, {1, -1, 1}, {1, -1, 1},
+                                         {1, -1, 1, -1}, {1, -1, 1, -1}, {1, -1, 0, 1}, {1, 0, -1, 1},
+                                         {1, -1, 0, -1}, {1, 0, 1, -1}, {1, -1, 0, 1, -1}};
+// command lengths as: 0 t, 1 u, 2 v, 3 π/2
+__constant__ signed char kRsTr[12][5] = {{0, 1, 2}, {0, 1, 2}, {0, 1, 2}, {0, 1, 2}, {0, 1, 2},
+                                         {0, 1, 1, 2}, {0, 1, 1, 2}, {0, 3, 1, 2}, {0, 1, 3, 2},
+                                         {0, 3, 1, 2}, {0, 1, 3, 2}, {0, 3, 1, 3, 2}};
+__constant__ signed char kRsN[12] = {3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 5};
+
+__device__ __forceinline__ double rs_word(int w_, const RsPre& R, Cmd* c) {
+  const int w = __builtin_amdgcn_readfirstlane(w_);  // wave-uniform word: scalar branches and table loads
   const double p = R.p;
-  double rho, th, t, u, v, a, cost;
-  c->n = 0;
-  switch (w) {
-    case 1:
-      u = R.rA;
-      t = R.tA;
-      v = mpj_modpi_bl(p - t);
-      cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
-      c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
-      c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->st[0] = 1; c->st[1] = 0; c->st[2] = 1;
-      return fin(t, u, v, cost);
-    case 2:
-      rho = R.rB;
-      th = R.tB;
-      if (!(rho >= 2)) return __builtin_inf();
-      u = mpj_sqrt(rho * rho - 4);
-      t = mpj_modpi_bl(th + mpj_atan2(2, u));
-      v = mpj_modpi_bl(t - p);
-      cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
-      c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
-      c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->st[0] = 1; c->st[1] = 0; c->st[2] = -1;
-      return fin(t, u, v, cost);
-    case 3:
-    case 4:
-      rho = R.rA;
-      th = R.tA;
-      if (!(rho <= 4)) return __builtin_inf();
-      a = mpj_acos(rho / 4);
-      t = mpj_modpi_bl(th + PI2 + a);
-      u = mpj_modpi_bl(MPJ_PI - 2 * a);
-      v = (w == 3) ? mpj_modpi_bl(p - t - u) : mpj_modpi_bl(t + u - p);
-      cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
-      c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
-      c->st[0] = 1; c->st[1] = -1; c->st[2] = 1;
-      c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = (w == 3) ? 1 : -1;
-      return fin(t, u, v, cost);
-    case 5:
-      rho = R.rA;
-      th = R.tA;
-      if (!(rho <= 4)) return __builtin_inf();
-      u = mpj_acos(1 - (rho * rho) / 8);
-      a = mpj_asin(2 * mpj_sin(u) / rho);
-      t = mpj_modpi_bl(th + PI2 - a);
-      v = mpj_modpi_bl(t - p - u);
-      cost = __builtin_fabs(t) + __builtin_fabs(u) + __builtin_fabs(v);
-      c->n = 3; c->tr[0] = t; c->tr[1] = u; c->tr[2] = v;
-      c->st[0] = 1; c->st[1] = -1; c->st[2] = 1; c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = -1;
-      return fin(t, u, v, cost);
-    case 6:
-      rho = R.rB;
-      th = R.tB;
-      if (!(rho <= 4)) return __builtin_inf();
-      if (rho <= 2) {
-        a = mpj_acos((rho + 2) / 4);
-        t = mpj_modpi_bl(th + PI2 + a);
-        u = mpj_modpi_bl(a);
-        v = mpj_modpi_bl(p - t + 2 * u);
-      } else {
-        a = mpj_acos((rho - 2) / 4);
-        t = mpj_modpi_bl(th + PI2 - a);
-        u = mpj_modpi_bl(MPJ_PI - a);
-        v = mpj_modpi_bl(p - t + 2 * u);
-      }
-      cost = __builtin_fabs(t) + 2 * __builtin_fabs(u) + __builtin_fabs(v);
-      c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = u; c->tr[3] = v;
-      c->st[0] = 1; c->st[1] = -1; c->st[2] = 1; c->st[3] = -1;
-      c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = -1; c->ge[3] = -1;
-      return fin(t, u, v, cost);
-    case 7: {
-      rho = R.rB;
-      th = R.tB;
-      const double u1 = (20 - rho * rho) / 16;
-      if (!((rho <= 6) && (0 <= u1) && (u1 <= 1))) return __builtin_inf();
-      u = mpj_acos(u1);
-      a = mpj_asin(2 * mpj_sin(u) / rho);
-      t = mpj_modpi_bl(th + PI2 + a);
-      v = mpj_modpi_bl(t - p);
-      cost = __builtin_fabs(t) + 2 * __builtin_fabs(u) + __builtin_fabs(v);
-      c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = u; c->tr[3] = v;
-      c->st[0] = 1; c->st[1] = -1; c->st[2] = 1; c->st[3] = -1;
-      c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = -1; c->ge[3] = 1;
-      return fin(t, u, v, cost);
-    }
-    case 8:
-      rho = R.rA;
-      th = R.tA;
-      if (!(rho >= 2)) return __builtin_inf();
-      u = mpj_sqrt(rho * rho - 4) - 2;
-      a = mpj_atan2(2, u + 2);
-      t = mpj_modpi_bl(th + PI2 + a);
-      v = mpj_modpi_bl(t - p + PI2);
-      cost = __builtin_fabs(t) + PI2 + __builtin_fabs(u) + __builtin_fabs(v);
-      c->n = 4; c->tr[0] = t; c->tr[1] = PI2; c->tr[2] = u; c->tr[3] = v;
-      c->st[0] = 1; c->st[1] = -1; c->st[2] = 0; c->st[3] = 1;
-      c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = -1; c->ge[3] = -1;
-      return fin(t, u, v, cost);
-    case 9:
-      rho = R.rA;
-      th = R.tA;
-      if (!(rho >= 2)) return __builtin_inf();
-      u = mpj_sqrt(rho * rho - 4) - 2;
-      a = mpj_atan2(u + 2, 2);
-      t = mpj_modpi_bl(th + PI2 - a);
-      v = mpj_modpi_bl(t - p - PI2);
-      cost = __builtin_fabs(t) + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
-      c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = PI2; c->tr[3] = v;
-      c->st[0] = 1; c->st[1] = 0; c->st[2] = -1; c->st[3] = 1;
-      c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->ge[3] = -1;
-      return fin(t, u, v, cost);
-    case 10:
-      rho = R.rB;
-      th = R.tB;
-      if (!(rho >= 2)) return __builtin_inf();
-      t = mpj_modpi_bl(th + PI2);
-      u = rho - 2;
-      v = mpj_modpi_bl(p - t - PI2);
-      cost = __builtin_fabs(t) + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
-      c->n = 4; c->tr[0] = t; c->tr[1] = PI2; c->tr[2] = u; c->tr[3] = v;
-      c->st[0] = 1; c->st[1] = -1; c->st[2] = 0; c->st[3] = -1;
-      c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = -1; c->ge[3] = -1;
-      return fin(t, u, v, cost);
-    case 11:
-      rho = R.rB;
-      th = R.tB;
-      if (!(rho >= 2)) return __builtin_inf();
-      t = mpj_modpi_bl(th);
-      u = rho - 2;
-      v = mpj_modpi_bl(p - t - PI2);
-      cost = __builtin_fabs(t) + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
-      c->n = 4; c->tr[0] = t; c->tr[1] = u; c->tr[2] = PI2; c->tr[3] = v;
-      c->st[0] = 1; c->st[1] = 0; c->st[2] = 1; c->st[3] = -1;
-      c->ge[0] = 1; c->ge[1] = 1; c->ge[2] = 1; c->ge[3] = -1;
-      return fin(t, u, v, cost);
-    default:
-      rho = R.rB;
-      th = R.tB;
-      if (!(rho >= 4)) return __builtin_inf();
-      u = mpj_sqrt(rho * rho - 4) - 4;
-      a = mpj_atan2(2, u + 4);
-      t = mpj_modpi_bl(th + PI2 + a);
-      v = mpj_modpi_bl(t - p);
-      cost = __builtin_fabs(t) + PI2 + __builtin_fabs(u) + PI2 + __builtin_fabs(v);
-      c->n = 5; c->tr[0] = t; c->tr[1] = PI2; c->tr[2] = u; c->tr[3] = PI2; c->tr[4] = v;
-      c->st[0] = 1; c->st[1] = -1; c->st[2] = 0; c->st[3] = 1; c->st[4] = -1;
-      c->ge[0] = 1; c->ge[1] = -1; c->ge[2] = -1; c->ge[3] = -1; c->ge[4] = 1;
-      return fin(t, u, v, cost);
+  const bool useA = (w == 1) | (w == 3) | (w == 4) | (w == 5) | (w == 8) | (w == 9);
+  const double rho = useA ? R.rA : R.rB, th = useA ? R.tA : R.tB;
+  const double r2 = rho * rho;
+  double sq = 0.0, ang = 0.0, ac = 0.0;
+  if (w == 2 || w == 8 || w == 9 || w == 12) sq = mpj_sqrt(r2 - 4);
+  double u;  // words 1, 2, 8-12: direct; 3-7: below
+  if (w == 1) u = rho;
+  else if (w == 2) u = sq;
+  else if (w == 8 || w == 9) u = sq - 2;
+  else if (w == 10 || w == 11) u = rho - 2;
+  else if (w == 12) u = sq - 4;
+  else u = 0.0;
+  const double u1 = (20 - r2) / 16;
+  if (w >= 3 && w <= 7) {
+    double arg;
+    if (w <= 4) arg = rho / 4;
+    else if (w == 5) arg = 1 - r2 / 8;
+    else if (w == 6) arg = rho <= 2 ? (rho + 2) / 4 : (rho - 2) / 4;
+    else arg = u1;
+    ac = mpj_acos(arg);
   }
+  if (w == 5 || w == 7) {
+    u = ac;
+    ang = mpj_asin(2 * mpj_sin(u) / rho);
+  } else if (w == 2 || w == 8 || w == 9 || w == 12) {
+    double y, x;
+    if (w == 2) { y = 2; x = u; }
+    else if (w == 8) { y = 2; x = u + 2; }
+    else if (w == 9) { y = u + 2; x = 2; }
+    else { y = 2; x = u + 4; }
+    ang = mpj_atan2_bl(y, x);
+  } else if (w >= 3 && w <= 6) {
+    ang = ac;
+  }
+  // t = modπ(targ)   (word 1: t = θ, and modπ(θ) == θ for θ = atan2(...) ∈ [-π, π])
+  double targ;
+  if (w == 1 || w == 11) targ = th;
+  else if (w == 2) targ = th + ang;
+  else if (w == 10) targ = th + PI2;
+  else if (w == 5 || w == 9 || (w == 6 && !(rho <= 2))) targ = th + PI2 - ang;
+  else targ = th + PI2 + ang;
+  const double t = mpj_modpi_bl(targ);
+  if (w == 3 || w == 4 || w == 6) {  // u = modπ(π - 2a) / modπ(a) / modπ(π - a)
+    const double uarg = (w == 6) ? (rho <= 2 ? ang : MPJ_PI - ang) : MPJ_PI - 2 * ang;
+    u = mpj_modpi_bl(uarg);
+  }
+  double varg;
+  if (w == 1 || w == 10 || w == 11) varg = (w == 1) ? p - t : p - t - PI2;
+  else if (w == 2 || w == 7 || w == 12) varg = t - p;
+  else if (w == 3) varg = p - t - u;
+  else if (w == 4) varg = t + u - p;
+  else if (w == 5) varg = t - p - u;
+  else if (w == 6) varg = p - t + 2 * u;
+  else if (w == 8) varg = t - p + PI2;
+  else varg = t - p - PI2;  // w == 9
+  const double v = mpj_modpi_bl(varg);
+  const double at = __builtin_fabs(t), au = __builtin_fabs(u), av = __builtin_fabs(v);
+  double cost;
+  if (w <= 5) cost = at + au + av;
+  else if (w <= 7) cost = at + 2 * au + av;
+  else if (w == 8) cost = at + PI2 + au + av;
+  else if (w <= 11) cost = at + au + PI2 + av;
+  else cost = at + PI2 + au + PI2 + av;
+  bool valid;
+  if (w == 1) valid = true;
+  else if (w == 2 || (w >= 8 && w <= 11)) valid = rho >= 2;
+  else if (w <= 6) valid = rho <= 4;
+  else if (w == 7) valid = (rho <= 6) && (0 <= u1) && (u1 <= 1);
+  else valid = rho >= 4;
+  {
+    const int wi = w - 1;
+    c->n = kRsN[wi];
+#pragma unroll
+    for (int r = 0; r < 5; r++) {
+      const int code = kRsTr[wi][r];
+      c->tr[r] = code == 0 ? t : code == 1 ? u : code == 2 ? v : PI2;
+      c->ge[r] = kRsGe[wi][r];
+      c->st[r] = kRsSt[wi][r];
+    }
+  }
+  return valid ? fin(t, u, v, cost) : __builtin_inf();
 }
 
 // Julia findmin order on (cost, candidate id): NaN first (lowest id among NaNs), else the
@@ -256,55 +215,6 @@ __device__ __forceinline__ void rs_variant(const double* s, int var, double* q) 
   if (var == 1) { q[0] = -q[0]; q[2] = -q[2]; }       // timeflip
   else if (var == 2) { q[1] = -q[1]; q[2] = -q[2]; }  // reflect
   else if (var == 3) { q[0] = -q[0]; q[1] = -q[1]; }  // reverse
-}
-
-__device__ __forceinline__ double rs_best(const double* s, int lane, int* best_id, double* cm) {
-  double q[3];
-  rs_variant(s, lane & 3, q);
-  const RsPre R = rs_pre(q);
-  double bc = __builtin_inf();
-  int bi = 1 << 20;
-#pragma unroll 1
-  for (int w = 1; w <= 12; w++) {
-    Cmd c;
-    const double cost = rs_path(w, R, &c);
-    const int id = 4 * (w - 1) + (lane & 3);
-    if (rs_before(cost, id, bc, bi)) { bc = cost; bi = id; }
-  }
-#pragma unroll
-  for (int o = 2; o >= 1; o >>= 1) {  // lanes 4j..4j+3 hold identical copies of variants 0..3
-    const double ov = __shfl_xor(bc, o);
-    const int oi = __shfl_xor(bi, o);
-    if (rs_before(ov, oi, bc, bi)) { bc = ov; bi = oi; }
-  }
-  *best_id = bi;
-  if (cm) {
-    // the winner's commands: re-evaluate its word (wave-uniform), apply the variant's
-    // gear / steer flips exactly as allpath does (-1 * x)
-    const int wv = bi & 3;
-    double qw[3];
-    rs_variant(s, wv, qw);
-    Cmd c;
-    const double cost = rs_path(bi / 4 + 1, rs_pre(qw), &c);
-    const int n = cost < __builtin_inf() ? c.n : 0;
-    if (lane == 0) {
-#pragma unroll
-      for (int r = 0; r < 5; r++) {
-        double ge = 0.0, st = 0.0, tr = 0.0;
-        if (r < n) {
-          tr = c.tr[r];
-          ge = c.ge[r];
-          st = c.st[r];
-          if (wv == 1 || wv == 3) ge = -1 * ge;
-          if (wv == 2 || wv == 3) st = -1 * st;
-        }
-        cm[r * 3 + 0] = tr;
-        cm[r * 3 + 1] = ge;
-        cm[r * 3 + 2] = st;
-      }
-    }
-  }
-  return bc;
 }
 
 __device__ __forceinline__ void change_basis(const double* init, const double* term, double minR, double* out) {
@@ -492,61 +402,157 @@ __device__ __forceinline__ OutRef out_ref(const IterArgs& A, int s, int slot, in
   return r;
 }
 
-__global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
+constexpr int HT = 256;   // threads per block of ha_iter_kernel (4 waves)
+constexpr int HW = HT / 64;
+
+// allpath + findmin split over the block's 4 waves: wave w evaluates words 3w+1..3w+3 for
+// its lanes' candidates (lane&3 = variant of the state in `s`), the per-wave winners are
+// combined in LDS in word order with the same total order (rs_before).  Every wave returns
+// the block-wide winner for its lanes; *best_id is the winning candidate id.
+__device__ __forceinline__ double rs_best_split(const double* s, int tid, int* best_id, double* sh_c, int* sh_i) {
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, var = lane & 3;
+  double q[3];
+  rs_variant(s, var, q);
+  const RsPre R = rs_pre(q);
+  HTIME(12);
+  double bc = __builtin_inf();
+  int bi = 1 << 20;
+#pragma unroll 1
+  for (int w = 3 * wave + 1; w <= 3 * wave + 3; w++) {
+    Cmd c;
+    const double cost = rs_word(w, R, &c);
+    const int id = 4 * (w - 1) + var;
+    if (rs_before(cost, id, bc, bi)) { bc = cost; bi = id; }
+  }
+#pragma unroll
+  for (int o = 2; o >= 1; o >>= 1) {
+    const double ov = __shfl_xor(bc, o);
+    const int oi = __shfl_xor(bi, o);
+    if (rs_before(ov, oi, bc, bi)) { bc = ov; bi = oi; }
+  }
+  HTIME(13);
+  sh_c[tid] = bc;
+  sh_i[tid] = bi;
+  __syncthreads();
+  double v = sh_c[lane];
+  int ix = sh_i[lane];
+  for (int w = 1; w < HW; w++) {
+    const double ov = sh_c[64 * w + lane];
+    const int oi = sh_i[64 * w + lane];
+    if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; }
+  }
+  *best_id = ix;
+  return v;
+}
+
+// the winner's commands (re-evaluated, wave-uniform) with allpath's gear/steer flips
+__device__ __forceinline__ void rs_commands(const double* s, int bi, double* cm) {
+  const int wv = __builtin_amdgcn_readfirstlane(bi & 3);
+  bi = __builtin_amdgcn_readfirstlane(bi);
+  double qw[3];
+  rs_variant(s, wv, qw);
+  Cmd c;
+  const double cost = rs_word(bi / 4 + 1, rs_pre(qw), &c);
+  const int n = cost < __builtin_inf() ? c.n : 0;
+#pragma unroll
+  for (int r = 0; r < 5; r++) {
+    double ge = 0.0, st = 0.0, tr = 0.0;
+    if (r < n) {
+      tr = c.tr[r];
+      ge = c.ge[r];
+      st = c.st[r];
+      if (wv == 1 || wv == 3) ge = -1 * ge;
+      if (wv == 2 || wv == 3) st = -1 * st;
+    }
+    cm[r * 3 + 0] = tr;
+    cm[r * 3 + 1] = ge;
+    cm[r * 3 + 2] = st;
+  }
+}
+
+__global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   __shared__ double wp[MAXW * 10];
   __shared__ double wpre[MAXW * 24];
   __shared__ double cmd[15];
   __shared__ double psi_s[101], ix_s[101], iy_s[101];
   __shared__ double path_s[MAXPATH * 3];
-  __shared__ int sh_best;
+  __shared__ double red_c[HT];
+  __shared__ int red_i[HT];
+  __shared__ double g_nb[NBG][3];
+  __shared__ long long g_ix[NBG];
+  __shared__ int g_free[NBG];
+  __shared__ int sh_n;
   const int per = 1 + (P.n_prim + NBG - 1) / NBG;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
   if (slot >= A.n_active) return;
   if (item == 0 && !A.do_rs) return;
   if (item > 0 && !A.do_exp) return;
+  const bool rs = item == 0;  // block-uniform role: RS_connected, else a 16-neighbour group
   const int s = A.scene_of[slot];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   HMARK(1);
   HTIME(0);
   const int nw = P.n_walls;
   const double* node = A.node + 3 * s;
   const double* goal = A.goal + 3 * s;
-  // wall corners (Block2Pts) in LDS
-  for (int i = lane; i < nw; i += 64) {
+  const OutRef R = out_ref(A, s, slot, P.n_prim);
+  const int k0 = rs ? 0 : (item - 1) * NBG, nk = rs ? 0 : min(NBG, P.n_prim - k0);
+  // wall corners (Block2Pts) and their SAT tables in LDS
+  for (int i = tid; i < nw; i += HT) {
     const double* wl = A.walls + ((size_t)s * nw + i) * 5;
     rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], wp + 10 * i);
     sat_base_pre(wp + 10 * i, wpre + 24 * i);
   }
-  HMARK(5);
-  __syncthreads();
+  if (tid < NBG) g_free[tid] = 1;
+  if (tid < nk) {  // transform + regulate_states + Encode of the group's neighbours (:396-405)
+    const int k = k0 + tid;
+    double t[3], nb[3];
+    transform1(node, A.sc + 3 * k, t);
+    regulate(P, t, nb);
+    const long long ix = encode(P, nb);
+    R.nb[3 * k] = nb[0];
+    R.nb[3 * k + 1] = nb[1];
+    R.nb[3 * k + 2] = nb[2];
+    R.idx[k] = ix;
+    g_nb[tid][0] = nb[0];
+    g_nb[tid][1] = nb[1];
+    g_nb[tid][2] = nb[2];
+    g_ix[tid] = ix;
+  }
   HMARK(6);
   HTIME(1);
-  if (item == 0) {
-    // ------------------------------------------------ RS_connected
-    double ns[3];
-    change_basis(node, goal, P.minR, ns);
-    HMARK(7);
-    HTIME(2);
-    int best;
-    rs_best(ns, lane, &best, cmd);
-    HMARK(3);
-    HTIME(3);
+  __syncthreads();
+  // allpath + findmin (one call site for both roles): RS_connected's optimal command from the
+  // popped node, or rs_heuristic of the 16 neighbours (lanes 4j..4j+3 = variants of neighbour j)
+  const int j = lane >> 2;
+  double ns[3];
+  if (rs) change_basis(node, goal, P.minR, ns);
+  else change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
+  HTIME(2);
+  int best;
+  const double cb = rs_best_split(ns, tid, &best, red_c, red_i);
+  HTIME(3);
+  int npose;
+  if (rs) {
+    // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment
+    {  // every thread evaluates the winner (no divergent region); thread 0 stores it
+      double cm[15];
+      rs_commands(ns, best, cm);
+      if (tid == 0)
+        for (int i = 0; i < 15; i++) cmd[i] = cm[i];
+    }
     __syncthreads();
     int nseg = 0;
     for (int i = 0; i < 5; i++) {
       if (cmd[i * 3 + 1] == 0) break;
       nseg++;
     }
-    HMARK(4);
-    const OutRef R = out_ref(A, s, slot, P.n_prim);
-    double* path = R.path;
     double sx = node[0], sy = node[1], sp = node[2];
-    if (lane == 0) { path_s[0] = sx; path_s[1] = sy; path_s[2] = sp; }
+    if (tid == 0) { path_s[0] = sx; path_s[1] = sy; path_s[2] = sp; }
     for (int seg = 0; seg < nseg; seg++) {
       const double dt = __builtin_fabs(cmd[seg * 3]) / 100;
       const double v = cmd[seg * 3 + 1], st = cmd[seg * 3 + 2];
-      // heading recurrence ψ_{k+1} = ψ_k + (st*v)*dt on one lane (adds only)
-      if (lane == 0) {
+      if (tid == 0) {  // heading recurrence ψ_{k+1} = ψ_k + (st*v)*dt (adds only)
         psi_s[0] = sp;
         double q = sp;
         for (int k = 0; k < 100; k++) {
@@ -555,18 +561,17 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
         }
       }
       __syncthreads();
-      // per-step increments (trigonometry on all lanes)
-      for (int k = lane; k < 100; k += 64) {
+      if (tid < 100) {  // per-step increments
         double sn, cs;
-        mpj_sincos_bl(psi_s[k], &sn, &cs);
+        mpj_sincos_bl(psi_s[tid], &sn, &cs);
         double d0 = v * cs, d1 = v * sn;
         d0 = d0 * P.minR;
         d1 = d1 * P.minR;
-        ix_s[k] = d0 * dt;
-        iy_s[k] = d1 * dt;
+        ix_s[tid] = d0 * dt;
+        iy_s[tid] = d1 * dt;
       }
       __syncthreads();
-      if (lane == 0) {
+      if (tid == 0) {  // running sums in order
 #pragma unroll 10
         for (int k = 0; k < 100; k++) {
           sx = sx + ix_s[k];
@@ -576,77 +581,50 @@ __global__ __launch_bounds__(64) void ha_iter_kernel(HaDev P, IterArgs A) {
           o[1] = sy;
           o[2] = psi_s[k + 1];
         }
+        ix_s[100] = sx;
+        iy_s[100] = sy;
       }
-      sx = __shfl(sx, 0);
-      sy = __shfl(sy, 0);
+      __syncthreads();
+      sx = ix_s[100];
+      sy = iy_s[100];
       sp = psi_s[100];
       HMARK(10 + seg);
       HTIME(4 + seg);
       __syncthreads();
     }
     const int n = 100 * nseg + 1;
-    __syncthreads();
-    for (int i = lane; i < 3 * n; i += 64) path[i] = path_s[i];
-    // block_collision_check on poses 1:5:end (or the first column only)
-    const int npose = n > 5 ? (n - 1) / 5 + 1 : 1;
-    int freep = 1;
-    for (int j = lane; j < npose; j += 64) freep &= pose_free(P, path_s + 3 * (j * 5), wp, wpre, nw);
-    HMARK(20);
-    HTIME(10);
-    const int ok = !__any(!freep);
-    if (lane == 0) {
-      *R.ok = (unsigned char)ok;
-      *R.len = n;
-    }
-    return;
+    for (int i = tid; i < 3 * n; i += HT) R.path[i] = path_s[i];
+    npose = n > 5 ? (n - 1) / 5 + 1 : 1;  // block_collision_check on poses 1:5:end
+    if (tid == 0) sh_n = n;
+  } else {
+    npose = P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1;  // dg_cost: primitive poses 1:5:n_col
   }
-  // ------------------------------- FindNewNode, neighbours k0 .. k0+15 (one 16-wide group)
-  const int k0 = (item - 1) * NBG, nk = min(NBG, P.n_prim - k0);
-  __shared__ double g_nb[NBG][3];
-  __shared__ long long g_ix[NBG];
-  __shared__ int g_free[NBG];
-  if (lane < nk) {  // transform + regulate_states + Encode (hybrid_astar_utils.jl:396-405)
-    const int k = k0 + lane;
-    double t[3], nb[3];
-    transform1(node, A.sc + 3 * k, t);
-    regulate(P, t, nb);
-    const long long ix = encode(P, nb);
-    const OutRef R = out_ref(A, s, slot, P.n_prim);
-    R.nb[3 * k] = nb[0];
-    R.nb[3 * k + 1] = nb[1];
-    R.nb[3 * k + 2] = nb[2];
-    R.idx[k] = ix;
-    g_nb[lane][0] = nb[0];
-    g_nb[lane][1] = nb[1];
-    g_nb[lane][2] = nb[2];
-    g_ix[lane] = ix;
-    g_free[lane] = 1;
-  }
-  HTIME(11);
-  __syncthreads();
-  // dg_cost -> block_collision_check on primitive poses 1:5:n_col, (neighbour, pose) pairs on lanes
-  const int npose = P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1;
-  double nsn, ncs;
-  mpj_sincos_bl(node[2], &nsn, &ncs);
-  for (int t = lane; t < nk * npose; t += 64) {
-    const int j = t / npose, jp = t - j * npose;
-    if (g_ix[j] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
+  // one collision sweep for both roles: (neighbour, pose) pairs or the RS path's poses
+  double nsn = 0.0, ncs = 1.0;
+  if (!rs) mpj_sincos_bl(node[2], &nsn, &ncs);
+  const int total = rs ? npose : nk * npose;
+  for (int t = tid; t < total; t += HT) {
+    const int jn = rs ? 0 : t / npose, jp = rs ? t : t - jn * npose;
+    if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
     double q[3];
-    transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + j) * P.n_col + jp * 5) * 3, q);
-    if (!pose_free(P, q, wp, wpre, nw)) g_free[j] = 0;  // benign race: every writer stores 0
+    if (rs) {
+      q[0] = path_s[3 * (jp * 5)];
+      q[1] = path_s[3 * (jp * 5) + 1];
+      q[2] = path_s[3 * (jp * 5) + 2];
+    } else {
+      transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
+    }
+    if (!pose_free(P, q, wp, wpre, nw)) g_free[jn] = 0;  // every writer stores 0
   }
-  HTIME(12);
+  HMARK(20);
+  HTIME(10);
   __syncthreads();
-  // rs_heuristic for all 16 neighbours at once: lanes 4j..4j+3 = the variants of neighbour j
-  const int j = lane >> 2;
-  const int jj = j < nk ? j : 0;
-  double ns[3];
-  change_basis(g_nb[jj], goal, P.minR, ns);
-  int best;
-  const double cb = rs_best(ns, lane, &best, nullptr);
-  HTIME(13);
-  if ((lane & 3) == 0 && j < nk) {
-    const OutRef R = out_ref(A, s, slot, P.n_prim);
+  if (rs) {
+    if (tid == 0) {
+      *R.ok = (unsigned char)g_free[0];
+      *R.len = sh_n;
+    }
+  } else if (tid < 64 && (lane & 3) == 0 && j < nk) {
     const int fr = g_ix[j] != 0 && g_free[j];
     R.fr[k0 + j] = (unsigned char)fr;
     R.h[k0 + j] = fr ? cb * P.minR : 0.0;
@@ -670,7 +648,7 @@ __global__ __launch_bounds__(64) void allpath_kernel(int B, const double* __rest
 #pragma unroll 1
   for (int w = 1; w <= 12; w++) {
     Cmd c;
-    const double cst = rs_path(w, R, &c);
+    const double cst = rs_word(w, R, &c);
     const int id = 4 * (w - 1) + var;
     if (rs_before(cst, id, bc, bi)) { bc = cst; bi = id; }
     if (live) {
@@ -730,7 +708,7 @@ int need_prims(mp_ctx* ctx, const mp_ha_params* p) {
 int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
   if (A.n_active <= 0) return MP_OK;
   mp_time_begin(ctx);
-  hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(A.n_active * (1 + (D.n_prim + NBG - 1) / NBG))), dim3(64), 0,
+  hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(A.n_active * (1 + (D.n_prim + NBG - 1) / NBG))), dim3(HT), 0,
                      ctx->stream, D, A);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
@@ -742,6 +720,84 @@ struct HNode {
   double st[3];
   long long index;
   double g, h, f;
+};
+
+// Fork-join pool for the per-scene host bookkeeping of mp_ha_plan: worker threads wait on a
+// generation counter (a short spin, then yield: the GPU phase between two joins is ~0.1 ms),
+// items are claimed in chunks from an atomic counter, each thread has its own scratch.
+template <class Scratch>
+class WorkPool {
+ public:
+  explicit WorkPool(int n) : n_(n), scratch_(n) {
+    for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { loop(t); });
+  }
+  ~WorkPool() {
+    quit_.store(true, std::memory_order_release);
+    gen_.fetch_add(1, std::memory_order_release);
+    for (auto& t : th_) t.join();
+  }
+  template <class F>
+  void run(int count, F&& f, bool each = false) {
+    each_ = each;
+    for (auto& sc : scratch_) sc.term.clear();
+    fn_ = [&f](int i, Scratch& sc) { f(i, sc); };
+    count_ = count;
+    next_.store(0, std::memory_order_relaxed);
+    done_.store(0, std::memory_order_relaxed);
+    gen_.fetch_add(1, std::memory_order_release);
+    work(0);
+    while (done_.load(std::memory_order_acquire) != n_ - 1) __builtin_ia32_pause();
+  }
+  // every thread t (0 = the caller) runs f(t, scratch[t]) once: static partitions with affinity
+  template <class F>
+  void run_each(F&& f) {
+    run(n_, [&f](int t, Scratch& sc) { f(t, sc); }, true);
+  }
+  int size() const { return n_; }
+  std::vector<std::pair<int, int>> terminated() const {
+    std::vector<std::pair<int, int>> all;
+    for (const auto& sc : scratch_) all.insert(all.end(), sc.term.begin(), sc.term.end());
+    return all;
+  }
+
+ private:
+  void loop(int t) {
+    unsigned long long seen = 0;
+    for (;;) {
+      unsigned long long g;
+      int spins = 0;
+      while ((g = gen_.load(std::memory_order_acquire)) == seen) {  // brief spin, then yield the core
+        if (++spins < 256) __builtin_ia32_pause();
+        else std::this_thread::yield();
+      }
+      seen = g;
+      if (quit_.load(std::memory_order_acquire)) return;
+      work(t);
+      done_.fetch_add(1, std::memory_order_release);
+    }
+  }
+  void work(int t) {
+    if (count_ == n_ && each_) {  // run_each: item t on thread t
+      fn_(t, scratch_[t]);
+      return;
+    }
+    constexpr int CH = 4;
+    for (;;) {
+      const int i = next_.fetch_add(CH, std::memory_order_relaxed);
+      if (i >= count_) break;
+      const int e = std::min(i + CH, count_);
+      for (int j = i; j < e; j++) fn_(j, scratch_[t]);
+    }
+  }
+  int n_;
+  std::vector<Scratch> scratch_;
+  std::vector<std::thread> th_;
+  std::function<void(int, Scratch&)> fn_;
+  int count_ = 0;
+  bool each_ = false;
+  std::atomic<int> next_{0}, done_{0};
+  std::atomic<unsigned long long> gen_{0};
+  std::atomic<bool> quit_{false};
 };
 
 }  // namespace
@@ -970,7 +1026,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                           (long long)(mpj_round((p->stbound[3] - p->stbound[2]) / p->res[1]) + 1) *
                           (long long)(mpj_round((p->stbound[5] - p->stbound[4]) / p->res[2]) + 1);
   MP_CHECK(ctx, ncell > 0 && ncell < (1LL << 31), "state lattice too large (%lld cells)", ncell);
-  std::vector<int> done(B, 0), cur(B, -1), loop(B, 0);
+  std::vector<int> done(B, 0), cur(B, -1), loop(B, 0), popped(B, 0), slot_of(B, -1);
   std::vector<long long> start_index(B);
   for (int b = 0; b < B; b++) {
     found[b] = 0;
@@ -1000,118 +1056,173 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   std::vector<int> act;
   std::vector<std::pair<OpenKey, int>> changed;  // (pre-iteration key, id) of in-place f updates
   std::vector<int> appended;
-  for (;;) {
-    act.clear();
-    for (int b = 0; b < B; b++) {
-      if (done[b]) continue;
-      Scene& S = sc[b];
-      if (S.n_open == 0 || loop[b] >= mp) { done[b] = 1; continue; }
-      loop[b]++;
-      for (;;) {  // popfirst! of the sorted list: the least live key
-        const OpenKey k = S.open.top();
-        S.open.pop();
-        if (S.in_open[k.id] && S.seq[k.id] == k.seq) { cur[b] = k.id; break; }
+  struct Scratch {
+    std::vector<std::pair<OpenKey, int>> changed;  // (pre-iteration key, id) of in-place f updates
+    std::vector<int> appended;
+    std::vector<std::pair<int, int>> term;         // (scene, slot) that terminated this iteration
+  };
+  const char* hout_c = hout;
+  auto book = [&](int slot, Scratch& W) {
+    const int b = act[slot];
+    const char* rq = hout_c + (size_t)slot * rb;  // this slot's record (see IterArgs::rec)
+    const double* h_h = (const double*)rq;
+    const double* h_nb = h_h + np;
+    const long long* h_idx = (const long long*)(h_nb + 3 * np);
+    const int h_len = *(const int*)(h_idx + np);
+    const unsigned char h_ok = *(const unsigned char*)((const int*)(h_idx + np) + 1);
+    const unsigned char* h_fr = (const unsigned char*)((const int*)(h_idx + np) + 1) + 1;
+    Scene& S = sc[b];
+    std::vector<HNode>& nd = S.nd;
+    if (h_ok) {  // termination (:259-271)
+      found[b] = 1;
+      done[b] = 1;
+      rs_len[b] = h_len;
+      W.term.push_back({b, slot});
+      int c = cur[b], ns = 0;
+      double* so = states_out + (size_t)b * mp * 3;
+      for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
+      ns++;
+      while (nd[c].parent >= 0 && nd[c].index != start_index[b] && ns < mp) {
+        c = S.get(nd[c].parent);
+        if (c < 0) break;
+        for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
+        ns++;
       }
-      S.in_open[cur[b]] = 0;
-      S.n_open--;
-      pop_seq[(size_t)b * mp + loop[b] - 1] = S.nd[cur[b]].index;
-      const int slot = (int)act.size();
-      act.push_back(b);
-      for (int r = 0; r < 3; r++) h_node[3 * b + r] = S.nd[cur[b]].st[r];
-      h_so[slot] = b;
+      n_states[b] = ns;
+      return;
     }
+    // FindNewNode bookkeeping (:418-446), neighbours in order
+    auto& changed = W.changed;
+    auto& appended = W.appended;
+    changed.clear();
+    appended.clear();
+    const HNode cn = nd[cur[b]];
+    for (int k = 0; k < np; k++) {
+      if (h_idx[k] == 0 || !h_fr[k]) continue;
+      const double tg = cn.g + p->expand_time;
+      double th = std::fmax(h_h[k], 0.0);
+      if (h_h[k] != h_h[k]) th = h_h[k];
+      const double tf = tg + th;
+      const int hit = S.get(h_idx[k]);
+      int id;
+      bool upd = false;
+      if (hit >= 0) {
+        id = hit;
+        if (tg < nd[id].g) {
+          if (S.in_open[id] == 1) {  // first in-place update this iteration: remember the list position
+            changed.push_back({OpenKey{nd[id].f, S.seq[id], id}, id});
+            S.in_open[id] = 3;
+          }
+          nd[id].g = tg; nd[id].h = th; nd[id].f = tf; nd[id].parent = cn.index;
+          upd = true;
+        }
+      } else {
+        id = (int)nd.size();
+        nd.push_back(HNode{cn.index, {h_nb[3 * k], h_nb[3 * k + 1], h_nb[3 * k + 2]}, h_idx[k], tg, th, tf});
+        S.seq.push_back(-1);
+        S.in_open.push_back(0);
+        if (h_idx[k] > 0 && h_idx[k] <= ncell) S.dict[h_idx[k]] = id;
+        upd = true;
+      }
+      if (upd && !S.in_open[id]) {  // !InOpen -> push! (appended at the list end)
+        S.in_open[id] = 2;            // 2: appended this iteration
+        appended.push_back(id);
+        S.n_open++;
+      }
+    }
+    // re-key: in-place updates in their previous list order (first update's old key), then appends
+    std::sort(changed.begin(), changed.end(), [](const std::pair<OpenKey, int>& u, const std::pair<OpenKey, int>& v) {
+      return After()(v.first, u.first);
+    });
+    for (const auto& ck : changed) {
+      const int id = ck.second;
+      S.in_open[id] = 1;
+      S.seq[id] = S.ctr++;
+      S.open.push(OpenKey{nd[id].f, S.seq[id], id});
+    }
+    for (int id : appended) {
+      S.in_open[id] = 1;
+      S.seq[id] = S.ctr++;
+      S.open.push(OpenKey{nd[id].f, S.seq[id], id});
+    }
+  };
+  // a small spin-synchronised pool for the per-scene bookkeeping (scenes are independent)
+  const int hw = (int)std::thread::hardware_concurrency();
+  const char* ev = getenv("MPGPU_HA_THREADS");
+  int nthreads = ev ? atoi(ev) : std::min(16, std::max(1, hw));
+  nthreads = std::max(1, std::min(nthreads, B / 16 > 0 ? B / 16 : 1));
+  WorkPool<Scratch> pool(nthreads);
+  static const bool prof = getenv("MPGPU_HA_PROFILE") != nullptr;  // host/device time split
+  double t_pop = 0, t_gpu = 0, t_book = 0;
+  long long n_iter = 0;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  // popfirst! of scene b (:242-244): the least live (f, seq) key; scene b always on pool thread
+  // b % T (with its bookkeeping), so its heap stays in that core's cache
+  auto pop = [&](int b) {
+    popped[b] = 0;
+    if (done[b]) return;
+    Scene& S = sc[b];
+    if (S.n_open == 0 || loop[b] >= mp) { done[b] = 1; return; }
+    loop[b]++;
+    for (;;) {
+      const OpenKey k = S.open.top();
+      S.open.pop();
+      if (S.in_open[k.id] && S.seq[k.id] == k.seq) { cur[b] = k.id; break; }
+    }
+    S.in_open[cur[b]] = 0;
+    S.n_open--;
+    pop_seq[(size_t)b * mp + loop[b] - 1] = S.nd[cur[b]].index;
+    for (int r = 0; r < 3; r++) h_node[3 * b + r] = S.nd[cur[b]].st[r];
+    popped[b] = 1;
+  };
+  bool first = true;
+  auto t_a = now();
+  for (;;) {
+    if (prof) t_a = now();
+    if (first) {  // the first popfirst! (later ones run with the previous iteration's bookkeeping)
+      pool.run_each([&](int t, Scratch&) {
+        for (int b = t; b < B; b += nthreads) pop(b);
+      });
+      first = false;
+    }
+    act.clear();
+    for (int b = 0; b < B; b++)
+      if (popped[b]) {
+        slot_of[b] = (int)act.size();
+        h_so[(int)act.size()] = b;
+        act.push_back(b);
+      }
     if (act.empty()) break;
     const int na = (int)act.size();
+    auto t_b = now();
     MP_HIP(ctx, hipMemcpyAsync(din, h_node, in_bytes, hipMemcpyHostToDevice, ctx->stream));
     A.n_active = na;
     if ((st = launch_iter(ctx, D, A))) return st;
     MP_HIP(ctx, hipMemcpyAsync(hout, dout, (size_t)na * rb, hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    for (int slot = 0; slot < na; slot++) {
-      const int b = act[slot];
-      const char* rq = hout + (size_t)slot * rb;  // this slot's record (see IterArgs::rec)
-      const double* h_h = (const double*)rq;
-      const double* h_nb = h_h + np;
-      const long long* h_idx = (const long long*)(h_nb + 3 * np);
-      const int h_len = *(const int*)(h_idx + np);
-      const unsigned char h_ok = *(const unsigned char*)((const int*)(h_idx + np) + 1);
-      const unsigned char* h_fr = (const unsigned char*)((const int*)(h_idx + np) + 1) + 1;
-      Scene& S = sc[b];
-      std::vector<HNode>& nd = S.nd;
-      if (h_ok) {  // termination (:259-271)
-        found[b] = 1;
-        done[b] = 1;
-        rs_len[b] = h_len;
-        MP_HIP(ctx, hipMemcpy(rs_path + (size_t)b * MAXPATH * 3, A.rs_path + (size_t)slot * MAXPATH * 3,
-                              sizeof(double) * 3 * h_len, hipMemcpyDeviceToHost));
-        int c = cur[b], ns = 0;
-        double* so = states_out + (size_t)b * mp * 3;
-        for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
-        ns++;
-        while (nd[c].parent >= 0 && nd[c].index != start_index[b] && ns < mp) {
-          c = S.get(nd[c].parent);
-          if (c < 0) break;
-          for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
-          ns++;
-        }
-        n_states[b] = ns;
-        continue;
+    auto t_c = now();
+    // bookkeeping per active scene (independent scenes: spread over the worker pool)
+    pool.run_each([&](int t, Scratch& W) {  // bookkeeping, then the next iteration's pop
+      for (int b = t; b < B; b += nthreads) {
+        if (popped[b]) book(slot_of[b], W);
+        pop(b);
       }
-      // FindNewNode bookkeeping (:418-446), neighbours in order
-      changed.clear();
-      appended.clear();
-      const HNode cn = nd[cur[b]];
-      for (int k = 0; k < np; k++) {
-        const size_t o = (size_t)k;
-        if (h_idx[o] == 0 || !h_fr[o]) continue;
-        const double tg = cn.g + p->expand_time;
-        double th = std::fmax(h_h[o], 0.0);
-        if (h_h[o] != h_h[o]) th = h_h[o];
-        const double tf = tg + th;
-        const int hit = S.get(h_idx[o]);
-        int id;
-        bool upd = false;
-        if (hit >= 0) {
-          id = hit;
-          if (tg < nd[id].g) {
-            if (S.in_open[id] == 1) {  // first in-place update this iteration: remember the list position
-              changed.push_back({OpenKey{nd[id].f, S.seq[id], id}, id});
-              S.in_open[id] = 3;
-            }
-            nd[id].g = tg; nd[id].h = th; nd[id].f = tf; nd[id].parent = cn.index;
-            upd = true;
-          }
-        } else {
-          id = (int)nd.size();
-          nd.push_back(HNode{cn.index, {h_nb[3 * o], h_nb[3 * o + 1], h_nb[3 * o + 2]}, h_idx[o], tg, th, tf});
-          S.seq.push_back(-1);
-          S.in_open.push_back(0);
-          if (h_idx[o] > 0 && h_idx[o] <= ncell) S.dict[h_idx[o]] = id;
-          upd = true;
-        }
-        if (upd && !S.in_open[id]) {  // !InOpen -> push! (appended at the list end)
-          S.in_open[id] = 2;            // 2: appended this iteration
-          appended.push_back(id);
-          S.n_open++;
-        }
-      }
-      // re-key: in-place updates in their previous list order (first update's old key), then appends
-      std::sort(changed.begin(), changed.end(), [](const std::pair<OpenKey, int>& u, const std::pair<OpenKey, int>& v) {
-        return After()(v.first, u.first);
-      });
-      for (const auto& ck : changed) {
-        const int id = ck.second;
-        S.in_open[id] = 1;
-        S.seq[id] = S.ctr++;
-        S.open.push(OpenKey{nd[id].f, S.seq[id], id});
-      }
-      for (int id : appended) {
-        S.in_open[id] = 1;
-        S.seq[id] = S.ctr++;
-        S.open.push(OpenKey{nd[id].f, S.seq[id], id});
-      }
+    });
+    for (const auto& tm : pool.terminated()) {  // RS path of scenes that terminated
+      MP_HIP(ctx, hipMemcpy(rs_path + (size_t)tm.first * MAXPATH * 3, A.rs_path + (size_t)tm.second * MAXPATH * 3,
+                            sizeof(double) * 3 * rs_len[tm.first], hipMemcpyDeviceToHost));
+    }
+    if (prof) {
+      const auto t_d = now();
+      t_pop += std::chrono::duration<double>(t_b - t_a).count();
+      t_gpu += std::chrono::duration<double>(t_c - t_b).count();
+      t_book += std::chrono::duration<double>(t_d - t_c).count();
+      n_iter++;
     }
   }
+  if (prof)
+    fprintf(stderr, "[mp_ha_plan] B=%d iterations %lld: host pop %.1f ms, launch+kernel+copies %.1f ms, host bookkeeping %.1f ms\n",
+            B, n_iter, t_pop * 1e3, t_gpu * 1e3, t_book * 1e3);
   for (int b = 0; b < B; b++) {
     pops[b] = loop[b];
     n_nodes[b] = (int)sc[b].nd.size();

@@ -38,6 +38,8 @@ def lib():
             f.argtypes = [_D]
         L.or_m_atan2.restype = _D
         L.or_m_atan2.argtypes = [_D, _D]
+        L.or_m_atan2_bl.restype = _D
+        L.or_m_atan2_bl.argtypes = [_D, _D]
         L.or_vehicle_dynamics.restype = _D
         L.or_vehicle_dynamics.argtypes = [_V, _V, _V]
         L.or_rollout.restype = _D

@@ -346,6 +346,7 @@ double or_m_log(double x) { return mpj_log(x); }
 double or_m_modpi(double x) { return mpj_modpi(x); }
 double or_m_atan_bl(double x) { return mpj_atan_bl(x); }
 double or_m_modpi_bl(double x) { return mpj_modpi_bl(x); }
+double or_m_atan2_bl(double y, double x) { return mpj_atan2_bl(y, x); }
 double or_m_atan_tab(double x) {
   static double tab[20];
   static int ready = 0;

@@ -77,3 +77,13 @@ def test_modpi_branchless_bitidentical():
     for x in xs:
         a, b = oracle.m("modpi_bl", float(x)), oracle.m("modpi", float(x))
         assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), x
+
+
+def test_atan2_branchless_core_bitidentical():
+    r = np.random.default_rng(6)
+    pts = list(r.uniform(-5, 5, (20000, 2))) + [(0.0, -1.0), (-0.0, -1.0), (1.0, 0.0), (-1.0, 0.0), (2.0, 1.0),
+                                                (1e-300, 1e300), (1e300, 1e-300), (np.inf, 1.0), (1.0, np.inf),
+                                                (np.inf, -np.inf), (3.0, 3.0), (-2.0, 2.0)]
+    for y, x in pts:
+        a, b = oracle.m("atan2_bl", float(y), float(x)), oracle.m("atan2", float(y), float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], (y, x)

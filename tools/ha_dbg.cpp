@@ -43,7 +43,7 @@ int main() {
   {
     const unsigned long long* t = reinterpret_cast<const unsigned long long*>(buf + 64 * 64);
     printf("RS block phase cycles from start:");
-    for (int i = 1; i <= 10; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
+    for (int i = 1; i <= 14; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
     printf("\n");
   }
   printf("st %d ok %d len %d end %g %g %g\n", st, ok, len, path[3 * (len - 1)], path[3 * (len - 1) + 1], path[3 * (len - 1) + 2]);
