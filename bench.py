@@ -5,7 +5,10 @@ S scenes per GPU (default 8 = the per-GPU shard of configs[4], "64 scenes sharde
 8xMI355X"); every scene is configs[1]: K=8192 rollouts, H=50 horizon steps, 7-state
 dynamic bicycle, 100x100 occupancy grid, device Philox noise, the full
 TrajectoryCollection (every rollout's trajectory and control list) written to HBM,
-weights + MPPICtrl + final rollout.  Two launches per step (noise, plan).  Inputs
+weights + MPPICtrl + final rollout.  Two launches per step (noise, plan) on the context stream + the final rollout of
+MPPICtrl on the side stream (final_stream=1; --final-inline keeps it in the plan kernel),
+so step i's serial final rollout overlaps step i+1's rollouts; every step's outputs are
+complete when the timed region's closing synchronize returns.  Inputs
 are resident in HBM before the timed region.  N>1: one process per GPU, each
 solves its own S scenes (weak scaling) and the ranks all-gather the optimal
 controls over RCCL (the north star's exchange step).  The single-scene
@@ -44,6 +47,8 @@ def parse():
     ap.add_argument("--no-single", action="store_true", help="skip the single-scene (configs[1]) line")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py) for roofline.traffic")
+    ap.add_argument("--final-inline", action="store_true",
+                    help="final rollout at the end of the plan kernel (final_stream=0) instead of the side stream")
     ap.add_argument("--no-extras", action="store_true", help="skip the iLQR (configs[2]) and Hybrid A* (configs[3]) lines")
     return ap.parse_args()
 
@@ -64,6 +69,7 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
     c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415)
     p = c["params"]
     p.scene_base = rank * S  # global scene ids: rank r plans scenes [rS, (r+1)S) of the job
+    p.final_stream = 0 if a.final_inline else 1  # final rollout on the side stream, overlapping the next step
     K, H = p.K, p.H
 
     def t(x, dt=torch.float64):
@@ -166,6 +172,8 @@ def main():
                         "H=50 dynamic bicycle, 2-D occupancy-grid cost, full TrajectoryCollection, weights + "
                         "MPPICtrl + final rollout)",
             "K": K, "H": H, "scenes_per_gpu": S, "feasibility_count": fc,
+            "final_rollout": "in plan kernel" if a.final_inline else
+                             "side stream (final_stream=1): overlaps the next step's rollouts",
             "parallelism": f"scene-sharded x{world}" + (" + RCCL all_gather(MPPICtrl)" if world > 1 else ""),
         },
         "roofline": {

@@ -48,8 +48,12 @@ int mp_ctx_destroy(mp_ctx* ctx);
 const char* mp_last_error(mp_ctx* ctx);
 const char* mp_version(void);
 int mp_device_count(int* n);
-/* Synchronise the context stream (after _dev calls). */
+/* Synchronise the context stream and its side stream (after _dev calls). */
 int mp_ctx_synchronize(mp_ctx* ctx);
+/* Order the context stream after all side-stream work enqueued so far (the deferred
+ * MPPI final rollouts, mp_mppi_params.final_stream = 1): consumers of traj_out /
+ * cost_out / feasible_out on the context stream call this first. */
+int mp_ctx_join(mp_ctx* ctx);
 /* The hipStream_t the context launches on (for HIP-event timing). */
 void* mp_ctx_stream(mp_ctx* ctx);
 /* Kernel timing: when enabled, every launch of the dominant kernel of a call
@@ -86,9 +90,14 @@ typedef struct mp_mppi_params {
   uint64_t seed;             /* Philox key                                      */
   uint64_t offset;           /* Philox counter word (advance per solve)         */
   int32_t scene_base;        /* global index of this call's scene 0 (Philox     */
-  int32_t reserved;          /*   counter word): a rank planning scenes [a,b)   */
+                             /*   counter word): a rank planning scenes [a,b)   */
                              /*   of a sharded batch passes a, so every scene   */
                              /*   draws the same stream at any world size       */
+  int32_t final_stream;      /* 0: the final TrajectoryRollout(MPPICtrl) runs   */
+                             /*   at the end of the plan kernel.  1: it runs on */
+                             /*   the context's side stream from a snapshot of  */
+                             /*   its inputs, overlapping the next call's       */
+                             /*   rollouts (see mp_mppi_plan_dev)               */
 } mp_mppi_params;
 
 /*
@@ -123,7 +132,13 @@ int mp_mppi_plan(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* 
                  int32_t* feasible_count_out, double* coll_traj, double* coll_ctrl,
                  double* coll_cost, uint8_t* coll_feas);
 
-/* Same contract, DEVICE pointers, asynchronous on the context stream. */
+/* Same contract, DEVICE pointers, asynchronous on the context stream.
+ * With p->final_stream = 1, U_out, rollout/feasible counts and the TrajectoryCollection
+ * are complete in context-stream order as usual, while traj_out, cost_out and
+ * feasible_out (the final rollout, MPPIUtils.jl:192-198) are written by the side stream:
+ * read them after mp_ctx_join() (stream order) or mp_ctx_synchronize().  The inputs may
+ * be overwritten as soon as the context stream has passed the call (the side stream
+ * works on a device snapshot).  The NaN check of the final cost is not reported. */
 int mp_mppi_plan_dev(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* X0,
                      const double* goal, const double* U_nom, const double* obstacles,
                      const uint8_t* grid, const double* noise, double* U_out, double* traj_out,

@@ -80,7 +80,7 @@ struct MppiParams
     seed::UInt64
     offset::UInt64
     scene_base::Int32
-    reserved::Int32
+    final_stream::Int32
 end
 
 """MppiParams from an MPPISearcher's settings (MPPI/src/types.jl:10-31, setup.jl:3-59)."""

@@ -70,7 +70,7 @@ class MPPIParams(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("offset", ctypes.c_uint64),
         ("scene_base", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("final_stream", ctypes.c_int32),
     ]
 
 
@@ -116,6 +116,7 @@ SIGNATURES = {
     "mp_version": (ctypes.c_char_p, []),
     "mp_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "mp_ctx_synchronize": (ctypes.c_int, [_V]),
+    "mp_ctx_join": (ctypes.c_int, [_V]),
     "mp_ctx_stream": (_V, [_V]),
     "mp_ctx_kernel_timing": (ctypes.c_int, [_V, ctypes.c_int]),
     "mp_ctx_kernel_ms": (ctypes.c_int, [_V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]),

@@ -456,14 +456,14 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
   const size_t n = (size_t)B * (D.N - 1);
   double* dD = (double*)mp_ws(ctx, WS_ILQR0, sizeof(double) * n * ND);
   if (!dD) return MP_ERR_NOMEM;
-  mp_time_begin(ctx);
+  mp_time_begin(ctx);  // the timed region covers both kernels of the backward pass
   hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
                      active, dD);
   MP_HIP(ctx, hipGetLastError());
-  mp_time_end(ctx);
   hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, dX, dD, active, dk,
                      dK);
   MP_HIP(ctx, hipGetLastError());
+  mp_time_end(ctx);
   return MP_OK;
 }
 
@@ -533,9 +533,11 @@ int mp_ilqr_forward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const doubl
   double* dUn = mp_alloc_out(ctx, WS_IO6, Unew, 2 * N * B, &st);
   double* dJ = mp_alloc_out(ctx, WS_IO7, Jnew, (size_t)B, &st);
   if (st) return st;
+  mp_time_begin(ctx);
   hipLaunchKernelGGL(ilqr_forward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, dX, dU, dk, dK, da,
                      dXn, dUn, dJ);
   MP_HIP(ctx, hipGetLastError());
+  mp_time_end(ctx);
   if ((st = mp_download(ctx, Xnew, (const double*)dXn, 4 * N * B))) return st;
   if ((st = mp_download(ctx, Unew, (const double*)dUn, 2 * N * B))) return st;
   if ((st = mp_download(ctx, Jnew, (const double*)dJ, (size_t)B))) return st;
@@ -573,9 +575,11 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   for (int outer = 0; outer <= D.max_iter + 1; outer++) {
     if ((st = run_backward(ctx, D, B, dX, dU, dact, dk, dK))) return st;
     MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
+    mp_time_begin(ctx);
     hipLaunchKernelGGL(ilqr_search_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit,
                        dfl, dn);
     MP_HIP(ctx, hipGetLastError());
+    mp_time_end(ctx);
     MP_HIP(ctx, hipMemcpyAsync(hn, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (*hn == 0) break;

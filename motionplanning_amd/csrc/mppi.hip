@@ -77,11 +77,35 @@ struct PlanArgs {
   int lds_unom, lds_obs, lds_grid;  // offsets (in doubles) into dynamic LDS; lds_grid < 0: grid stays in HBM
   int lds_ctrl, lds_part;           // control lists [RPB][2H+1] / staged partials (< 0: use HBM)
   unsigned long long* stamps;       // diagnostic build only (MPGPU_STAMPS=1): [grid][8] s_memrealtime
+  double* fin;                      // deferred final rollout: per-scene input snapshot (FinRec), or null
+  int fin_stride;                   // doubles per scene record
+};
+
+// Snapshot record of one scene for the deferred final rollout (final_stream = 1), in doubles:
+// [0, 2H) MPPICtrl | [2H, 4H) U_nom | X0[7] | goal[2] | obstacles[3 n_obs] | grid bytes
+struct FinRec {
+  int u, unom, x0, goal, obs, grid, stride;
+  __host__ __device__ FinRec(int H, int n_obs, int gbytes) {
+    u = 0;
+    unom = 2 * H;
+    x0 = 4 * H;
+    goal = x0 + 7;
+    obs = goal + 2;
+    grid = obs + 3 * n_obs;
+    stride = (grid + (gbytes + 7) / 8 + 1) & ~1;
+  }
 };
 
 #define MP_STAMP(i)                                                                  \
   do {                                                                               \
-    if (A.stamps && threadIdx.x == 0) A.stamps[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    if (A.stamps && threadIdx.x == 0) {                                              \
+      A.stamps[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memrealtime();            \
+      if ((i) == 0) {                                                                \
+        unsigned xcc;                                                                \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));           \
+        A.stamps[blockIdx.x * 32 + 30] = xcc;                                        \
+      }                                                                              \
+    }                                                                                \
   } while (0)
 // per-wave phase-1 end time [8 + w] and HW_ID (SIMD placement) [20 + w], diagnostic build only
 #define MP_STAMP_WAVE()                                                              \
@@ -357,10 +381,34 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   }
   __syncthreads();
   MP_STAMP(4);
+  for (int t = tid; t < H2; t += NT) A.U_out[(size_t)s * H2 + t] = Ush[t];
+  if (tid == 0) {
+    A.rc_out[s] = m + 1;
+    A.fc_out[s] = sh_fc;
+    A.tickets[s] = 0u;  // every block of this scene has arrived
+    if (rho != rho) atomicOr(A.flags, 1);
+  }
+  if (A.fin) {
+    // deferred final rollout (final_rollout_kernel on the side stream): snapshot its inputs
+    const FinRec R(H, P.n_obs, P.gnx * P.gny);
+    double* rec = A.fin + (size_t)s * A.fin_stride;
+    for (int t = tid; t < H2; t += NT) {
+      rec[R.u + t] = Ush[t];
+      rec[R.unom + t] = unom[t];
+    }
+    if (tid < 7) rec[R.x0 + tid] = X0[tid];
+    if (tid < 2) rec[R.goal + tid] = goal[tid];
+    for (int i = tid; i < 3 * P.n_obs; i += NT) rec[R.obs + i] = obs[i];
+    if (grid) {
+      unsigned char* rg = reinterpret_cast<unsigned char*>(rec + R.grid);
+      for (int i = tid; i < P.gnx * P.gny; i += NT) rg[i] = grid[i];
+    }
+    MP_STAMP(5);
+    return;
+  }
   // final TrajectoryRollout(MPPICtrl) on wave 0 only (its 32 pairs run it redundantly, all write
   // the same values): the other waves leave, so the serial tail owns its SIMD instead of
   // sharing it with an identical copy
-  for (int t = tid; t < H2; t += NT) A.U_out[(size_t)s * H2 + t] = Ush[t];
   if (tid >= 64) return;
   __builtin_amdgcn_s_setprio(3);  // the serial tail first on its SIMD
   {
@@ -372,13 +420,45 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     if (tid == 0) {
       A.cost_out[s] = c2;
       A.feas_out[s] = f2;
-      A.rc_out[s] = m + 1;
-      A.fc_out[s] = sh_fc;
-      A.tickets[s] = 0u;  // every block of this scene has arrived
-      if (c2 != c2 || rho != rho) atomicOr(A.flags, 1);
+      if (c2 != c2) atomicOr(A.flags, 1);
     }
   }
   MP_STAMP(5);
+}
+
+// Deferred final TrajectoryRollout(MPPICtrl) (MPPIUtils.jl:192-198), one wave per scene on the
+// context's side stream, from the FinRec snapshot the plan kernel's last block wrote: the
+// same rollout_pair as the in-kernel tail (bit-identical outputs), while the next call's
+// rollouts already occupy the rest of the GPU.
+__global__ __launch_bounds__(64) void final_rollout_kernel(MppiDev P, const double* fin, int fin_stride,
+                                                           int grid_lds, double* traj_out, double* cost_out,
+                                                           int* feas_out, int* flags) {
+  extern __shared__ double fsh[];
+  __shared__ double atab[20];
+  const int s = blockIdx.x, tid = threadIdx.x, side = tid & 1, H = P.H;
+  const FinRec R(H, P.n_obs, P.gnx * P.gny);
+  const double* rec = fin + (size_t)s * fin_stride;
+  const int nw = grid_lds ? R.stride : R.grid;  // the grid stays in the record when it does not fit
+  for (int i = tid; i < nw; i += 64) fsh[i] = rec[i];
+  if (tid == 0) mpj_atan_tab_init(atab);
+  __syncthreads();
+  // issue priority 0 (lowest): the serial chain fills the issue bubbles of the next call's
+  // rollout waves on its SIMD instead of delaying them (the plan kernel ends with its slowest
+  // SIMD); measured: prio 0 -> 354 us plan kernel, prio 3 -> 379 us (cfg2, 8 scenes)
+  const double* U = fsh + R.u;
+  auto ctrl = [&](int j, double* u) { u[0] = U[2 * j]; u[1] = U[2 * j + 1]; };
+  auto store = [&](int, const double*) {};
+  const unsigned char* grid =
+      P.gnx > 0 ? reinterpret_cast<const unsigned char*>((grid_lds ? fsh : rec) + R.grid) : nullptr;
+  const TrajOut traj{traj_out + (size_t)s * (H + 1) * 7, 7, 1};
+  int f2;
+  const double c2 = rollout_pair(P, fsh + R.x0, fsh + R.goal, P.n_obs > 0 ? fsh + R.obs : nullptr, grid,
+                                 fsh + R.unom, side, ctrl, store, traj, &f2, atab);
+  if (tid == 0) {
+    cost_out[s] = c2;
+    feas_out[s] = f2;
+    if (c2 != c2) atomicOr(flags, 1);
+  }
 }
 
 // ------------------------------------------------------------- mp_rollout
@@ -520,7 +600,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                        const double* U_nom, const double* obstacles, const uint8_t* grid, const double* noise,
                        double* U_out, double* traj_out, double* cost_out, int32_t* feasible_out,
                        int32_t* rc_out, int32_t* fc_out, double* coll_traj, double* coll_ctrl,
-                       double* coll_cost, uint8_t* coll_feas) {
+                       double* coll_cost, uint8_t* coll_feas, int final_stream) {
   const int K = D.K, H = D.H;
   // 8-wave blocks once the launch fills every CU with one (the dispatcher then places
   // exactly two waves per SIMD; with 4-wave blocks, two per CU, it can stack 3 + 1 and
@@ -595,11 +675,30 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                                     (int)kMaxLds));
     attr_set = true;
   }
+  // deferred final rollout: snapshot buffer of this call's parity, free once the final
+  // rollout of the call two back (same parity) is done
+  A.fin = nullptr;
+  A.fin_stride = 0;
+  int par = 0;
+  if (final_stream) {
+    int st2 = mp_side_init(ctx);
+    if (st2) return st2;
+    par = ctx->fin_par;
+    ctx->fin_par ^= 1;
+    const FinRec R(H, D.n_obs, D.gnx * D.gny);
+    A.fin_stride = R.stride;
+    A.fin = (double*)mp_ws(ctx, WS_FIN0 + par, sizeof(double) * (size_t)S * R.stride);
+    if (!A.fin) return MP_ERR_NOMEM;
+    // The host (not the context stream) waits for the final rollout two calls back to have
+    // read this buffer: it finished during the previous call's rollouts, and a cross-stream
+    // wait packet would stall the context stream between kernels instead.
+    MP_HIP(ctx, hipEventSynchronize(ctx->ev_fin[par]));
+  }
   A.stamps = nullptr;
   static const bool stamps_on = getenv("MPGPU_STAMPS") != nullptr;
   if (stamps_on) {
     A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA2, sizeof(unsigned long long) * 32 * S * nb);
-    MP_HIP(ctx, hipMemsetAsync(A.stamps, 0, sizeof(unsigned long long) * 8 * S * nb, ctx->stream));
+    MP_HIP(ctx, hipMemsetAsync(A.stamps, 0, sizeof(unsigned long long) * 32 * S * nb, ctx->stream));
   }
   mp_time_begin(ctx);
   if (BT == 512)
@@ -608,6 +707,24 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     hipLaunchKernelGGL(mppi_plan_kernel<256>, dim3(S * nb), dim3(256), shmem, ctx->stream, D, A);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
+  if (final_stream) {
+    const FinRec R(H, D.n_obs, D.gnx * D.gny);
+    const int grid_lds = (size_t)R.stride * 8 <= 64 * 1024;
+    const size_t fsh = sizeof(double) * (size_t)(grid_lds ? R.stride : R.grid);
+    MP_CHECK(ctx, fsh <= kMaxLds, "final rollout snapshot too large for LDS (%zu B)", fsh);
+    static bool fattr = false;
+    if (!fattr) {
+      MP_HIP(ctx, hipFuncSetAttribute((const void*)final_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kMaxLds));
+      fattr = true;
+    }
+    MP_HIP(ctx, hipEventRecord(ctx->ev_plan[par], ctx->stream));
+    MP_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_plan[par], 0));
+    hipLaunchKernelGGL(final_rollout_kernel, dim3(S), dim3(64), fsh, ctx->side, D, A.fin, A.fin_stride, grid_lds,
+                       traj_out, cost_out, feasible_out, ctx->flags);
+    MP_HIP(ctx, hipGetLastError());
+    MP_HIP(ctx, hipEventRecord(ctx->ev_fin[par], ctx->side));
+  }
   if (stamps_on) {
     std::vector<unsigned long long> h(32 * S * nb);
     MP_HIP(ctx, hipMemcpyAsync(h.data(), A.stamps, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -655,6 +772,23 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
       fprintf(stderr, " | wave-end p0/50/90/100 %.1f %.1f %.1f %.1f | blocks by max waves/SIMD 1:%d 2:%d 3:%d 4:%d",
               we[0], we[m / 2], we[m * 9 / 10], we[m - 1], hist[1], hist[2], hist[3], hist[4]);
     }
+    {  // per-XCC wave-end mean / max and block count
+      double sum[16] = {0}, mx[16] = {0};
+      int cnt[16] = {0}, nbk[16] = {0};
+      for (int b = 0; b < S * nb; b++) {
+        const int x = (int)(h[32 * b + 30] & 15);
+        nbk[x]++;
+        for (int w = 0; w < 8; w++) {
+          const unsigned long long tw = h[32 * b + 8 + w];
+          if (!tw) continue;
+          const double v = (tw - t0) / 100.0;
+          sum[x] += v; cnt[x]++; mx[x] = std::max(mx[x], v);
+        }
+      }
+      fprintf(stderr, " | xcc(blocks mean/max):");
+      for (int x = 0; x < 16; x++)
+        if (cnt[x]) fprintf(stderr, " %d(%d %.1f/%.1f)", x, nbk[x], sum[x] / cnt[x], mx[x]);
+    }
     if (last >= 0) {
       const unsigned long long* q = &h[32 * last];
       fprintf(stderr, " | last block: start+%.2f combine %.2f final-rollout %.2f | total %.2f", (q[0] - t0) / 100.0,
@@ -684,8 +818,10 @@ int mp_mppi_plan_dev(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const doub
   MP_CHECK(ctx, p->noise_mode != MP_NOISE_EXTERNAL || noise, "noise is NULL in MP_NOISE_EXTERNAL mode");
   MP_CHECK(ctx, p->n_obs == 0 || obstacles, "obstacles NULL with n_obs > 0");
   MP_CHECK(ctx, p->grid_nx == 0 || grid, "grid NULL with grid_nx > 0");
+  MP_CHECK(ctx, p->final_stream == 0 || p->final_stream == 1, "final_stream (%d) must be 0 or 1", p->final_stream);
   return plan_launch(ctx, D, S, X0, goal, U_nom, obstacles, grid, noise, U_out, traj_out, cost_out, feasible_out,
-                     rollout_count_out, feasible_count_out, coll_traj, coll_ctrl, coll_cost, coll_feas);
+                     rollout_count_out, feasible_count_out, coll_traj, coll_ctrl, coll_cost, coll_feas,
+                     p->final_stream);
 }
 
 int mp_mppi_plan(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* X0, const double* goal,
@@ -724,9 +860,11 @@ int mp_mppi_plan(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* 
   uint8_t* dcf = mp_alloc_out(ctx, WS_IO16, coll_feas, K * S, &st);
   if (st) return st;
   MP_HIP(ctx, hipMemsetAsync(ctx->flags, 0, sizeof(int), ctx->stream));
+  MP_CHECK(ctx, p->final_stream == 0 || p->final_stream == 1, "final_stream (%d) must be 0 or 1", p->final_stream);
   st = plan_launch(ctx, D, S, dX0, dgoal, dun, dobs, dgrid, dnoise, dU, dtraj, dcost, dfe, drc, dfc, dct, dcc,
-                   dco, dcf);
+                   dco, dcf, p->final_stream);
   if (st) return st;
+  if (p->final_stream && (st = mp_ctx_join(ctx))) return st;  // downloads below follow the side stream
   int flag = 0;
   if ((st = mp_download(ctx, U_out, dU, 2 * H * S))) return st;
   if ((st = mp_download(ctx, traj_out, dtraj, (H + 1) * 7 * S))) return st;

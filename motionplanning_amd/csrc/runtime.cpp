@@ -26,7 +26,7 @@ void* mp_ws(mp_ctx* ctx, int slot, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (ctx->ws_size[slot] >= bytes) return ctx->ws_ptr[slot];
   if (ctx->ws_ptr[slot]) {
-    hipStreamSynchronize(ctx->stream);
+    mp_sync_all(ctx);
     hipFree(ctx->ws_ptr[slot]);
     ctx->ws_ptr[slot] = nullptr;
     ctx->ws_size[slot] = 0;
@@ -45,7 +45,7 @@ void* mp_ws(mp_ctx* ctx, int slot, size_t bytes) {
 int mp_ticket_reserve(mp_ctx* ctx, int n) {
   if (ctx->n_tickets >= n) return MP_OK;
   if (ctx->tickets) {
-    hipStreamSynchronize(ctx->stream);
+    mp_sync_all(ctx);
     hipFree(ctx->tickets);
     ctx->tickets = nullptr;
   }
@@ -64,6 +64,23 @@ void* mp_pinned(mp_ctx* ctx, size_t bytes) {
   if (hipHostMalloc(&ctx->pinned, bytes, 0) != hipSuccess) return nullptr;
   ctx->pinned_size = bytes;
   return ctx->pinned;
+}
+
+void mp_sync_all(mp_ctx* ctx) {
+  hipStreamSynchronize(ctx->stream);
+  if (ctx->side) hipStreamSynchronize(ctx->side);
+}
+
+int mp_side_init(mp_ctx* ctx) {
+  if (ctx->side) return MP_OK;
+  MP_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  for (int i = 0; i < 2; i++) {
+    MP_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_plan[i], hipEventDisableTiming));
+    MP_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fin[i], hipEventDisableTiming));
+    MP_HIP(ctx, hipEventRecord(ctx->ev_fin[i], ctx->side));  // "buffer free" from the start
+  }
+  MP_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  return MP_OK;
 }
 
 static hipEvent_t next_event(mp_ctx* ctx) {
@@ -154,7 +171,7 @@ int mp_ctx_create(int device, mp_ctx** out) {
 int mp_ctx_destroy(mp_ctx* ctx) {
   if (!ctx) return MP_OK;
   hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
+  mp_sync_all(ctx);
   for (void* p : ctx->ws_ptr)
     if (p) hipFree(p);
   if (ctx->pinned) hipHostFree(ctx->pinned);
@@ -163,6 +180,12 @@ int mp_ctx_destroy(mp_ctx* ctx) {
   for (hipEvent_t e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->ha_states_candi) hipFree(ctx->ha_states_candi);
   if (ctx->ha_paths_candi) hipFree(ctx->ha_paths_candi);
+  for (int i = 0; i < 2; i++) {
+    if (ctx->ev_plan[i]) hipEventDestroy(ctx->ev_plan[i]);
+    if (ctx->ev_fin[i]) hipEventDestroy(ctx->ev_fin[i]);
+  }
+  if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
+  if (ctx->side) hipStreamDestroy(ctx->side);
   hipStreamDestroy(ctx->stream);
   delete ctx;
   return MP_OK;
@@ -176,6 +199,15 @@ const char* mp_last_error(mp_ctx* ctx) {
 int mp_ctx_synchronize(mp_ctx* ctx) {
   if (!ctx) return MP_ERR_INVALID;
   MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->side) MP_HIP(ctx, hipStreamSynchronize(ctx->side));
+  return MP_OK;
+}
+
+int mp_ctx_join(mp_ctx* ctx) {
+  if (!ctx) return MP_ERR_INVALID;
+  if (!ctx->side) return MP_OK;
+  MP_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->side));
+  MP_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
   return MP_OK;
 }
 

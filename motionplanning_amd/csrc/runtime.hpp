@@ -32,7 +32,17 @@ struct mp_ctx {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
+  // side stream of the deferred MPPI final rollout (mp_mppi_params.final_stream = 1):
+  // plan-done / final-done events per snapshot buffer (double-buffered by call parity)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_plan[2] = {nullptr, nullptr}, ev_fin[2] = {nullptr, nullptr}, ev_join = nullptr;
+  int fin_par = 0;
 };
+
+// Create the side stream and its events on first use.
+int mp_side_init(mp_ctx* ctx);
+// Wait for the context stream and (if created) the side stream.
+void mp_sync_all(mp_ctx* ctx);
 
 // Bracket a kernel launch with timing events when ctx->timing is on.
 void mp_time_begin(mp_ctx* ctx);
@@ -67,6 +77,8 @@ enum {
   WS_HA0,
   WS_HA1,
   WS_HA2,
+  WS_FIN0,  // MPPI final-rollout snapshots, two buffers (call parity)
+  WS_FIN1,
   WS_COUNT
 };
 

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+try:  # load torch's HIP runtime before libmpgpu so device pointers and streams are shared
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
