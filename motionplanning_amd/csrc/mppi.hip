@@ -14,6 +14,8 @@
 #include "mppi_device.hpp"
 #include "runtime.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -77,6 +79,7 @@ struct PlanArgs {
   int lds_unom, lds_obs, lds_grid;  // offsets (in doubles) into dynamic LDS; lds_grid < 0: grid stays in HBM
   int lds_ctrl, lds_part;           // control lists [RPB][2H+1] / staged partials (< 0: use HBM)
   unsigned long long* stamps;       // diagnostic build only (MPGPU_STAMPS=1): [grid][8] s_memrealtime
+  int inline_noise;                 // 1: Philox draws inside the rollout loop (no noise_prep pass)
   double* fin;                      // deferred final rollout: per-scene input snapshot (FinRec), or null
   int fin_stride;                   // doubles per scene record
 };
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
 
   const double* X0 = A.X0 + 7 * s;
   const double* goal = A.goal + 2 * s;
-  const double* noise = A.noise + (size_t)K * H2 * s;  // h-major [H][K][2] (noise_prep_kernel)
+  const double* noise = A.noise ? A.noise + (size_t)K * H2 * s : nullptr;  // h-major [H][K][2] (noise_prep_kernel)
   // Stage the scene's read-only inputs in LDS: the rollout loop then issues no
   // global loads but the prefetched noise, so no s_waitcnt vmcnt ever waits on
   // the (uncoalesced) TrajectoryCollection stores (CDNA4 vmcnt counts stores).
@@ -201,11 +204,28 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   {
     // z for step j+1 is loaded at the top of step j: the wait for it never covers
     // the TrajectoryCollection stores issued later in the step.
-    const double2* zrow = reinterpret_cast<const double2*>(noise) + kk;
-    double2 zc = zrow[0];
+    // Inline Philox (device noise): the pair draws two steps at once, the even lane step j and
+    // the odd lane step j+1 (one instruction stream, lane-varying counter), and swaps: one
+    // Box–Muller per lane per two steps, issued into the dynamics chain's latency bubbles.
+    const double2* zrow = noise ? reinterpret_cast<const double2*>(noise) + kk : nullptr;
+    double2 zc = zrow ? zrow[0] : make_double2(0.0, 0.0), zn = zc;
     auto ctrl = [&](int j, double* u) {
-      const double z[2] = {zc.x, zc.y};
-      if (j + 1 < H) zc = zrow[(size_t)(j + 1) * K];
+      double2 zj;
+      if (A.inline_noise) {
+        if ((j & 1) == 0) {
+          double zz[2];
+          philox_normal2(P, (unsigned)s, (unsigned)kk, (unsigned)(j + side), zz);
+          const double o0 = pair_swap(zz[0]), o1 = pair_swap(zz[1]);
+          zj = side ? make_double2(o0, o1) : make_double2(zz[0], zz[1]);
+          zn = side ? make_double2(zz[0], zz[1]) : make_double2(o0, o1);
+        } else {
+          zj = zn;
+        }
+      } else {
+        zj = zc;
+        if (j + 1 < H) zc = zrow[(size_t)(j + 1) * K];
+      }
+      const double z[2] = {zj.x, zj.y};
       sample_ctrl(P, z, unom + 2 * j, u);
       // Self-balancing issue priority: a wave's priority drops by one per quarter of the
       // horizon it has completed, so the waves sharing a SIMD (oldest-first arbitration
@@ -360,7 +380,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   }
   __syncthreads();
   const double inv_eta = 1.0 / sh_eta;
-  const double* noiseS = A.noise + (size_t)K * H2 * s;
+  const double* noiseS = A.noise ? A.noise + (size_t)K * H2 * s : nullptr;
   for (int t = tid; t < H2; t += NT) {
     double acc = 0.0;
 #pragma unroll 8
@@ -370,8 +390,14 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       for (int r = 0; r < m - p0; r++) {
         const int kr = p0 + r, h = t >> 1;
         double u[2];
-        const double2 zz = reinterpret_cast<const double2*>(noiseS)[(size_t)h * K + kr];
-        const double z[2] = {zz.x, zz.y};
+        double z[2];
+        if (A.inline_noise) {
+          philox_normal2(P, (unsigned)s, (unsigned)kr, (unsigned)h, z);
+        } else {
+          const double2 zz = reinterpret_cast<const double2*>(noiseS)[(size_t)h * K + kr];
+          z[0] = zz.x;
+          z[1] = zz.y;
+        }
         sample_ctrl(P, z, unom + 2 * h, u);
         ap = ap + sh_e[r] * u[t & 1];
       }
@@ -612,15 +638,18 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   PlanArgs A;
   A.X0 = X0; A.goal = goal; A.unom = U_nom; A.obs = D.n_obs > 0 ? obstacles : nullptr;
   A.grid = D.gnx > 0 ? grid : nullptr;
-  double* zh = (double*)mp_ws(ctx, WS_NOISE, sizeof(double) * (size_t)S * K * H * 2);
-  if (!zh) return MP_ERR_NOMEM;
-  {
+  static const bool noise_pass = getenv("MPGPU_NOISE_PASS") != nullptr;
+  A.inline_noise = D.noise_mode == MP_NOISE_PHILOX && !noise_pass;
+  A.noise = nullptr;
+  if (!A.inline_noise) {  // caller's z (parity mode): transposed h-major by noise_prep_kernel
+    double* zh = (double*)mp_ws(ctx, WS_NOISE, sizeof(double) * (size_t)S * K * H * 2);
+    if (!zh) return MP_ERR_NOMEM;
     const long long n = (long long)S * K * H;
     hipLaunchKernelGGL(noise_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, S, noise,
                        zh);
     MP_HIP(ctx, hipGetLastError());
+    A.noise = zh;
   }
-  A.noise = zh;
   A.cost_all = coll_cost ? coll_cost : (double*)mp_ws(ctx, WS_MPPI_COST, sizeof(double) * (size_t)S * K);
   A.feas_all = coll_feas ? coll_feas : (unsigned char*)mp_ws(ctx, WS_MPPI_FEAS, (size_t)S * K);
   A.part = (double*)mp_ws(ctx, WS_MPPI_PART, sizeof(double) * (size_t)S * nb * pstride);
@@ -675,8 +704,8 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                                     (int)kMaxLds));
     attr_set = true;
   }
-  // deferred final rollout: snapshot buffer of this call's parity, free once the final
-  // rollout of the call two back (same parity) is done
+  // deferred final rollout: snapshot ring slot of this call, free once the final rollout of
+  // the call MP_FIN_RING back (same slot) is done
   A.fin = nullptr;
   A.fin_stride = 0;
   int par = 0;
@@ -684,14 +713,15 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     int st2 = mp_side_init(ctx);
     if (st2) return st2;
     par = ctx->fin_par;
-    ctx->fin_par ^= 1;
+    ctx->fin_par = (par + 1) % MP_FIN_RING;
     const FinRec R(H, D.n_obs, D.gnx * D.gny);
     A.fin_stride = R.stride;
     A.fin = (double*)mp_ws(ctx, WS_FIN0 + par, sizeof(double) * (size_t)S * R.stride);
     if (!A.fin) return MP_ERR_NOMEM;
-    // The host (not the context stream) waits for the final rollout two calls back to have
-    // read this buffer: it finished during the previous call's rollouts, and a cross-stream
-    // wait packet would stall the context stream between kernels instead.
+    // The host (not the context stream) waits for the final rollout MP_FIN_RING calls back to
+    // have read this slot (long done): a cross-stream wait packet would stall the context
+    // stream between kernels, and a wait on the previous call's final rollout (which runs
+    // beside the next plan kernel) would hold the host back until the GPU idles.
     MP_HIP(ctx, hipEventSynchronize(ctx->ev_fin[par]));
   }
   A.stamps = nullptr;
@@ -700,13 +730,17 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA2, sizeof(unsigned long long) * 32 * S * nb);
     MP_HIP(ctx, hipMemsetAsync(A.stamps, 0, sizeof(unsigned long long) * 32 * S * nb, ctx->stream));
   }
-  mp_time_begin(ctx);
+  // timing events ride on the dispatch packet (hipExtLaunchKernel), and the stop event doubles
+  // as the side stream's plan-done dependency: no marker packets between consecutive plans
+  hipEvent_t t_start, t_stop;
+  mp_time_pair(ctx, &t_start, &t_stop);
   if (BT == 512)
-    hipLaunchKernelGGL(mppi_plan_kernel<512>, dim3(S * nb), dim3(512), shmem, ctx->stream, D, A);
+    hipExtLaunchKernelGGL(mppi_plan_kernel<512>, dim3(S * nb), dim3(512), shmem, ctx->stream, t_start, t_stop, 0, D,
+                          A);
   else
-    hipLaunchKernelGGL(mppi_plan_kernel<256>, dim3(S * nb), dim3(256), shmem, ctx->stream, D, A);
+    hipExtLaunchKernelGGL(mppi_plan_kernel<256>, dim3(S * nb), dim3(256), shmem, ctx->stream, t_start, t_stop, 0, D,
+                          A);
   MP_HIP(ctx, hipGetLastError());
-  mp_time_end(ctx);
   if (final_stream) {
     const FinRec R(H, D.n_obs, D.gnx * D.gny);
     const int grid_lds = (size_t)R.stride * 8 <= 64 * 1024;
@@ -718,8 +752,12 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                                       (int)kMaxLds));
       fattr = true;
     }
-    MP_HIP(ctx, hipEventRecord(ctx->ev_plan[par], ctx->stream));
-    MP_HIP(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_plan[par], 0));
+    hipEvent_t plan_done = t_stop;
+    if (!plan_done) {
+      plan_done = ctx->ev_plan[par];
+      MP_HIP(ctx, hipEventRecord(plan_done, ctx->stream));
+    }
+    MP_HIP(ctx, hipStreamWaitEvent(ctx->side, plan_done, 0));
     hipLaunchKernelGGL(final_rollout_kernel, dim3(S), dim3(64), fsh, ctx->side, D, A.fin, A.fin_stride, grid_lds,
                        traj_out, cost_out, feasible_out, ctx->flags);
     MP_HIP(ctx, hipGetLastError());

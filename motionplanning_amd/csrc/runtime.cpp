@@ -74,7 +74,7 @@ void mp_sync_all(mp_ctx* ctx) {
 int mp_side_init(mp_ctx* ctx) {
   if (ctx->side) return MP_OK;
   MP_HIP(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < MP_FIN_RING; i++) {
     MP_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_plan[i], hipEventDisableTiming));
     MP_HIP(ctx, hipEventCreateWithFlags(&ctx->ev_fin[i], hipEventDisableTiming));
     MP_HIP(ctx, hipEventRecord(ctx->ev_fin[i], ctx->side));  // "buffer free" from the start
@@ -102,6 +102,16 @@ void mp_time_end(mp_ctx* ctx) {
   if (!ctx->timing) return;
   hipEvent_t e = next_event(ctx);
   if (e) hipEventRecord(e, ctx->stream);
+}
+
+void mp_time_pair(mp_ctx* ctx, hipEvent_t* start, hipEvent_t* stop) {
+  *start = *stop = nullptr;
+  if (!ctx->timing) return;
+  hipEvent_t a = next_event(ctx);
+  hipEvent_t b = a ? next_event(ctx) : nullptr;
+  if (!a || !b) return;
+  *start = a;
+  *stop = b;
 }
 
 extern "C" {
@@ -180,7 +190,7 @@ int mp_ctx_destroy(mp_ctx* ctx) {
   for (hipEvent_t e : ctx->ev_pool) hipEventDestroy(e);
   if (ctx->ha_states_candi) hipFree(ctx->ha_states_candi);
   if (ctx->ha_paths_candi) hipFree(ctx->ha_paths_candi);
-  for (int i = 0; i < 2; i++) {
+  for (int i = 0; i < MP_FIN_RING; i++) {
     if (ctx->ev_plan[i]) hipEventDestroy(ctx->ev_plan[i]);
     if (ctx->ev_fin[i]) hipEventDestroy(ctx->ev_fin[i]);
   }

@@ -10,6 +10,11 @@
 
 #include "../../include/mpgpu.h"
 
+// Snapshot buffers of the deferred final rollout.  A call waits (on the host) for the final
+// rollout MP_FIN_RING calls back; with 4 that one finished long before, so the host stays
+// ahead of the GPU and the context stream never idles between plan kernels.
+#define MP_FIN_RING 4
+
 struct mp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -33,9 +38,9 @@ struct mp_ctx {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   // side stream of the deferred MPPI final rollout (mp_mppi_params.final_stream = 1):
-  // plan-done / final-done events per snapshot buffer (double-buffered by call parity)
+  // plan-done / final-done events per snapshot buffer (a ring of MP_FIN_RING, by call count)
   hipStream_t side = nullptr;
-  hipEvent_t ev_plan[2] = {nullptr, nullptr}, ev_fin[2] = {nullptr, nullptr}, ev_join = nullptr;
+  hipEvent_t ev_plan[MP_FIN_RING] = {}, ev_fin[MP_FIN_RING] = {}, ev_join = nullptr;
   int fin_par = 0;
 };
 
@@ -47,6 +52,9 @@ void mp_sync_all(mp_ctx* ctx);
 // Bracket a kernel launch with timing events when ctx->timing is on.
 void mp_time_begin(mp_ctx* ctx);
 void mp_time_end(mp_ctx* ctx);
+// Timing event pair for hipExtLaunchKernel (recorded by the dispatch itself, no marker
+// packets between kernels); both nullptr when timing is off.
+void mp_time_pair(mp_ctx* ctx, hipEvent_t* start, hipEvent_t* stop);
 
 // workspace slots
 enum {
@@ -77,8 +85,8 @@ enum {
   WS_HA0,
   WS_HA1,
   WS_HA2,
-  WS_FIN0,  // MPPI final-rollout snapshots, two buffers (call parity)
-  WS_FIN1,
+  WS_FIN0,  // MPPI final-rollout snapshots, MP_FIN_RING slots
+  WS_FIN_END = WS_FIN0 + MP_FIN_RING - 1,
   WS_COUNT
 };
 

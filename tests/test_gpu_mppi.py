@@ -74,6 +74,19 @@ def test_feasibility_count_prefix(ctx, fc):
     _check_plan(gpu, ref)
 
 
+@pytest.mark.parametrize("fc", [0, 300])
+def test_philox_feasibility_prefix(ctx, fc):
+    """Device Philox noise drawn inside the rollout loop + the FeasibilityCount boundary block
+    (whose controls phase 2 regenerates from the same counters)."""
+    p = configs.mppi_params(K=1500, H=21, T=3.0, n_obs=3, feasibility_count=fc, noise_mode=MP_NOISE_PHILOX,
+                            seed=99, offset=4)
+    obs = np.array(configs.OBSTACLES_REF)
+    X0, goal, un = np.array(configs.X0_REF), np.array(configs.GOAL_REF), np.zeros((21, 2))
+    gpu = mppi_plan_batch(p, X0[None], goal[None], un[None], obs[None], None, None, collect=True, ctx=ctx)
+    ref = oracle.mppi_plan(p, X0, goal, un, obs, None, None, collect=True)
+    _check_plan(gpu, ref)
+
+
 def test_philox_mode_matches_oracle(ctx):
     c = configs.cfg1()
     p = c["params"]
