@@ -5,8 +5,9 @@ S scenes per GPU (default 8 = the per-GPU shard of configs[4], "64 scenes sharde
 8xMI355X"); every scene is configs[1]: K=8192 rollouts, H=50 horizon steps, 7-state
 dynamic bicycle, 100x100 occupancy grid, device Philox noise, the full
 TrajectoryCollection (every rollout's trajectory and control list) written to HBM,
-weights + MPPICtrl + final rollout.  Two launches per step (noise, plan) on the context stream + the final rollout of
-MPPICtrl on the side stream (final_stream=1; --final-inline keeps it in the plan kernel),
+weights + MPPICtrl + final rollout.  One plan launch per step on the context stream (Philox
+noise drawn inside the rollout loop) + the final rollout of MPPICtrl on the side stream
+(final_stream=1; --final-inline keeps it in the plan kernel),
 so step i's serial final rollout overlaps step i+1's rollouts; every step's outputs are
 complete when the timed region's closing synchronize returns.  Inputs
 are resident in HBM before the timed region.  N>1: one process per GPU, each
@@ -55,9 +56,9 @@ def parse():
 
 def algorithmic_bytes(S, K, H):
     """Compulsory HBM bytes of one mppi_plan_kernel launch: per rollout-step
-    16 B noise read + 16 B control written + 56 B state written; per rollout the initial
-    state row, cost and feasibility flag."""
-    per_rollout = H * (16 + 16 + 56) + 56 + 8 + 1
+    16 B control + 56 B state written (the TrajectoryCollection; device Philox noise is drawn
+    in registers, nothing read); per rollout the initial state row, cost and feasibility flag."""
+    per_rollout = H * (16 + 56) + 56 + 8 + 1
     return S * K * per_rollout
 
 
@@ -166,7 +167,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded Philox noise; cfg1 circles rasterised into a 100x100 grid)",
+        "data": "synthetic (seeded Philox noise drawn on device; cfg1 circles rasterised into a 100x100 grid)",
         "config": {
             "workload": f"configs[4] per-GPU shard: {S} independent scenes per GPU, each configs[1] (MPPI K=8192 "
                         "H=50 dynamic bicycle, 2-D occupancy-grid cost, full TrajectoryCollection, weights + "

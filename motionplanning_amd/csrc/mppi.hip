@@ -144,10 +144,12 @@ __global__ __launch_bounds__(256) void noise_prep_kernel(MppiDev P, int S, const
   reinterpret_cast<double2*>(zh)[i] = make_double2(z[0], z[1]);
 }
 
-// BT threads per block (4 or 8 waves), BT/2 rollouts per block.
-template <int BT>
+// BT threads per block (4 or 8 waves); LPR lanes per rollout: 2 = lane pair (dyn_pair, the
+// two tire chains on the two lanes), 1 = one rollout per lane (dyn_lane) when the launch has a
+// rollout per lane for every SIMD.  BT/LPR rollouts per block.
+template <int BT, int LPR>
 __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
-  constexpr int NT = BT, RPB = BT / 2, NQ = BT / 128;
+  constexpr int NT = BT, RPB = BT / LPR, NQ = BT / 128;
   __shared__ double sh_red[NT / 64];
   __shared__ double sh_e[RPB];
   __shared__ double sh_q[NQ][128];
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   extern __shared__ double dyn[];
   const int H = P.H, H2 = 2 * H, K = P.K;
   const int s = blockIdx.x / A.nb, b = blockIdx.x % A.nb;
-  const int tid = threadIdx.x, pair = tid >> 1, side = tid & 1;
+  const int tid = threadIdx.x, pair = LPR == 2 ? tid >> 1 : tid, side = LPR == 2 ? tid & 1 : 0;
   const int k = b * RPB + pair;
   const bool active = k < K;
   const int kk = active ? k : K - 1;
@@ -196,7 +198,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     }
     __syncthreads();
   }
-  double* ctrl_g = A.ctrl_all ? A.ctrl_all + ((size_t)s * H * K + kk) * 2 + side : nullptr;
+  double* ctrl_g = A.ctrl_all ? A.ctrl_all + ((size_t)s * H * K + kk) * 2 + side : nullptr;  // LPR 1: + 0
 
   // ---------------- phase 1: the rollout of this lane pair
   int feas;
@@ -211,7 +213,11 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     double2 zc = zrow ? zrow[0] : make_double2(0.0, 0.0), zn = zc;
     auto ctrl = [&](int j, double* u) {
       double2 zj;
-      if (A.inline_noise) {
+      if (A.inline_noise && LPR == 1) {
+        double zz[2];
+        philox_normal2(P, (unsigned)s, (unsigned)kk, (unsigned)j, zz);
+        zj = make_double2(zz[0], zz[1]);
+      } else if (A.inline_noise) {
         if ((j & 1) == 0) {
           double zz[2];
           philox_normal2(P, (unsigned)s, (unsigned)kk, (unsigned)(j + side), zz);
@@ -238,12 +244,20 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       }
     };
     auto store = [&](int j, const double* u) {
-      if (ush) ush[pair * ustr + 2 * j + side] = u[side];
-      if (ctrl_g) ctrl_g[(size_t)j * K * 2] = u[side];
+      if (LPR == 2) {
+        if (ush) ush[pair * ustr + 2 * j + side] = u[side];
+        if (ctrl_g) ctrl_g[(size_t)j * K * 2] = u[side];
+      } else {
+        if (ush) {
+          ush[pair * ustr + 2 * j] = u[0];
+          ush[pair * ustr + 2 * j + 1] = u[1];
+        }
+        if (ctrl_g) *reinterpret_cast<double2*>(ctrl_g + (size_t)j * K * 2) = make_double2(u[0], u[1]);
+      }
     };
     // inactive pairs (k >= K) recompute rollout K-1 and write identical values
     const TrajOut traj{A.coll_traj ? A.coll_traj + (size_t)s * (H + 1) * 7 * K + kk : nullptr, 7LL * K, (long long)K};
-    c = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas, atab);
+    c = rollout_pair<LPR>(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas, atab);
   }
   MP_STAMP(1);
   MP_STAMP_WAVE();
@@ -442,7 +456,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     auto store = [&](int, const double*) {};
     const TrajOut traj{A.traj_out + (size_t)s * (H + 1) * 7, 7, 1};  // every pair writes the same values
     int f2;
-    const double c2 = rollout_pair(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &f2, atab);
+    const double c2 = rollout_pair(P, X0, goal, obs, grid, unom, tid & 1, ctrl, store, traj, &f2, atab);
     if (tid == 0) {
       A.cost_out[s] = c2;
       A.feas_out[s] = f2;
@@ -631,8 +645,17 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   // 8-wave blocks once the launch fills every CU with one (the dispatcher then places
   // exactly two waves per SIMD; with 4-wave blocks, two per CU, it can stack 3 + 1 and
   // the slowest SIMD sets the end time), else 4-wave blocks for more CUs at small S.
-  const int BT = (size_t)S * ((K + 255) / 256) >= 256 ? 512 : 256;
-  const int RPBh = BT / 2;
+  // One rollout per lane once that gives every SIMD two waves (S*K >= 2 x 256 CUs x 4 SIMDs x
+  // 64 lanes).  Measured (cfg2, K=8192, H=50): 16 scenes, LPR 1 (2 waves/SIMD, the tire chains
+  // interleaved in a lane, costs evaluated once) 0.536 ms vs LPR 2 (4 waves/SIMD) 0.703 ms;
+  // 8 scenes, LPR 1 (1 wave/SIMD) 0.384 ms vs LPR 2 (2 waves/SIMD) 0.375 ms: a lone wave
+  // cannot cover the fp64 dependency latency.
+  const char* lpr_s = getenv("MPGPU_LPR");  // 1 / 2 forces the layout (tests, comparisons)
+  const int lpr_env = lpr_s ? atoi(lpr_s) : 0;
+  const int LPR = lpr_env == 1 || lpr_env == 2 ? lpr_env : ((size_t)S * K >= 131072 ? 1 : 2);
+  const int BT = LPR == 1 ? ((size_t)S * ((K + 511) / 512) >= 256 ? 512 : 256)
+                          : ((size_t)S * ((K + 255) / 256) >= 256 ? 512 : 256);
+  const int RPBh = BT / LPR;
   const int nb = (K + RPBh - 1) / RPBh;
   const int pstride = 4 + 2 * H;
   PlanArgs A;
@@ -698,10 +721,14 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   MP_CHECK(ctx, shmem <= kMaxLds, "K/H/obstacles too large for one scene (dynamic LDS %zu B)", shmem);
   static bool attr_set = false;
   if (!attr_set) {
-    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kMaxLds));
-    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kMaxLds));
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<256, 2>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<512, 2>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<256, 1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<512, 1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
     attr_set = true;
   }
   // deferred final rollout: snapshot ring slot of this call, free once the final rollout of
@@ -734,12 +761,15 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   // as the side stream's plan-done dependency: no marker packets between consecutive plans
   hipEvent_t t_start, t_stop;
   mp_time_pair(ctx, &t_start, &t_stop);
-  if (BT == 512)
-    hipExtLaunchKernelGGL(mppi_plan_kernel<512>, dim3(S * nb), dim3(512), shmem, ctx->stream, t_start, t_stop, 0, D,
-                          A);
+  const dim3 grd(S * nb);
+  if (LPR == 1 && BT == 512)
+    hipExtLaunchKernelGGL(mppi_plan_kernel<512, 1>, grd, dim3(512), shmem, ctx->stream, t_start, t_stop, 0, D, A);
+  else if (LPR == 1)
+    hipExtLaunchKernelGGL(mppi_plan_kernel<256, 1>, grd, dim3(256), shmem, ctx->stream, t_start, t_stop, 0, D, A);
+  else if (BT == 512)
+    hipExtLaunchKernelGGL(mppi_plan_kernel<512, 2>, grd, dim3(512), shmem, ctx->stream, t_start, t_stop, 0, D, A);
   else
-    hipExtLaunchKernelGGL(mppi_plan_kernel<256>, dim3(S * nb), dim3(256), shmem, ctx->stream, t_start, t_stop, 0, D,
-                          A);
+    hipExtLaunchKernelGGL(mppi_plan_kernel<256, 2>, grd, dim3(256), shmem, ctx->stream, t_start, t_stop, 0, D, A);
   MP_HIP(ctx, hipGetLastError());
   if (final_stream) {
     const FinRec R(H, D.n_obs, D.gnx * D.gny);

@@ -71,6 +71,35 @@ __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, 
   d[6] = sr;
 }
 
+// VehicleDynamics for one lane holding the whole rollout: the front and rear tire chains of
+// dyn_pair as two independent instruction chains of the same lane (the same operations on
+// the same operands, so the same bits), no lane exchange.  Used when the launch has enough
+// rollouts for one per lane to fill every SIMD: the costs and the state update are then not
+// evaluated twice, and the two tire chains interleave in the single wave's latency bubbles.
+__device__ __forceinline__ void dyn_lane(const double* x, double sr, double ax, double* d, const double* atab) {
+  const double la = 1.56, lb = 1.64, M = 2020.0, Izz = 4095.0, g = 9.81, mu = 0.8;
+  const double KFZF = 1018.28 / 2, KFZR = 963.34 / 2, KFZX = 186.22;
+  const double B = -10.4 / mu, C = 1.3, E = 0.1556;
+  const double v = x[2], r = x[3], psi = x[4], ux = x[5], sa = x[6];
+  const double t = (ax - r * v) * KFZX;
+  const double FZf = 2 * (KFZF * g + -t), FZr = 2 * (KFZR * g + t);
+  const double af = mpj_atan_tab((v + la * r) / (ux + 0.01), atab) - sa;
+  const double ar = mpj_atan_tab((v + (-lb) * r) / (ux + 0.01), atab) - 0.0;
+  const double Xf = B * af, Xr = B * ar;
+  const double FY1 = mu * FZf * 1.0 * mpj_sin_bl(C * mpj_atan_tab(Xf - E * (Xf - mpj_atan_tab(Xf, atab)), atab));
+  const double FY2 = mu * FZr * 1.0 * mpj_sin_bl(C * mpj_atan_tab(Xr - E * (Xr - mpj_atan_tab(Xr, atab)), atab));
+  const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);
+  double sp, cp;
+  mpj_sincos_bl(psi, &sp, &cp);
+  d[0] = uxc * cp - v * sp;
+  d[1] = uxc * sp + v * cp;
+  d[2] = (FY1 + FY2) / M - r * uxc;
+  d[3] = (FY1 * la - FY2 * lb) / Izz;
+  d[4] = r;
+  d[5] = ax;
+  d[6] = sr;
+}
+
 // running cost, vehicledynamics.jl:52
 __device__ __forceinline__ double run_cost(const double* x, double sr, double ax) {
   const double y = x[1], v = x[2], r = x[3], sa = x[6];
@@ -79,6 +108,7 @@ __device__ __forceinline__ double run_cost(const double* x, double sr, double ax
 
 // ObstacleEvaluation (MPPIUtils.jl:120-132) + occupancy grid (build extension).
 // Branch-free: `c = hit ? c + pen : c` is bit-identical to `if (hit) c = c + pen`.
+template <int LPR = 2>
 __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* x, const double* obs,
                                                 const unsigned char* grid, int* ok, int side) {
   double c = 0.0;
@@ -89,10 +119,16 @@ __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* 
     c = (hit ? c + P.obs_pen : c);
   }
   if (P.gnx > 0) {
-    // cell coordinates: even lane divides x, odd lane y, one DPP swap
-    const double f = (side ? x[1] - P.gy0 : x[0] - P.gx0) / (side ? P.gdy : P.gdx);
-    const double fo = pair_swap(f);
-    const double fx = side ? fo : f, fy = side ? f : fo;
+    double fx, fy;
+    if (LPR == 2) {  // cell coordinates: even lane divides x, odd lane y, one DPP swap
+      const double f = (side ? x[1] - P.gy0 : x[0] - P.gx0) / (side ? P.gdy : P.gdx);
+      const double fo = pair_swap(f);
+      fx = side ? fo : f;
+      fy = side ? f : fo;
+    } else {
+      fx = (x[0] - P.gx0) / P.gdx;
+      fy = (x[1] - P.gy0) / P.gdy;
+    }
     const int inb = fx >= 0.0 && fy >= 0.0 && fx < (double)P.gnx && fy < (double)P.gny;
     const int ix = inb ? (int)fx : 0, iy = inb ? (int)fy : 0;
     const int hit = inb && grid[iy * P.gnx + ix];
@@ -190,9 +226,15 @@ struct TrajOut {
   long long rs, cs;
 };
 
-// The even lane of the pair stores x[0..3], the odd lane x[4..6].
+// The even lane of the pair stores x[0..3], the odd lane x[4..6] (LPR 1: the lane all 7).
+template <int LPR = 2>
 __device__ __forceinline__ void store_state(const TrajOut& T, int j, const double* x, int side) {
   double* q = T.p + (long long)j * T.rs;
+  if (LPR == 1) {
+#pragma unroll
+    for (int i = 0; i < 7; i++) q[(long long)i * T.cs] = x[i];
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double v = MPJ_SEL(side, x[4 + i < 7 ? 4 + i : 6], x[i]);
@@ -204,7 +246,7 @@ __device__ __forceinline__ void store_state(const TrajOut& T, int j, const doubl
 // TrajectoryRollout for the lane pair (MPPIUtils.jl:31-57).  `ctrl(j, u)` yields the
 // control of step j.  traj.p (optional) gets the H+1 states (store_state).
 // Returns cost_total; *feas = constraint.
-template <class CtrlFn, class StoreFn>
+template <int LPR = 2, class CtrlFn, class StoreFn>
 __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X0, const double* goal,
                                                const double* obs, const unsigned char* grid,
                                                const double* unom, int side, CtrlFn ctrl, StoreFn store,
@@ -212,7 +254,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
   double x[7];
 #pragma unroll
   for (int i = 0; i < 7; i++) x[i] = X0[i];
-  if (traj.p) store_state(traj, 0, x, side);
+  if (traj.p) store_state<LPR>(traj, 0, x, side);
   double sum = 0.0;
   int ok_all = 1;
   for (int j = 0; j < P.H; j++) {
@@ -222,15 +264,17 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     int okc = 1, okb = 1;
     double cc = 0.0, cb = 0.0;
     if (j > 0) {
-      cc = obstacle_cost(P, x, obs, grid, &okc, side);
+      cc = obstacle_cost<LPR>(P, x, obs, grid, &okc, side);
       cb = bound_cost(P, x, &okb);
     }
     const double pc = run_cost(x, u[0], u[1]);
     double k1[7], k2[7], x2[7];
-    dyn_pair(x, u[0], u[1], k1, side, atab);
+    if (LPR == 2) dyn_pair(x, u[0], u[1], k1, side, atab);
+    else dyn_lane(x, u[0], u[1], k1, atab);
 #pragma unroll
     for (int i = 0; i < 7; i++) x2[i] = x[i] + k1[i] * P.dt;
-    dyn_pair(x2, u[0], u[1], k2, side, atab);
+    if (LPR == 2) dyn_pair(x2, u[0], u[1], k2, side, atab);
+    else dyn_lane(x2, u[0], u[1], k2, atab);
 #pragma unroll
     for (int i = 0; i < 7; i++) x[i] = x[i] + P.dt * (k1[i] + k2[i]) / 2;
     double cj = pc + cb + cc;
@@ -243,12 +287,12 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     }
     sum = sum + cj;
     ok_all &= okc & okb;
-    if (traj.p) store_state(traj, j + 1, x, side);
+    if (traj.p) store_state<LPR>(traj, j + 1, x, side);
   }
   {  // terminal (:49-54): only the running cost of the extra RK2 step is used
     int okc = 1, okb = 1;
     const double pc = run_cost(x, 0.0, 0.0);
-    const double cc = obstacle_cost(P, x, obs, grid, &okc, side);
+    const double cc = obstacle_cost<LPR>(P, x, obs, grid, &okc, side);
     const double cb = bound_cost(P, x, &okb);
     sum = sum + (pc + cb + cc);
     ok_all &= okc & okb;
