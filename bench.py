@@ -228,34 +228,50 @@ def _sync_max(x, world, dev):
     return float(t[0])
 
 
-def bench_ilqr(ctx, world, rank, cpu=False, reps=5, B=4096, N=100):
+def bench_ilqr(ctx, world, rank, cpu=False, reps=20, B=4096, N=100):
     """configs[2]: one backward Riccati sweep + one forward trial (alpha = 1) over B=4096
-    initial states x H=100 knots per GPU (weak scaling).  Unit: one instance-knot of
-    (backward + forward).  Host buffers in/out (the iLQR entry points take host arrays), so
-    the wall rate includes PCIe; kernel_rate uses the library's HIP-event kernel time."""
+    initial states x H=100 knots per GPU (weak scaling), inputs resident in HBM (the _dev entry
+    points).  Unit: one instance-knot of (backward + forward).  kernel_ms: the HIP-event time of
+    the deriv + backward + forward kernels per pass."""
     from motionplanning_amd import ilqr
+    from motionplanning_amd.abi import ptr
 
     dev = torch.device("cuda", torch.cuda.current_device())
     p = ilqr.params(N=N)
     x0, U = ilqr.cfg3_instances(B, N, seed=3 + rank)
     X, J = ilqr.ilqr_rollout(p, x0, U, ctx=ctx)
-    ilqr.ilqr_forward(p, X, U, *ilqr.ilqr_backward(p, X, U, ctx=ctx), np.ones(B), ctx=ctx)  # warm-up
+    dX, dU = torch.as_tensor(X, device=dev), torch.as_tensor(U, device=dev)
+    dk = torch.empty((B, N - 1, 2), dtype=torch.float64, device=dev)
+    dK = torch.empty((B, N - 1, 4, 2), dtype=torch.float64, device=dev)
+    dXn, dUn = torch.empty_like(dX), torch.empty_like(dU)
+    dJn = torch.empty(B, dtype=torch.float64, device=dev)
+    dal = torch.ones(B, dtype=torch.float64, device=dev)
+
+    def one():
+        ctx.check(ctx.lib.mp_ilqr_backward_dev(ctx.handle, ctypes.byref(p), B, ptr(dX), ptr(dU), ptr(dk), ptr(dK)))
+        ctx.check(ctx.lib.mp_ilqr_forward_dev(ctx.handle, ctypes.byref(p), B, ptr(dX), ptr(dU), ptr(dk), ptr(dK),
+                                              ptr(dal), ptr(dXn), ptr(dUn), ptr(dJn)))
+
+    one()
+    torch.cuda.synchronize()
     ms, cnt = ctypes.c_double(), ctypes.c_int32()
     ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        k, K = ilqr.ilqr_backward(p, X, U, ctx=ctx)
-        Xn, Un, Jn = ilqr.ilqr_forward(p, X, U, k, K, np.ones(B), ctx=ctx)
+        one()
+    torch.cuda.synchronize()
     el = _sync_max(time.perf_counter() - t0, world, dev)
     ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
     kms = _sync_max(ms.value / reps, world, dev)
     units = B * (N - 1)
+    Jn = dJn.cpu().numpy()
     out = {"metric": "iLQR instance-knots/s (backward Riccati + forward trial), H=100, 4096 instances per GPU",
            "value": world * units * reps / el, "kernel_rate": world * units / (kms * 1e-3), "kernel_ms": kms,
            "ms_per_pass": el / reps * 1e3, "dtype": "f64", "scaling": "weak", "valid": bool(np.isfinite(Jn).all()),
-           "bound": "valu-fp64 (FD derivatives: ~130 stage-cost + 48 dynamics evals per knot)"}
+           "bound": "latency (fp64 FD derivatives; serial Riccati sweep per instance)"}
     if cpu:
         import oracle
 

@@ -201,6 +201,12 @@ int mp_ilqr_backward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const doub
 int mp_ilqr_forward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X,
                     const double* U, const double* k, const double* Kg, const double* alpha,
                     double* Xnew, double* Unew, double* Jnew);
+/* Same contracts, DEVICE pointers, asynchronous on the context stream. */
+int mp_ilqr_backward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X,
+                         const double* U, double* k, double* Kg);
+int mp_ilqr_forward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X,
+                        const double* U, const double* k, const double* Kg, const double* alpha,
+                        double* Xnew, double* Unew, double* Jnew);
 /* The whole script loop (ILQR.jl:39-88) per instance: backward + halving line
  * search until |ΔJ/J| <= tol.  X/U in: initial guess; out: solution. */
 int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U,

@@ -545,6 +545,32 @@ int mp_ilqr_forward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const doubl
   return MP_OK;
 }
 
+int mp_ilqr_backward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X, const double* U,
+                         double* k, double* Kg) {
+  if (!ctx) return MP_ERR_INVALID;
+  IlqrDev D;
+  int st = make_ilqr(ctx, p, B, &D);
+  if (st) return st;
+  MP_CHECK(ctx, X && U && k && Kg, "required pointer is NULL");
+  return run_backward(ctx, D, B, X, U, nullptr, k, Kg);
+}
+
+int mp_ilqr_forward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X, const double* U,
+                        const double* k, const double* Kg, const double* alpha, double* Xnew, double* Unew,
+                        double* Jnew) {
+  if (!ctx) return MP_ERR_INVALID;
+  IlqrDev D;
+  int st = make_ilqr(ctx, p, B, &D);
+  if (st) return st;
+  MP_CHECK(ctx, X && U && k && Kg && alpha && Xnew && Unew && Jnew, "required pointer is NULL");
+  mp_time_begin(ctx);
+  hipLaunchKernelGGL(ilqr_forward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, X, U, k, Kg, alpha,
+                     Xnew, Unew, Jnew);
+  MP_HIP(ctx, hipGetLastError());
+  mp_time_end(ctx);
+  return MP_OK;
+}
+
 int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U, double* J,
                   int32_t* iters) {
   if (!ctx) return MP_ERR_INVALID;

@@ -65,3 +65,33 @@ def test_cfg3_full_size_one_pass(ctx):
     for b in np.linspace(0, 4095, 16).astype(int):
         ko, Ko = oracle.ilqr_backward(p, X[b], U[b])
         assert np.array_equal(k[b], ko) and np.array_equal(K[b], Ko)
+
+
+def test_dev_entry_points_match_host(ctx):
+    """mp_ilqr_{backward,forward}_dev on HBM-resident tensors == the host-pointer calls (bit-exact)."""
+    import ctypes
+
+    import torch
+
+    from motionplanning_amd.abi import ptr
+
+    p = ilqr.params(N=30)
+    x0, U = ilqr.cfg3_instances(96, 30, seed=8)
+    X, _ = ilqr.ilqr_rollout(p, x0, U, ctx=ctx)
+    k, K = ilqr.ilqr_backward(p, X, U, ctx=ctx)
+    Xn, Un, Jn = ilqr.ilqr_forward(p, X, U, k, K, np.full(96, 0.5), ctx=ctx)
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
+    with torch.cuda.stream(stream):
+        dX, dU = torch.as_tensor(X, device=dev), torch.as_tensor(U, device=dev)
+        dk, dK = torch.empty((96, 29, 2), dtype=torch.float64, device=dev), torch.empty(
+            (96, 29, 4, 2), dtype=torch.float64, device=dev)
+        dXn, dUn, dJn = torch.empty_like(dX), torch.empty_like(dU), torch.empty(96, dtype=torch.float64, device=dev)
+        dal = torch.full((96,), 0.5, dtype=torch.float64, device=dev)
+        ctx.check(ctx.lib.mp_ilqr_backward_dev(ctx.handle, ctypes.byref(p), 96, ptr(dX), ptr(dU), ptr(dk), ptr(dK)))
+        ctx.check(ctx.lib.mp_ilqr_forward_dev(ctx.handle, ctypes.byref(p), 96, ptr(dX), ptr(dU), ptr(dk), ptr(dK),
+                                              ptr(dal), ptr(dXn), ptr(dUn), ptr(dJn)))
+        ctx.synchronize()
+    assert np.array_equal(dk.cpu().numpy(), k) and np.array_equal(dK.cpu().numpy(), K)
+    assert np.array_equal(dXn.cpu().numpy(), Xn) and np.array_equal(dUn.cpu().numpy(), Un)
+    assert np.array_equal(dJn.cpu().numpy(), Jn)
