@@ -682,17 +682,17 @@ MPJ_FN double mpj_atan2_bl(double y, double x) {
   return (z - pi_lo) - pi;
 }
 
-/* sin and cos for |x| <= ~9π/4 without a divergent branch (cw2c reduction, n in {0, ±1..±4}). */
-MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
+/* sin and cos for |x| <= ~9π/4 as straight-line code (cw2c reduction, n in {0, ±1..±4}).
+ * mpj_sincos_fast never branches: lanes outside the fast range set *bad and get garbage; the
+ * caller re-evaluates with the exact routine (mpj_sincos_bl does so per call, the iLQR kernels
+ * per trajectory). */
+MPJ_FN void mpj_sincos_fast(double x, double* so, double* co, int* bad) {
   const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
   const double ax = mpj_fabs(x);
   const int small = ax < MPJ_PIO4;
   /* exact-path cases: |x| > ~9π/4, NaN/Inf, or the cwext points near kπ/2 (e_rem_pio2.c) */
   const int ext = (xhp <= 0x400f6a7au && (xhp & 0xfffffu) == 0x921fbu) || xhp == 0x4012d97cu || xhp == 0x401921fbu;
-  if (MPJ_ANY(xhp > 0x401c463bu || (!small && ext))) {
-    mpj_sincos(x, so, co);
-    return;
-  }
+  *bad |= xhp > 0x401c463bu || (!small && ext);
   /* |n| = 1..4 by range (e_rem_pio2.c), Cody–Waite with fn = ±|n| */
   const int na = 1 + (xhp > 0x4002d97cu) + (xhp > 0x400f6a7au) + (xhp > 0x4015fdbcu);
   const int ni = x > 0.0 ? na : -na;
@@ -717,12 +717,174 @@ MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
   *so = MPJ_SEL(small, s0, sr);
   *co = MPJ_SEL(small, c0, cr);
 }
+/* sin and cos for every finite |x| < 2^20·π/2 as straight-line code: the cw2c reduction of
+ * mpj_sincos_fast and, selected per lane, the 3-stage Cody–Waite reduction mpj_cwext uses for
+ * |x| > 9π/4 and next to kπ/2 (its two data-dependent stage tests become selects).  NaN/Inf
+ * and larger |x| set *bad. */
+MPJ_FN void mpj_sincos_wide(double x, double* so, double* co, int* bad) {
+  const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
+  const double ax = mpj_fabs(x);
+  const int small = ax < MPJ_PIO4;
+  *bad |= xhp >= 0x413921fbu;
+  const int med = (xhp <= 0x400f6a7au && (xhp & 0xfffffu) == 0x921fbu) || xhp == 0x4012d97cu ||
+                  xhp == 0x401921fbu || xhp > 0x401c463bu;
+  /* cw2c: |n| = 1..4 by range */
+  const int na = 1 + (xhp > 0x4002d97cu) + (xhp > 0x400f6a7au) + (xhp > 0x4015fdbcu);
+  const int ni = x > 0.0 ? na : -na;
+  double c0, c1;
+  mpj_cw2c(x, (double)ni, 0, &c0, &c1);
+  /* cwext, straight line (bad lanes: the conversion below is clamped by the select) */
+  const double fn = mpj_round(MPJ_SEL(xhp >= 0x413921fbu, 0.0, x) * MPJ_INVPIO2);
+  const int32_t j = (int32_t)(xhp >> 20);
+  const double r1 = mpj_fma(-fn, MPJ_PIO2_1, x), w1 = fn * MPJ_PIO2_1T, a1 = r1 - w1;
+  const int32_t i1 = j - (int32_t)((mpj_hi(a1) >> 20) & 0x7ff);
+  const double w2a = fn * MPJ_PIO2_2, r2 = r1 - w2a;
+  const double w2 = mpj_fma(fn, MPJ_PIO2_2T, -((r1 - r2) - w2a)), a2 = r2 - w2;
+  const int32_t i2 = j - (int32_t)((mpj_hi(a2) >> 20) & 0x7ff);
+  const double w3a = fn * MPJ_PIO2_3, r3 = r2 - w3a;
+  const double w3 = mpj_fma(fn, MPJ_PIO2_3T, -((r2 - r3) - w3a)), a3 = r3 - w3;
+  const int s2 = i1 > 16, s3 = s2 && i2 > 49;
+  const double er = MPJ_SEL(s3, r3, MPJ_SEL(s2, r2, r1)), ew = MPJ_SEL(s3, w3, MPJ_SEL(s2, w2, w1));
+  const double ea = MPJ_SEL(s3, a3, MPJ_SEL(s2, a2, a1));
+  const double y0 = MPJ_SEL(med, ea, c0), y1 = MPJ_SEL(med, (er - ea) - ew, c1);
+  const int nr = med ? (int)fn : ni;
+  const double xa = MPJ_SEL(small, x, y0), ya = MPJ_SEL(small, 0.0, y1);
+  const double z = xa * xa, w = z * z;
+  const double r = mpj_fma(z, mpj_fma(z, MPJ_S4, MPJ_S3), MPJ_S2) + z * w * mpj_fma(z, MPJ_S6, MPJ_S5);
+  const double v = z * xa;
+  const double sk0 = xa + v * (MPJ_S1 + z * r);
+  const double sk = xa - ((z * (0.5 * ya - v * r) - ya) - v * MPJ_S1);
+  const double ck = mpj_cos_k(xa, ya);
+  const double s0 = MPJ_SEL(ax < MPJ_SQRT_EPS, x, sk0);
+  const double cc0 = MPJ_SEL(ax < MPJ_SQRT_HALF_EPS, 1.0, ck);
+  const int n = nr & 3;
+  const double ts = MPJ_SEL(n & 1, ck, sk), tc = MPJ_SEL(n & 1, sk, ck);
+  const double sr = mpj_flip(ts, (uint32_t)(n & 2) << 30);
+  const double cr = mpj_flip(tc, (uint32_t)((n + 1) & 2) << 30);
+  *so = MPJ_SEL(small, s0, sr);
+  *co = MPJ_SEL(small, cc0, cr);
+}
+MPJ_FN void mpj_sincos_bl(double x, double* so, double* co) {
+  const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
+  const int ext = (xhp <= 0x400f6a7au && (xhp & 0xfffffu) == 0x921fbu) || xhp == 0x4012d97cu || xhp == 0x401921fbu;
+  if (MPJ_ANY(xhp > 0x401c463bu || (!(mpj_fabs(x) < MPJ_PIO4) && ext))) {
+    mpj_sincos(x, so, co);
+    return;
+  }
+  int bad = 0;
+  mpj_sincos_fast(x, so, co, &bad);
+}
 
 /* sin only, same fast range. */
 MPJ_FN double mpj_sin_bl(double x) {
   double s, c;
   mpj_sincos_bl(x, &s, &c);
   return s;
+}
+
+/* exp for 2^-28 <= |x| < 704 as one basic block (FDLIBM e_exp.c with every branch a select):
+ * the |x| < 1.5 ln2 reduction (hi = x ∓ ln2HI, lo = ±ln2LO, k = ±1) is the general one with
+ * t = k = ±1 (x - (-1)·ln2HI == x + ln2HI exactly), and (x·c)/(c-2) == -((x·c)/(2-c)) exactly,
+ * so one division serves both the k == 0 and the k != 0 result.  Other arguments (incl. NaN,
+ * Inf, overflow/underflow, k <= -1022) take mpj_exp through a wave-uniform branch. */
+MPJ_FN double mpj_exp_fast(double x, int* bad) {
+  const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
+               invln2 = 1.44269504088896338700e+00,
+               P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
+               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
+               P5 = 4.13813679705723846039e-08;
+  const uint32_t hx0 = mpj_hi(x);
+  const uint32_t hx = hx0 & 0x7fffffffu;
+  *bad |= hx < 0x3e300000u || hx >= 0x40860000u;
+  const int xsb = (int)(hx0 >> 31);
+  const int red = hx > 0x3fd62e42u;
+  const int kfar = (int)(invln2 * MPJ_SEL(hx >= 0x40860000u, 0.0, x) + (xsb ? -0.5 : 0.5)); /* no UB on bad lanes */
+  const int k = red ? (hx < 0x3FF0A2B2u ? 1 - xsb - xsb : kfar) : 0;
+  const double t = (double)k;
+  const double hi = x - t * ln2HI, lo = t * ln2LO;
+  const double xr = MPJ_SEL(red, hi - lo, x);
+  const double tt = xr * xr;
+  const double c = xr - tt * mpj_fma(tt, mpj_fma(tt, mpj_fma(tt, mpj_fma(tt, P5, P4), P3), P2), P1);
+  const double q = (xr * c) / (2.0 - c);
+  const double r0 = 1.0 - ((-q) - xr);
+  const double y = 1.0 - ((lo - q) - hi);
+  const double twopk = mpj_from_words((uint32_t)(0x3ff00000 + (k << 20)), 0);
+  return MPJ_SEL(k == 0, r0, y * twopk);
+}
+MPJ_FN double mpj_exp_bl(double x) {
+  const uint32_t hx = mpj_hi(x) & 0x7fffffffu;
+  if (MPJ_ANY(hx < 0x3e300000u || hx >= 0x40860000u)) return mpj_exp(x);
+  int bad = 0;
+  return mpj_exp_fast(x, &bad);
+}
+
+/* tan for |x| <= π/4 as one basic block (FDLIBM k_tan.c with iy = 1, both the |x| < 0.6744
+ * and the reflected |x| >= 0.6744 forms, selected); larger |x|, NaN and Inf take mpj_tan. */
+MPJ_FN double mpj_tan_fast(double x, int* bad) {
+  const double T0 = 3.33333333333334091986e-01, T1 = 1.33333333333201242699e-01,
+               T2 = 5.39682539762260521377e-02, T3 = 2.18694882948595424599e-02,
+               T4 = 8.86323982359930005737e-03, T5 = 3.59207910759131235356e-03,
+               T6 = 1.45620945432529025516e-03, T7 = 5.88041240820264096874e-04,
+               T8 = 2.46463134818469906812e-04, T9 = 7.81794442939557092300e-05,
+               T10 = 7.14072491382608190305e-05, T11 = -1.85586374855275456654e-05,
+               T12 = 2.59073051863633712884e-05, pio4lo = 3.06161699786838301793e-17;
+  const int32_t hx = (int32_t)mpj_hi(x);
+  const int32_t ix = hx & 0x7fffffff;
+  *bad |= ix > 0x3fe921fb;
+  const int big = ix >= 0x3FE59428;
+  const int neg = hx < 0;
+  const double xn = MPJ_SEL(neg, -x, x), yn = MPJ_SEL(neg, -0.0, 0.0);
+  const double xb = (MPJ_PIO4 - xn) + (pio4lo - yn);
+  const double xx = MPJ_SEL(big, xb, x);
+  const double y = 0.0;
+  const double z = xx * xx;
+  const double w = z * z;
+  double r = mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, T11, T9), T7), T5), T3), T1);
+  const double v = z * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, T12, T10), T8), T6), T4), T2);
+  const double s = z * xx;
+  r = y + z * (s * (r + v) + y);
+  r += T0 * s;
+  const double ww = xx + r;
+  const double rb = (double)(1 - ((hx >> 30) & 2)) * (1.0 - 2.0 * (xx - (ww * ww / (ww + 1.0) - r)));
+  return MPJ_SEL(ix < 0x3e400000, x, MPJ_SEL(big, rb, ww));
+}
+
+MPJ_FN double mpj_tan_bl(double x) {
+  if (MPJ_ANY((mpj_hi(x) & 0x7fffffffu) > 0x3fe921fbu)) return mpj_tan(x);
+  int bad = 0;
+  return mpj_tan_fast(x, &bad);
+}
+
+/* atan2 as one basic block for finite y, x, not both zero (FDLIBM e_atan2.c: the y == 0,
+ * x == 0 and |exponent difference| > 60 cases are selects around the general case; x == 1
+ * gives atan(y) == ±atan(|y|) there too); NaN/Inf/(0, 0) set *bad. */
+MPJ_FN double mpj_atan2_fast(double y, double x, int* bad) {
+  const double pi_o_2 = 1.5707963267948965580E+00, pi = 3.1415926535897931160E+00,
+               pi_lo = 1.2246467991473531772E-16;
+  const uint32_t hx = mpj_hi(x), lx = mpj_lo(x), hy = mpj_hi(y), ly = mpj_lo(y);
+  const int32_t ix = (int32_t)(hx & 0x7fffffffu), iy = (int32_t)(hy & 0x7fffffffu);
+  const int xz = (ix | (int32_t)lx) == 0, yz = (iy | (int32_t)ly) == 0;
+  *bad |= ix >= 0x7ff00000 || iy >= 0x7ff00000 || (xz && yz);
+  const int32_t k = (iy - ix) >> 20;
+  const int mq = (int)(((hy >> 31) & 1) | ((hx >> 30) & 2));
+  const int kbig = k > 60, ksmall = (hx >> 31) && k < -60;
+  const int m = kbig ? (mq & 1) : mq;
+  const double za = mpj_atan_bl(mpj_fabs(y / x));
+  const double z = MPJ_SEL(kbig, pi_o_2 + 0.5 * pi_lo, MPJ_SEL(ksmall, 0.0, za));
+  const double zl = z - pi_lo;
+  const double r01 = mpj_flip(z, (uint32_t)(m & 1) << 31);
+  const double r2 = pi - zl, r3 = zl - pi;
+  const double rg = MPJ_SEL(m & 2, MPJ_SEL(m & 1, r3, r2), r01);
+  /* y == 0: m 0/1 -> y, 2 -> pi, 3 -> -pi;  x == 0: ±pi/2 by the sign of y */
+  const double ry = MPJ_SEL(mq & 2, MPJ_SEL(mq & 1, -pi, pi), y);
+  const double rx = MPJ_SEL(hy >> 31, -pi_o_2, pi_o_2);
+  return MPJ_SEL(yz, ry, MPJ_SEL(xz, rx, rg));
+}
+MPJ_FN double mpj_atan2_sel(double y, double x) {
+  int bad = 0;
+  const double r = mpj_atan2_fast(y, x, &bad);
+  if (MPJ_ANY(bad)) return mpj_atan2(y, x);
+  return r;
 }
 
 /* ----------------------------------------------------------- Julia idioms */

@@ -29,6 +29,11 @@ __global__ void math_kernel(int fn, long long n, const double* x, const double* 
     case 13: r = mpj_atan_tab(a, atab); break;
     case 14: { double s, c; mpj_sincos_bl(a, &s, &c); r = s; break; }
     case 15: { double s, c; mpj_sincos_bl(a, &s, &c); r = c; break; }
+    case 16: r = mpj_exp_bl(a); break;
+    case 17: r = mpj_tan_bl(a); break;
+    case 18: r = mpj_atan2_sel(a, y[i]); break;
+    case 19: { double s, c; int b = 0; mpj_sincos_wide(a, &s, &c, &b); r = b ? mpj_sin(a) : s; break; }
+    case 20: { double s, c; int b = 0; mpj_sincos_wide(a, &s, &c, &b); r = b ? mpj_cos(a) : c; break; }
   }
   out[i] = r;
 }
@@ -36,12 +41,12 @@ __global__ void math_kernel(int fn, long long n, const double* x, const double* 
 
 extern "C" int mp_math_eval(mp_ctx* ctx, int32_t fn, int64_t n, const double* x, const double* y, double* out) {
   if (!ctx) return MP_ERR_INVALID;
-  MP_CHECK(ctx, fn >= 0 && fn <= 15 && n >= 0 && x && out && (fn != 4 || y), "bad mp_math_eval arguments");
+  MP_CHECK(ctx, fn >= 0 && fn <= 20 && n >= 0 && x && out && ((fn != 4 && fn != 18) || y), "bad mp_math_eval arguments");
   if (n == 0) return MP_OK;
   MP_HIP(ctx, hipSetDevice(ctx->device));
   int st = MP_OK;
   const double* dx = mp_upload(ctx, WS_IO0, x, (size_t)n, &st);
-  const double* dy = mp_upload(ctx, WS_IO1, fn == 4 ? y : nullptr, (size_t)n, &st);
+  const double* dy = mp_upload(ctx, WS_IO1, (fn == 4 || fn == 18) ? y : nullptr, (size_t)n, &st);
   double* dout = mp_alloc_out(ctx, WS_IO2, out, (size_t)n, &st);
   if (st) return st;
   hipLaunchKernelGGL(math_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, fn, (long long)n, dx,

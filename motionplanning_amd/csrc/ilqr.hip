@@ -28,20 +28,66 @@ struct UPre {  // control-only part of Dynamics (Dynamics.jl:8-12)
   double tdl, beta, cb;
 };
 
-__device__ __forceinline__ UPre upre(double dl) {
+// libm policy.  LM<true>: straight-line FDLIBM cores (include/mp_jlmath.h *_fast): no branch
+// at all, so a whole knot is one basic block the scheduler can interleave; a lane whose
+// argument leaves a core's fast range sets `bad`, and the kernel then re-runs that unit of
+// work (knot / sweep / trial) for the wave with LM<false>, the exact branchy routines.  The
+// cores equal the exact routines bit for bit on their fast range (tests/test_jlmath.py).
+template <bool F> struct LM;
+// A/B builds: -DMP_ILQR_EXACT (exact libm only), -DMP_ILQR_NOREDO (timing only: no fallback)
+#if defined(MP_ILQR_EXACT)
+constexpr bool kFast = false;
+#else
+constexpr bool kFast = true;
+#endif
+#if defined(MP_ILQR_NOREDO)
+constexpr bool kRedo = false;
+#else
+constexpr bool kRedo = true;
+#endif
+#if defined(MP_ILQR_BADSTAT)  // diagnostics build: print arguments that leave a core's range
+__device__ int g_nbad = 0;
+#endif
+template <> struct LM<true> {
+#if !defined(MP_ILQR_BADSTAT)
+  static __device__ __forceinline__ double tan(double x, int& b) { return mpj_tan_fast(x, &b); }
+  static __device__ __forceinline__ double atan(double x, int&) { return mpj_atan_bl(x); }
+  static __device__ __forceinline__ void sincos(double x, double* s, double* c, int& b) { mpj_sincos_wide(x, s, c, &b); }
+  static __device__ __forceinline__ double exp(double x, int& b) { return mpj_exp_fast(x, &b); }
+  static __device__ __forceinline__ double atan2(double y, double x, int& b) { return mpj_atan2_fast(y, x, &b); }
+#else
+  static __device__ double tan(double x, int& b) { int t = 0; double r = mpj_tan_fast(x, &t); if (t) { b |= 1; if (atomicAdd(&g_nbad, 1) < 8) printf("tan %.17g\n", x); } return r; }
+  static __device__ double atan(double x, int&) { return mpj_atan_bl(x); }
+  static __device__ void sincos(double x, double* s, double* c, int& b) { int t = 0; mpj_sincos_wide(x, s, c, &t); if (t) { b |= 2; if (atomicAdd(&g_nbad, 1) < 8) printf("sincos %.17g\n", x); } }
+  static __device__ double exp(double x, int& b) { int t = 0; double r = mpj_exp_fast(x, &t); if (t) { b |= 4; if (atomicAdd(&g_nbad, 1) < 8) printf("exp %.17g\n", x); } return r; }
+  static __device__ double atan2(double y, double x, int& b) { int t = 0; double r = mpj_atan2_fast(y, x, &t); if (t) { b |= 8; if (atomicAdd(&g_nbad, 1) < 8) printf("atan2 %.17g %.17g\n", y, x); } return r; }
+#endif
+};
+template <> struct LM<false> {
+  static __device__ __forceinline__ double tan(double x, int&) { return mpj_tan(x); }
+  static __device__ __forceinline__ double atan(double x, int&) { return mpj_atan(x); }
+  static __device__ __forceinline__ void sincos(double x, double* s, double* c, int&) { mpj_sincos(x, s, c); }
+  static __device__ __forceinline__ double exp(double x, int&) { return mpj_exp(x); }
+  static __device__ __forceinline__ double atan2(double y, double x, int&) { return mpj_atan2(y, x); }
+};
+
+template <bool F>
+__device__ __forceinline__ UPre upre(double dl, int& bad) {
   const double la = 1.56, lb = 1.64;
   UPre q;
-  q.tdl = mpj_tan(dl);
-  q.beta = mpj_atan(la / (la + lb) * q.tdl);
-  q.cb = mpj_cos(q.beta);
+  q.tdl = LM<F>::tan(dl, bad);
+  q.beta = LM<F>::atan(la / (la + lb) * q.tdl, bad);
+  double sb;
+  LM<F>::sincos(q.beta, &sb, &q.cb, bad);  // cos β (the cos of sincos == mpj_cos bit for bit)
   return q;
 }
 
 // Dynamics.jl:1-16
-__device__ __forceinline__ void dyn(const double* s, double ax, const UPre& q, double* d) {
+template <bool F>
+__device__ __forceinline__ void dyn(const double* s, double ax, const UPre& q, double* d, int& bad) {
   const double la = 1.56, lb = 1.64;
   double sb, cbb;
-  mpj_sincos(s[3] + q.beta, &sb, &cbb);
+  LM<F>::sincos(s[3] + q.beta, &sb, &cbb, bad);
   d[0] = s[2] * cbb;
   d[1] = s[2] * sb;
   d[2] = ax;
@@ -49,31 +95,37 @@ __device__ __forceinline__ void dyn(const double* s, double ax, const UPre& q, d
 }
 
 // RK4Integration, Dynamics.jl:18-28
-__device__ __forceinline__ void rk4(const double* s, double ax, const UPre& q, double dT, double* o) {
+template <bool F>
+__device__ __forceinline__ void rk4(const double* s, double ax, const UPre& q, double dT, double* o, int& bad) {
   double k1[4], k2[4], k3[4], k4[4], x2[4], x3[4], x4[4];
-  dyn(s, ax, q, k1);
+  dyn<F>(s, ax, q, k1, bad);
 #pragma unroll
   for (int i = 0; i < 4; i++) x2[i] = s[i] + dT / 2 * k1[i];
-  dyn(x2, ax, q, k2);
+  dyn<F>(x2, ax, q, k2, bad);
 #pragma unroll
   for (int i = 0; i < 4; i++) x3[i] = s[i] + dT / 2 * k2[i];
-  dyn(x3, ax, q, k3);
+  dyn<F>(x3, ax, q, k3, bad);
 #pragma unroll
   for (int i = 0; i < 4; i++) x4[i] = s[i] + dT * k3[i];
-  dyn(x4, ax, q, k4);
+  dyn<F>(x4, ax, q, k4, bad);
 #pragma unroll
   for (int i = 0; i < 4; i++) o[i] = 1.0 / 6 * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]) * dT + s[i];
 }
 
 // sigmoid_boundary, Cost.jl:42-49
-__device__ __forceinline__ double sigmoid_boundary(double st, double mn, double mx) {
+template <bool F>
+__device__ __forceinline__ double sigmoid_boundary(double st, double mn, double mx, int& bad) {
   const double slope = 10, mag = 100;
-  const double c1 = 1 / (1 + mpj_exp(-slope * (st - mx)));
-  const double c2 = 1 / (1 + mpj_exp(slope * (st - mn)));
+  const double c1 = 1 / (1 + LM<F>::exp(-slope * (st - mx), bad));
+  const double c2 = 1 / (1 + LM<F>::exp(slope * (st - mn), bad));
   return mag * (c1 + c2);
 }
-__device__ __forceinline__ double sig_d(double dl) { return sigmoid_boundary(dl, -MPJ_PI / 6, MPJ_PI / 6); }
-__device__ __forceinline__ double sig_a(double ax) { return sigmoid_boundary(ax, -2, 2); }
+template <bool F>
+__device__ __forceinline__ double sig_d(double dl, int& bad) {
+  return sigmoid_boundary<F>(dl, -MPJ_PI / 6, MPJ_PI / 6, bad);
+}
+template <bool F>
+__device__ __forceinline__ double sig_a(double ax, int& bad) { return sigmoid_boundary<F>(ax, -2, 2, bad); }
 
 // StageCost (Cost.jl:10-27 / Parking_ILQR/Cost.jl:21) with the barrier terms supplied
 __device__ __forceinline__ double stage_pre(int variant, const double* s, double ax, double dl, double sd,
@@ -84,8 +136,9 @@ __device__ __forceinline__ double stage_pre(int variant, const double* s, double
            0.01 * (ux * ux) + sd + sa;
   return 10 * (ax * ax) + 10 * (dl * dl) + 0.01 * (ux * ux) + sd + sa;
 }
-__device__ __forceinline__ double stage(int variant, const double* s, const double* u) {
-  return stage_pre(variant, s, u[0], u[1], sig_d(u[1]), sig_a(u[0]));
+template <bool F>
+__device__ __forceinline__ double stage(int variant, const double* s, const double* u, int& bad) {
+  return stage_pre(variant, s, u[0], u[1], sig_d<F>(u[1], bad), sig_a<F>(u[0], bad));
 }
 // TerminalCost, Cost.jl:29-40
 __device__ __forceinline__ double terminal(int variant, const double* s) {
@@ -95,9 +148,10 @@ __device__ __forceinline__ double terminal(int variant, const double* s) {
               1 * ((psi - 0.0) * (psi - 0.0)));
 }
 
-__device__ double total_cost(int variant, int N, const double* X, const double* U) {
+__device__ double total_cost(int variant, int N, const double* X, const double* U) {  // exact libm
   double J = 0.0;
-  for (int i = 0; i < N - 1; i++) J = J + stage(variant, X + 4 * i, U + 2 * i);
+  int bad = 0;
+  for (int i = 0; i < N - 1; i++) J = J + stage<false>(variant, X + 4 * i, U + 2 * i, bad);
   return J + terminal(variant, X + 4 * (N - 1));
 }
 
@@ -112,114 +166,137 @@ __device__ __forceinline__ double cst(int variant, const double* s, const SigCac
   return stage_pre(variant, s, C.a[ia], C.d[id], C.sd[id], C.sa[ia]);
 }
 
-// LocallyLinearizeDynamics + CalculateMatrix for one knot (GetMatrix.jl:3-91)
-__device__ void knot_derivs(const IlqrDev& P, const double* s, const double* u, double* out) {
+// LocallyLinearizeDynamics + CalculateMatrix for one knot (GetMatrix.jl:3-91).  Output
+// component q goes to out[q * stride] (the record is component-major across instances, so
+// consecutive threads store consecutive doubles); every loop is unrolled so the perturbed
+// states stay in registers (no scratch).
+template <bool F>
+__device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
+                                            size_t stride, int& bad) {
   const double e = P.eps;
-  double* A = out;       // [4][4] row-major
-  double* Bm = out + 16; // [4][2]
-  double* lx = out + 24;
-  double* lu = out + 28;
-  double* lxx = out + 30;
-  double* luu = out + 46;
-  double* lux = out + 50;
-  // ---- dynamics Jacobians
-  const UPre q0 = upre(u[1]);
+#define DOUT(q) out[(size_t)(q) * stride]
+  // ---- dynamics Jacobians: A (row-major 4x4) at 0, B (4x2) at 16
+  const UPre q0 = upre<F>(u[1], bad);
   double sp[4], sm[4], fp[4], fm[4];
+#pragma unroll
   for (int i = 0; i < 4; i++) {
+#pragma unroll
     for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
     sp[i] = s[i] + e;
     sm[i] = s[i] - e;
-    rk4(sp, u[0], q0, P.dT, fp);
-    rk4(sm, u[0], q0, P.dT, fm);
-    for (int r = 0; r < 4; r++) A[4 * r + i] = (fp[r] - fm[r]) / (2 * e);
+    rk4<F>(sp, u[0], q0, P.dT, fp, bad);
+    rk4<F>(sm, u[0], q0, P.dT, fm, bad);
+#pragma unroll
+    for (int r = 0; r < 4; r++) DOUT(4 * r + i) = (fp[r] - fm[r]) / (2 * e);
   }
   {  // ax perturbation leaves the δ-only terms unchanged
-    rk4(s, u[0] + e, q0, P.dT, fp);
-    rk4(s, u[0] - e, q0, P.dT, fm);
-    for (int r = 0; r < 4; r++) Bm[2 * r + 0] = (fp[r] - fm[r]) / (2 * e);
-    const UPre qp = upre(u[1] + e), qm = upre(u[1] - e);
-    rk4(s, u[0], qp, P.dT, fp);
-    rk4(s, u[0], qm, P.dT, fm);
-    for (int r = 0; r < 4; r++) Bm[2 * r + 1] = (fp[r] - fm[r]) / (2 * e);
+    rk4<F>(s, u[0] + e, q0, P.dT, fp, bad);
+    rk4<F>(s, u[0] - e, q0, P.dT, fm, bad);
+#pragma unroll
+    for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 0) = (fp[r] - fm[r]) / (2 * e);
+    const UPre qp = upre<F>(u[1] + e, bad), qm = upre<F>(u[1] - e, bad);
+    rk4<F>(s, u[0], qp, P.dT, fp, bad);
+    rk4<F>(s, u[0], qm, P.dT, fm, bad);
+#pragma unroll
+    for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 1) = (fp[r] - fm[r]) / (2 * e);
   }
-  // ---- cost derivatives
+  // ---- cost derivatives: lx 24, lu 28, lxx 30, luu 46, lux 50
   SigCache C;
   C.a[0] = u[0] - 2 * e; C.a[1] = u[0] - e; C.a[2] = u[0]; C.a[3] = u[0] + e; C.a[4] = u[0] + 2 * e;
   C.d[0] = u[1] - 2 * e; C.d[1] = u[1] - e; C.d[2] = u[1]; C.d[3] = u[1] + e; C.d[4] = u[1] + 2 * e;
 #pragma unroll
   for (int t = 0; t < 5; t++) {
-    C.sa[t] = sig_a(C.a[t]);
-    C.sd[t] = sig_d(C.d[t]);
+    C.sa[t] = sig_a<F>(C.a[t], bad);
+    C.sd[t] = sig_d<F>(C.d[t], bad);
   }
   const int V = P.variant;
   const double c12 = 1 / (12 * (e * e)), c4 = 1 / (4 * (e * e));
   const double c0 = cst(V, s, C, 2, 2);
+#pragma unroll
   for (int i = 0; i < 4; i++) {
+#pragma unroll
     for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
     sp[i] = s[i] + e;
     sm[i] = s[i] - e;
-    lx[i] = (cst(V, sp, C, 2, 2) - cst(V, sm, C, 2, 2)) / (2 * e);
+    DOUT(24 + i) = (cst(V, sp, C, 2, 2) - cst(V, sm, C, 2, 2)) / (2 * e);
   }
-  lu[0] = (cst(V, s, C, 3, 2) - cst(V, s, C, 1, 2)) / (2 * e);
-  lu[1] = (cst(V, s, C, 2, 3) - cst(V, s, C, 2, 1)) / (2 * e);
+  DOUT(28) = (cst(V, s, C, 3, 2) - cst(V, s, C, 1, 2)) / (2 * e);
+  DOUT(29) = (cst(V, s, C, 2, 3) - cst(V, s, C, 2, 1)) / (2 * e);
   double t1[4], t2[4], t3[4], t4[4];
+#pragma unroll
   for (int i = 0; i < 4; i++)
+#pragma unroll
     for (int j = 0; j < 4; j++) {
+#pragma unroll
       for (int r = 0; r < 4; r++) { t1[r] = s[r]; t2[r] = s[r]; t3[r] = s[r]; t4[r] = s[r]; }
       if (i == j) {
         t1[i] = s[i] + 2 * e; t2[i] = s[i] + e; t3[i] = s[i] - e; t4[i] = s[i] - 2 * e;
-        lxx[4 * i + j] = c12 * (-cst(V, t1, C, 2, 2) + 16 * cst(V, t2, C, 2, 2) - 30 * c0 +
-                                16 * cst(V, t3, C, 2, 2) - cst(V, t4, C, 2, 2));
+        DOUT(30 + 4 * i + j) = c12 * (-cst(V, t1, C, 2, 2) + 16 * cst(V, t2, C, 2, 2) - 30 * c0 +
+                                      16 * cst(V, t3, C, 2, 2) - cst(V, t4, C, 2, 2));
       } else {
         t1[i] = s[i] + e; t1[j] = s[j] + e;
         t2[i] = s[i] - e; t2[j] = s[j] - e;
         t3[i] = s[i] + e; t3[j] = s[j] - e;
         t4[i] = s[i] - e; t4[j] = s[j] + e;
-        lxx[4 * i + j] = c4 * (cst(V, t1, C, 2, 2) + cst(V, t2, C, 2, 2) - cst(V, t3, C, 2, 2) - cst(V, t4, C, 2, 2));
+        DOUT(30 + 4 * i + j) =
+            c4 * (cst(V, t1, C, 2, 2) + cst(V, t2, C, 2, 2) - cst(V, t3, C, 2, 2) - cst(V, t4, C, 2, 2));
       }
     }
   // luu: index 0 = ax, 1 = δ
-  luu[0] = c12 * (-cst(V, s, C, 4, 2) + 16 * cst(V, s, C, 3, 2) - 30 * c0 + 16 * cst(V, s, C, 1, 2) - cst(V, s, C, 0, 2));
-  luu[3] = c12 * (-cst(V, s, C, 2, 4) + 16 * cst(V, s, C, 2, 3) - 30 * c0 + 16 * cst(V, s, C, 2, 1) - cst(V, s, C, 2, 0));
+  DOUT(46) = c12 * (-cst(V, s, C, 4, 2) + 16 * cst(V, s, C, 3, 2) - 30 * c0 + 16 * cst(V, s, C, 1, 2) - cst(V, s, C, 0, 2));
+  DOUT(49) = c12 * (-cst(V, s, C, 2, 4) + 16 * cst(V, s, C, 2, 3) - 30 * c0 + 16 * cst(V, s, C, 2, 1) - cst(V, s, C, 2, 0));
   // (i=0,j=1): v1 = (+e,+e), v2 = (-e,-e), v3 = (a+e, d-e), v4 = (a-e, d+e)
-  luu[1] = c4 * (cst(V, s, C, 3, 3) + cst(V, s, C, 1, 1) - cst(V, s, C, 3, 1) - cst(V, s, C, 1, 3));
+  DOUT(47) = c4 * (cst(V, s, C, 3, 3) + cst(V, s, C, 1, 1) - cst(V, s, C, 3, 1) - cst(V, s, C, 1, 3));
   // (i=1,j=0): v1 = (+e,+e), v2 = (-e,-e), v3 = (δ+e, a-e), v4 = (δ-e, a+e)
-  luu[2] = c4 * (cst(V, s, C, 3, 3) + cst(V, s, C, 1, 1) - cst(V, s, C, 1, 3) - cst(V, s, C, 3, 1));
+  DOUT(48) = c4 * (cst(V, s, C, 3, 3) + cst(V, s, C, 1, 1) - cst(V, s, C, 1, 3) - cst(V, s, C, 3, 1));
+#pragma unroll
   for (int i = 0; i < 2; i++)
+#pragma unroll
     for (int j = 0; j < 4; j++) {
+#pragma unroll
       for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
       sp[j] = s[j] + e;
       sm[j] = s[j] - e;
       const int ap = i == 0 ? 3 : 2, dp = i == 1 ? 3 : 2, am = i == 0 ? 1 : 2, dm = i == 1 ? 1 : 2;
-      lux[4 * i + j] = c4 * (cst(V, sp, C, ap, dp) + cst(V, sm, C, am, dm) - cst(V, sm, C, ap, dp) -
-                             cst(V, sp, C, am, dm));
+      DOUT(50 + 4 * i + j) = c4 * (cst(V, sp, C, ap, dp) + cst(V, sm, C, am, dm) - cst(V, sm, C, ap, dp) -
+                                   cst(V, sp, C, am, dm));
     }
+#undef DOUT
 }
 
+// Derivative records D[j][q][b] (component-major, instance fastest): thread t = j*B + b, so
+// both the stores here and the backward sweep's per-knot loads are coalesced.
 __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                          const int* active, double* D) {
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const int Nm = P.N - 1;
-  if (t >= (long long)B * Nm) return;
-  const int b = (int)(t / Nm), j = (int)(t % Nm);
-  if (active && !active[b]) return;
-  double out[ND];
-  knot_derivs(P, X + ((size_t)b * P.N + j) * 4, U + ((size_t)b * P.N + j) * 2, out);
-  double* d = D + (size_t)t * ND;
-#pragma unroll
-  for (int i = 0; i < ND; i++) d[i] = out[i];
+  const long long Bn = (long long)B * (P.N - 1);
+  long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= Bn) t = Bn - 1;  // tail lanes recompute the last knot (identical values): all lanes stay active
+  const int j = (int)(t / B), b = (int)(t % B);
+  if (active && __all(!active[b])) return;  // wave-uniform skip; stale records of inactive instances are unused
+  const double* xs = X + ((size_t)b * P.N + j) * 4;
+  const double* us = U + ((size_t)b * P.N + j) * 2;
+  const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
+  const double u[2] = {us[0], us[1]};
+  double* out = D + (size_t)j * ND * B + b;
+  int bad = 0;
+  knot_derivs<kFast>(P, s, u, out, (size_t)B, bad);
+  if (kFast && kRedo && __any(bad)) {  // some lane left a straight-line core's range: redo the wave exactly
+    int d = 0;
+    knot_derivs<false>(P, s, u, out, (size_t)B, d);
+  }
 }
 
 // pinv of a 2x2 (closed-form SVD; identical operation sequence to oracle/or_ilqr.c or_pinv2)
-__device__ void pinv2(const double* M, double* Pm) {
+template <bool FT>
+__device__ __forceinline__ void pinv2(const double* M, double* Pm, int& bad) {
   const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
   const double Q = mpj_sqrt(E * E + H * H), R = mpj_sqrt(F * F + G * G);
   const double sx = Q + R, sy = Q - R;
-  const double a1 = mpj_atan2(G, F), a2 = mpj_atan2(H, E);
+  const double a1 = LM<FT>::atan2(G, F, bad), a2 = LM<FT>::atan2(H, E, bad);
   const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
   double st, ct, sp, cp;
-  mpj_sincos(th, &st, &ct);
-  mpj_sincos(ph, &sp, &cp);
+  LM<FT>::sincos(th, &st, &ct, bad);
+  LM<FT>::sincos(ph, &sp, &cp, bad);
   const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
   const double tol = 4.440892098500626e-16 * smax;
   const double i1 = __builtin_fabs(sx) > tol ? 1.0 / sx : 0.0;
@@ -230,27 +307,39 @@ __device__ void pinv2(const double* M, double* Pm) {
   Pm[3] = -st * i1 * sp + ct * i2 * cp;
 }
 
-// ILQR.jl:46-67 for instance b
-__global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, const double* X, const double* D,
-                                                           const int* active, double* kout, double* Kout) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || (active && !active[b])) return;
+// ILQR.jl:46-67 for instance b: one thread per instance (the sweep is a serial chain in j).
+// The derivative record of knot j-1 is loaded while knot j is processed (coalesced: the
+// records are component-major, instance fastest), so the chain never waits on memory.
+template <bool FT>
+__device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, bool live, const double* X,
+                                               const double* D, double* kout, double* Kout, int& bad) {
   const int N = P.N;
   const double e = P.eps;
   const int V = P.variant;
+  const size_t ks = (size_t)ND * B;  // knot stride of the records
+  const double* Db = D + b;
+  double cur[ND];
+#pragma unroll
+  for (int q = 0; q < ND; q++) cur[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
   double Vx[4], Vxx[16];
   {  // CalculateMatrix(StatesList[:, end], [0 0], TerminalCost): only lx, lxx are used
-    const double* s = X + ((size_t)b * N + N - 1) * 4;
+    const double* xs = X + ((size_t)b * N + N - 1) * 4;
+    const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
     double sp[4], sm[4], t1[4], t2[4], t3[4], t4[4];
     const double c12 = 1 / (12 * (e * e)), c4 = 1 / (4 * (e * e));
+#pragma unroll
     for (int i = 0; i < 4; i++) {
+#pragma unroll
       for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
       sp[i] = s[i] + e;
       sm[i] = s[i] - e;
       Vx[i] = (terminal(V, sp) - terminal(V, sm)) / (2 * e);
     }
+#pragma unroll
     for (int i = 0; i < 4; i++)
+#pragma unroll
       for (int j = 0; j < 4; j++) {
+#pragma unroll
         for (int r = 0; r < 4; r++) { t1[r] = s[r]; t2[r] = s[r]; t3[r] = s[r]; t4[r] = s[r]; }
         if (i == j) {
           t1[i] = s[i] + 2 * e; t2[i] = s[i] + e; t3[i] = s[i] - e; t4[i] = s[i] - 2 * e;
@@ -266,110 +355,212 @@ __global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, con
       }
   }
   for (int j = N - 2; j >= 0; j--) {
-    const double* d = D + ((size_t)b * (N - 1) + j) * ND;
-    double A[16], Bm[8], lx[4], lu[2], lxx[16], luu[4], lux[8];
-    for (int i = 0; i < 16; i++) A[i] = d[i];
-    for (int i = 0; i < 8; i++) Bm[i] = d[16 + i];
-    for (int i = 0; i < 4; i++) lx[i] = d[24 + i];
-    lu[0] = d[28]; lu[1] = d[29];
-    for (int i = 0; i < 16; i++) lxx[i] = d[30 + i];
-    for (int i = 0; i < 4; i++) luu[i] = d[46 + i];
-    for (int i = 0; i < 8; i++) lux[i] = d[50 + i];
+    double nxt[ND];
+    const size_t jn = j > 0 ? (size_t)(j - 1) : 0;
+#pragma unroll
+    for (int q = 0; q < ND; q++) nxt[q] = Db[jn * ks + (size_t)q * B];
+    const double* A = cur;        // [4][4]
+    const double* Bm = cur + 16;  // [4][2]
+    const double* lx = cur + 24;
+    const double* lu = cur + 28;
+    const double* lxx = cur + 30;
+    const double* luu = cur + 46;
+    const double* lux = cur + 50;
     double Qx[4], Qu[2], Qxx[16], Quu[4], Qux[8], T44[16], T24[8], Pm[4];
+#pragma unroll
     for (int i = 0; i < 4; i++) {
       double acc = A[0 * 4 + i] * Vx[0];
+#pragma unroll
       for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vx[k];
       Qx[i] = lx[i] + acc;
     }
+#pragma unroll
     for (int i = 0; i < 2; i++) {
       double acc = Bm[0 * 2 + i] * Vx[0];
+#pragma unroll
       for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vx[k];
       Qu[i] = lu[i] + acc;
     }
+#pragma unroll
     for (int i = 0; i < 4; i++)
+#pragma unroll
       for (int c = 0; c < 4; c++) {
         double acc = A[0 * 4 + i] * Vxx[0 * 4 + c];
+#pragma unroll
         for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vxx[k * 4 + c];
         T44[4 * i + c] = acc;
       }
+#pragma unroll
     for (int i = 0; i < 4; i++)
+#pragma unroll
       for (int c = 0; c < 4; c++) {
         double acc = T44[4 * i + 0] * A[0 * 4 + c];
+#pragma unroll
         for (int k = 1; k < 4; k++) acc = acc + T44[4 * i + k] * A[k * 4 + c];
         Qxx[4 * i + c] = lxx[4 * i + c] + acc;
       }
+#pragma unroll
     for (int i = 0; i < 2; i++)
+#pragma unroll
       for (int c = 0; c < 4; c++) {
         double acc = Bm[0 * 2 + i] * Vxx[0 * 4 + c];
+#pragma unroll
         for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vxx[k * 4 + c];
         T24[4 * i + c] = acc;
       }
+#pragma unroll
     for (int i = 0; i < 2; i++)
+#pragma unroll
       for (int c = 0; c < 2; c++) {
         double acc = T24[4 * i + 0] * Bm[0 * 2 + c];
+#pragma unroll
         for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * Bm[k * 2 + c];
         Quu[2 * i + c] = luu[2 * i + c] + acc;
       }
+#pragma unroll
     for (int i = 0; i < 2; i++)
+#pragma unroll
       for (int c = 0; c < 4; c++) {
         double acc = T24[4 * i + 0] * A[0 * 4 + c];
+#pragma unroll
         for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * A[k * 4 + c];
         Qux[4 * i + c] = lux[4 * i + c] + acc;
       }
-    pinv2(Quu, Pm);
+    pinv2<FT>(Quu, Pm, bad);
     double kk[2], KK[8];
+#pragma unroll
     for (int i = 0; i < 2; i++) kk[i] = (-Pm[2 * i + 0]) * Qu[0] + (-Pm[2 * i + 1]) * Qu[1];
+#pragma unroll
     for (int i = 0; i < 2; i++)
+#pragma unroll
       for (int c = 0; c < 4; c++) KK[4 * i + c] = (-Pm[2 * i + 0]) * Qux[0 * 4 + c] + (-Pm[2 * i + 1]) * Qux[1 * 4 + c];
-    double* ko = kout + ((size_t)b * (N - 1) + j) * 2;
-    double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8;
-    ko[0] = kk[0];
-    ko[1] = kk[1];
-    for (int r = 0; r < 2; r++)
-      for (int c = 0; c < 4; c++) Ko[2 * c + r] = KK[4 * r + c];
+    if (live) {
+      double* ko = kout + ((size_t)b * (N - 1) + j) * 2;
+      double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8;
+      ko[0] = kk[0];
+      ko[1] = kk[1];
+#pragma unroll
+      for (int r = 0; r < 2; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) Ko[2 * c + r] = KK[4 * r + c];
+    }
     double qk[2];
+#pragma unroll
     for (int i = 0; i < 2; i++) qk[i] = Quu[2 * i + 0] * kk[0] + Quu[2 * i + 1] * kk[1];
+#pragma unroll
     for (int i = 0; i < 4; i++) Vx[i] = Qx[i] - (KK[0 * 4 + i] * qk[0] + KK[1 * 4 + i] * qk[1]);
     double KQ[8];
+#pragma unroll
     for (int i = 0; i < 4; i++)
+#pragma unroll
       for (int c = 0; c < 2; c++) KQ[2 * i + c] = KK[0 * 4 + i] * Quu[0 * 2 + c] + KK[1 * 4 + i] * Quu[1 * 2 + c];
+#pragma unroll
     for (int i = 0; i < 4; i++)
+#pragma unroll
       for (int c = 0; c < 4; c++)
         Vxx[4 * i + c] = Qxx[4 * i + c] - (KQ[2 * i + 0] * KK[0 * 4 + c] + KQ[2 * i + 1] * KK[1 * 4 + c]);
+#pragma unroll
+    for (int q = 0; q < ND; q++) cur[q] = nxt[q];
   }
 }
 
-// ILQR.jl:72-80: one closed-loop roll out at step size alpha; returns TotalCost
-__device__ double forward_trial(const IlqrDev& P, const double* X, const double* U, const double* k,
-                                const double* Kg, double alpha, double* Xn, double* Un) {
-  const int N = P.N;
-  for (int r = 0; r < 4; r++) Xn[r] = X[r];
-  for (int i = 0; i < N - 1; i++) {
-    double dx[4], u[2];
-    for (int r = 0; r < 4; r++) dx[r] = Xn[4 * i + r] - X[4 * i + r];
-    for (int r = 0; r < 2; r++) {
-      double acc = Kg[8 * i + 2 * 0 + r] * dx[0];
-      for (int c = 1; c < 4; c++) acc = acc + Kg[8 * i + 2 * c + r] * dx[c];
-      u[r] = (U[2 * i + r] + alpha * k[2 * i + r]) + acc;
-    }
-    Un[2 * i] = u[0];
-    Un[2 * i + 1] = u[1];
-    const UPre q = upre(u[1]);
-    rk4(Xn + 4 * i, u[0], q, P.dT, Xn + 4 * (i + 1));
+__global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, const double* X, const double* D,
+                                                           const int* active, double* kout, double* Kout) {
+  // every lane stays active (the straight-line libm selects with wave ballots): lanes past B or
+  // of converged instances recompute a live instance's sweep and store nothing
+  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < B && (!active || active[b0]);
+  if (__all(!live)) return;
+  const int b = b0 < B ? b0 : B - 1;
+  int bad = 0;
+  backward_sweep<kFast>(P, B, b, live, X, D, kout, Kout, bad);
+  if (kFast && kRedo && __any(bad)) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
+    int d = 0;
+    backward_sweep<false>(P, B, b, live, X, D, kout, Kout, d);
   }
-  Un[2 * (N - 1)] = 0.0;
-  Un[2 * (N - 1) + 1] = 0.0;
-  return total_cost(P.variant, N, Xn, Un);
+}
+
+// ILQR.jl:72-80: one closed-loop roll out at step size alpha; returns TotalCost.  The rolled
+// state stays in registers (Xn is only written), the next knot's reference state, gains and
+// nominal control are loaded one knot ahead, and TotalCost (Cost.jl:1-8) is accumulated in
+// the loop in the reference's order (J = J + stage_i, then + terminal).
+template <bool F>
+__device__ double forward_trial(const IlqrDev& P, const double* X, const double* U, const double* k,
+                                const double* Kg, double alpha, double* Xn, double* Un, bool wr, int& bad) {
+  const int N = P.N;
+  double x[4] = {X[0], X[1], X[2], X[3]};
+  if (wr)
+#pragma unroll
+    for (int r = 0; r < 4; r++) Xn[r] = x[r];
+  double xr[4], Kr[8], kr[2], ur[2];
+#pragma unroll
+  for (int r = 0; r < 4; r++) xr[r] = X[r];
+#pragma unroll
+  for (int r = 0; r < 8; r++) Kr[r] = Kg[r];
+  kr[0] = k[0]; kr[1] = k[1];
+  ur[0] = U[0]; ur[1] = U[1];
+  double J = 0.0;
+  for (int i = 0; i < N - 1; i++) {
+    const int in = i + 2 < N ? i + 1 : i;  // prefetch knot i+1 (clamped)
+    double nxr[4], nK[8], nk[2], nu[2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) nxr[r] = X[4 * in + r];
+#pragma unroll
+    for (int r = 0; r < 8; r++) nK[r] = Kg[8 * in + r];
+    nk[0] = k[2 * in]; nk[1] = k[2 * in + 1];
+    nu[0] = U[2 * in]; nu[1] = U[2 * in + 1];
+    double dx[4], u[2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) dx[r] = x[r] - xr[r];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      double acc = Kr[2 * 0 + r] * dx[0];
+#pragma unroll
+      for (int c = 1; c < 4; c++) acc = acc + Kr[2 * c + r] * dx[c];
+      u[r] = (ur[r] + alpha * kr[r]) + acc;
+    }
+    if (wr) {
+      Un[2 * i] = u[0];
+      Un[2 * i + 1] = u[1];
+    }
+    J = J + stage<F>(P.variant, x, u, bad);
+    const UPre q = upre<F>(u[1], bad);
+    double xn[4];
+    rk4<F>(x, u[0], q, P.dT, xn, bad);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      x[r] = xn[r];
+      if (wr) Xn[4 * (i + 1) + r] = xn[r];
+      xr[r] = nxr[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r++) Kr[r] = nK[r];
+    kr[0] = nk[0]; kr[1] = nk[1];
+    ur[0] = nu[0]; ur[1] = nu[1];
+  }
+  if (wr) {
+    Un[2 * (N - 1)] = 0.0;
+    Un[2 * (N - 1) + 1] = 0.0;
+  }
+  return J + terminal(P.variant, x);
 }
 
 __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                           const double* k, const double* Kg, const double* alpha,
                                                           double* Xn, double* Un, double* Jn) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < B;
+  const size_t b = live ? b0 : B - 1;  // all lanes active (ballot-based libm); tail lanes store nothing
   const size_t N = P.N;
-  Jn[b] = forward_trial(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha[b],
-                        Xn + b * N * 4, Un + b * N * 2);
+  int bad = 0;
+  double J = forward_trial<kFast>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
+                                 alpha[b], Xn + b * N * 4, Un + b * N * 2, live, bad);
+  if (kFast && kRedo && __any(bad)) {  // redo the wave's trials with the exact libm
+    int d = 0;
+    J = forward_trial<false>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha[b],
+                             Xn + b * N * 4, Un + b * N * 2, live, d);
+  }
+  if (live) Jn[b] = J;
 }
 
 // ILQR.jl:70-88 after the backward sweep: line search, accept, convergence test.
@@ -377,8 +568,10 @@ __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, cons
 __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
                                                          const double* Kg, double* Xn, double* Un, double* Jcur,
                                                          int* active, int* iters, int* flags, int* n_active) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B || !active[b]) return;
+  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < B && active[b0];
+  if (__all(!live)) return;
+  const size_t b = b0 < B ? b0 : B - 1;
   const size_t N = P.N;
   double* Xb = X + b * N * 4;
   double* Ub = U + b * N * 2;
@@ -388,13 +581,27 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   double Jn = J;
   double alpha = 1.0;
   int ls = 0;
-  while (Jn >= J) {
-    Jn = forward_trial(P, Xb, Ub, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha, Xnb, Unb);
-    alpha = alpha / 2;
-    ls++;
-    if (P.alpha_floor > 0 && alpha <= P.alpha_floor) break;
-    if (ls >= P.max_ls) { atomicOr(flags + b, 1); break; }
+  // The halving loop runs wave-uniformly (the libm selects with ballots): a lane whose search
+  // has ended keeps its accepted trial (stores predicated off) until the last lane is done.
+  bool searching = live && Jn >= J;
+  while (__any(searching)) {
+    int bad = 0;
+    double jt = forward_trial<kFast>(P, Xb, Ub, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha, Xnb, Unb, searching, bad);
+    if (kFast && kRedo && __any(bad)) {
+      int d = 0;
+      jt = forward_trial<false>(P, Xb, Ub, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha, Xnb, Unb, searching, d);
+    }
+    if (searching) {  // ILQR.jl:76-83: the break tests run before the loop condition
+      Jn = jt;
+      alpha = alpha / 2;
+      ls++;
+      bool brk = false;
+      if (P.alpha_floor > 0 && alpha <= P.alpha_floor) brk = true;
+      else if (ls >= P.max_ls) { atomicOr(flags + b, 1); brk = true; }
+      searching = !brk && Jn >= J;
+    }
   }
+  if (!live) return;
   for (size_t i = 0; i < N * 4; i++) Xb[i] = Xnb[i];
   for (size_t i = 0; i < N * 2; i++) Ub[i] = Unb[i];
   Jcur[b] = Jn;
@@ -409,26 +616,53 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   if (go) atomicAdd(n_active, 1);
 }
 
+// Initial guess roll out (ILQR.jl:31-37) with TotalCost accumulated in order.
+template <bool F>
+__device__ __forceinline__ double rollout_one(const IlqrDev& P, const double* x0, const double* Ub, double* Xb,
+                                              bool live, int& bad) {
+  const size_t N = P.N;
+  double x[4] = {x0[0], x0[1], x0[2], x0[3]};
+  if (live)
+#pragma unroll
+    for (int r = 0; r < 4; r++) Xb[r] = x[r];
+  double Jb = 0.0;
+  for (size_t i = 0; i + 1 < N; i++) {
+    const double u[2] = {Ub[2 * i], Ub[2 * i + 1]};
+    Jb = Jb + stage<F>(P.variant, x, u, bad);
+    const UPre q = upre<F>(u[1], bad);
+    double xn[4];
+    rk4<F>(x, u[0], q, P.dT, xn, bad);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      x[r] = xn[r];
+      if (live) Xb[4 * (i + 1) + r] = xn[r];
+    }
+  }
+  return Jb + terminal(P.variant, x);
+}
+
 __global__ __launch_bounds__(64) void ilqr_rollout_kernel(IlqrDev P, int B, const double* x0, const double* U,
                                                           double* X, double* J) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
+  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = b0 < B;
+  const size_t b = live ? b0 : B - 1;  // all lanes active (ballot-based libm)
   const size_t N = P.N;
-  double* Xb = X + b * N * 4;
-  const double* Ub = U + b * N * 2;
-  for (int r = 0; r < 4; r++) Xb[r] = x0[4 * b + r];
-  for (size_t i = 0; i + 1 < N; i++) {
-    const UPre q = upre(Ub[2 * i + 1]);
-    rk4(Xb + 4 * i, Ub[2 * i], q, P.dT, Xb + 4 * (i + 1));
+  int bad = 0;
+  double Jb = rollout_one<kFast>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, bad);
+  if (kFast && kRedo && __any(bad)) {
+    int d = 0;
+    Jb = rollout_one<false>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, d);
   }
-  J[b] = total_cost(P.variant, (int)N, Xb, Ub);
+  if (live) J[b] = Jb;
 }
 
 __global__ void ilqr_init_kernel(IlqrDev P, int B, const double* X, const double* U, double* Jcur, int* active,
                                  int* iters, int* flags) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  Jcur[b] = total_cost(P.variant, P.N, X + (size_t)b * P.N * 4, U + (size_t)b * P.N * 2);
+  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = b0 < B ? b0 : B - 1;  // all lanes active (ballot-based libm)
+  const double J = total_cost(P.variant, P.N, X + (size_t)b * P.N * 4, U + (size_t)b * P.N * 2);
+  if (b0 >= B) return;
+  Jcur[b] = J;
   active[b] = 1;
   iters[b] = 1;
   flags[b] = 0;

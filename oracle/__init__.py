@@ -32,7 +32,7 @@ def lib():
         if not os.path.exists(LIB):
             build()
         L = ctypes.CDLL(LIB)
-        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "atan_tab", "modpi_bl", "sin_bl", "cos_bl"]:
+        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "atan_tab", "modpi_bl", "sin_bl", "cos_bl", "exp_bl", "tan_bl", "sin_wide", "cos_wide"]:
             f = getattr(L, "or_m_" + n)
             f.restype = _D
             f.argtypes = [_D]
@@ -40,6 +40,8 @@ def lib():
         L.or_m_atan2.argtypes = [_D, _D]
         L.or_m_atan2_bl.restype = _D
         L.or_m_atan2_bl.argtypes = [_D, _D]
+        L.or_m_atan2_sel.restype = _D
+        L.or_m_atan2_sel.argtypes = [_D, _D]
         L.or_vehicle_dynamics.restype = _D
         L.or_vehicle_dynamics.argtypes = [_V, _V, _V]
         L.or_rollout.restype = _D

@@ -167,6 +167,16 @@ def test_plant_replay_mppi_csv(ctx):
             assert np.abs(his[b, -1] - rows[j[0], 1:]).max() < 1e-12
 
 
+EXP_EDGES = np.array([0.34657359027997264, 0.3465735902799727, 1.0397207708399179, 1.039720770839918, 7.450580596923828e-09,
+                      3.725290298461914e-09, 703.9, -703.9, 704.0, -708.4, 709.78, -745.2, 800.0, np.inf, -np.inf,
+                      0.5, -0.5, 1.0, -1.0, 2.0, -2.0, 5.23, -10.47])
+TAN_EDGES = np.array([0.6743884, 0.67438866, -0.67438866, 0.7853981633974483, -0.7853981633974483,
+                      0.7853981633974484, 1e-9, -1e-9, 0.5235987755982988, -0.5235987755982988, 1.2, -3.0])
+ATAN2_EDGES = np.array([(0.0, -1.0), (-0.0, -1.0), (1.0, 0.0), (-1.0, 0.0), (2.0, 1.0), (1e-300, 1e300),
+                        (1e300, 1e-300), (np.inf, 1.0), (1.0, np.inf), (np.inf, -np.inf), (3.0, 3.0), (-2.0, 2.0),
+                        (1e-17, -1.0), (-1e-17, -1.0), (1.0, 1e-17), (-3.0, -3.0)])
+
+
 def test_jlmath_bitexact(ctx):
     """Every device libm routine (exact FDLIBM restatements and the branch-free variants of the hot
     kernels) equals the CPU build bit for bit, incl. range edges and the kπ/2 Cody-Waite points."""
@@ -175,19 +185,25 @@ def test_jlmath_bitexact(ctx):
     r = np.random.default_rng(0)
     ranges = {0: (-30, 30), 1: (-30, 30), 2: (-1.5, 1.5), 3: (-60, 60), 4: (-5, 5), 5: (-1, 1), 6: (-1, 1),
               7: (-700, 700), 8: (1e-300, 1e4), 9: (-40, 40), 10: (0, 1e6), 11: (-15, 15), 12: (-60, 60),
-              13: (-60, 60), 14: (-10, 10), 15: (-10, 10)}
+              13: (-60, 60), 14: (-10, 10), 15: (-10, 10), 16: (-720, 720), 17: (-1.0, 1.0), 18: (-5, 5),
+              19: (-1e6, 1e6), 20: (-12, 12)}
     names = {0: "sin", 1: "cos", 2: "tan", 3: "atan", 4: "atan2", 5: "asin", 6: "acos", 7: "exp", 8: "log",
-             9: "modpi", 11: "modpi", 12: "atan", 13: "atan", 14: "sin", 15: "cos"}
+             9: "modpi", 11: "modpi", 12: "atan", 13: "atan", 14: "sin", 15: "cos", 16: "exp", 17: "tan",
+             18: "atan2", 19: "sin", 20: "cos"}
     edges = np.array([0.0, -0.0, 1e-300, -1e-300, 0.4375, 0.6875, 1.1875, 2.4375, np.pi / 4, np.pi / 2, np.pi,
                       2 * np.pi, 3 * np.pi / 4, 4 * np.pi, -4 * np.pi, 1e5, -1e5] +  # |x| < 2^20 pi/2 (Cody-Waite domain)
                      [np.nextafter(k * np.pi / 2, d) for k in range(-6, 7) for d in (-np.inf, np.inf)])
     for fn, (lo, hi) in ranges.items():
-        x = np.r_[r.uniform(lo, hi, 20000), edges if fn in (11, 12, 13, 14, 15) else []]
+        x = np.r_[r.uniform(lo, hi, 20000), edges if fn in (11, 12, 13, 14, 15, 16, 17, 19, 20) else [],
+                  EXP_EDGES if fn == 16 else [], TAN_EDGES if fn == 17 else []]
         y = r.uniform(-5, 5, len(x))
+        if fn == 18:
+            y[:len(ATAN2_EDGES)] = ATAN2_EDGES[:, 1]
+            x[:len(ATAN2_EDGES)] = ATAN2_EDGES[:, 0]
         out = np.zeros_like(x)
         ctx.check(ctx.lib.mp_math_eval(ctx.handle, fn, len(x), ptr(x), ptr(y), ptr(out)))
         if fn == 10:
             assert np.array_equal(out, np.sqrt(x))
             continue
-        cpu = np.array([oracle.m(names[fn], a, b) if fn == 4 else oracle.m(names[fn], a) for a, b in zip(x, y)])
+        cpu = np.array([oracle.m(names[fn], a, b) if fn in (4, 18) else oracle.m(names[fn], a) for a, b in zip(x, y)])
         assert np.array_equal(out.view(np.int64), cpu.view(np.int64)), (fn, names[fn], x[out.view(np.int64) != cpu.view(np.int64)][:5])

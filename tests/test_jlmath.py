@@ -87,3 +87,44 @@ def test_atan2_branchless_core_bitidentical():
     for y, x in pts:
         a, b = oracle.m("atan2_bl", float(y), float(x)), oracle.m("atan2", float(y), float(x))
         assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], (y, x)
+
+
+def test_exp_tan_atan2_select_variants_bitidentical():
+    """mpj_exp_bl / mpj_tan_bl / mpj_atan2_sel (one-basic-block forms used by the iLQR kernels) ==
+    the exact FDLIBM routines, incl. the reduction-range edges and the slow-path cases."""
+    r = np.random.default_rng(11)
+    xs = np.concatenate([r.uniform(-12, 12, 20000), r.uniform(-720, 720, 5000), r.uniform(-1e-7, 1e-7, 1000),
+                         np.array([0.34657359027997264, 0.3465735902799727, 1.0397207708399179, 1.039720770839918,
+                                   7.450580596923828e-09, 3.725290298461914e-09, 703.9, -703.9, 704.0, -708.4,
+                                   709.78, -745.2, 800.0, 0.0, -0.0, np.inf, -np.inf, np.nan])])
+    for x in xs:
+        a, b = oracle.m("exp_bl", float(x)), oracle.m("exp", float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), x
+    ts = np.concatenate([r.uniform(-0.8, 0.8, 20000), r.uniform(-3, 3, 2000),
+                         np.array([0.6743884, 0.67438866, -0.67438866, 0.7853981633974483, -0.7853981633974483,
+                                   0.7853981633974484, 1e-9, -1e-9, 0.0, -0.0, 0.5235987755982988, np.inf])])
+    for x in ts:
+        a, b = oracle.m("tan_bl", float(x)), oracle.m("tan", float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), x
+    pts = list(r.uniform(-5, 5, (20000, 2))) + [(0.0, -1.0), (-0.0, -1.0), (1.0, 0.0), (-1.0, 0.0), (2.0, 1.0),
+                                                (1e-300, 1e300), (1e300, 1e-300), (np.inf, 1.0), (1.0, np.inf),
+                                                (np.inf, -np.inf), (3.0, 3.0), (-2.0, 2.0), (1e-17, -1.0),
+                                                (-1e-17, -1.0), (1.0, 1e-17), (-3.0, -3.0), (0.5, 1.0)]
+    for y, x in pts:
+        a, b = oracle.m("atan2_sel", float(y), float(x)), oracle.m("atan2", float(y), float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], (y, x)
+
+
+def test_sincos_wide_bitidentical():
+    """mpj_sincos_wide (straight-line cw2c + 3-stage Cody-Waite, iLQR kernels) == mpj_sin / mpj_cos,
+    incl. arguments next to k*pi/2 (the cwext cases) and |x| up to 2^20*pi/2."""
+    r = np.random.default_rng(12)
+    near = np.concatenate([k * np.pi / 2 + r.uniform(-3e-7, 3e-7, 300) for k in range(-12, 13)])
+    xs = np.concatenate([r.uniform(-10, 10, 20000), r.uniform(-1e6, 1e6, 5000), near, r.uniform(-1e-8, 1e-8, 500),
+                         [np.nextafter(k * np.pi / 2, d) for k in range(-40, 41) for d in (-np.inf, np.inf)],
+                         np.array([0.0, -0.0, 1.5707961554653271, -1.5707961387395493, 1.6e6, -1.6e6,
+                                   np.inf, -np.inf])])
+    for x in xs:
+        for fw, fe in (("sin_wide", "sin"), ("cos_wide", "cos")):
+            a, b = oracle.m(fw, float(x)), oracle.m(fe, float(x))
+            assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), (fw, x)
