@@ -849,6 +849,83 @@ MPJ_FN double mpj_tan_fast(double x, int* bad) {
   return MPJ_SEL(ix < 0x3e400000, x, MPJ_SEL(big, rb, ww));
 }
 
+/* e_rem_pio2.c for finite |x| < 2^20·π/2 as straight-line code: the cw2c reduction (|n| =
+ * 1..4 by range) and, selected per lane, the 3-stage Cody–Waite mpj_cwext uses beyond 9π/4
+ * and next to kπ/2 (its two stage tests become selects).  Returns n; equals mpj_rem_pio2 bit
+ * for bit on that range (the caller flags larger |x|, NaN and Inf). */
+MPJ_FN int mpj_rem_pio2_sl(double x, double* y0, double* y1) {
+  const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
+  const int med = (xhp <= 0x400f6a7au && (xhp & 0xfffffu) == 0x921fbu) || xhp == 0x4012d97cu ||
+                  xhp == 0x401921fbu || xhp > 0x401c463bu;
+  const int na = 1 + (xhp > 0x4002d97cu) + (xhp > 0x400f6a7au) + (xhp > 0x4015fdbcu);
+  const int ni = x > 0.0 ? na : -na;
+  double c0, c1;
+  mpj_cw2c(x, (double)ni, 0, &c0, &c1);
+  const double fn = mpj_round(MPJ_SEL(xhp >= 0x413921fbu, 0.0, x) * MPJ_INVPIO2);
+  const int32_t j = (int32_t)(xhp >> 20);
+  const double r1 = mpj_fma(-fn, MPJ_PIO2_1, x), w1 = fn * MPJ_PIO2_1T, a1 = r1 - w1;
+  const int32_t i1 = j - (int32_t)((mpj_hi(a1) >> 20) & 0x7ff);
+  const double w2a = fn * MPJ_PIO2_2, r2 = r1 - w2a;
+  const double w2 = mpj_fma(fn, MPJ_PIO2_2T, -((r1 - r2) - w2a)), a2 = r2 - w2;
+  const int32_t i2 = j - (int32_t)((mpj_hi(a2) >> 20) & 0x7ff);
+  const double w3a = fn * MPJ_PIO2_3, r3 = r2 - w3a;
+  const double w3 = mpj_fma(fn, MPJ_PIO2_3T, -((r2 - r3) - w3a)), a3 = r3 - w3;
+  const int s2 = i1 > 16, s3 = s2 && i2 > 49;
+  const double er = MPJ_SEL(s3, r3, MPJ_SEL(s2, r2, r1)), ew = MPJ_SEL(s3, w3, MPJ_SEL(s2, w2, w1));
+  const double ea = MPJ_SEL(s3, a3, MPJ_SEL(s2, a2, a1));
+  *y0 = MPJ_SEL(med, ea, c0);
+  *y1 = MPJ_SEL(med, (er - ea) - ew, c1);
+  return med ? (int)fn : ni;
+}
+
+/* tan for every finite |x| < 2^20·π/2 as one basic block: mpj_rem_pio2_sl, then k_tan.c with
+ * all three result forms (|x| >= 0.6744 reflection, iy = 1, and the iy = -1 -1/tan form with
+ * its zero-low-word correction) evaluated and selected.  |x| <= π/4 takes k_tan(x, 0, 1) as
+ * s_tan.c does.  NaN, Inf and larger |x| set *bad. */
+MPJ_FN double mpj_tan_wide(double x, int* bad) {
+  const double T0 = 3.33333333333334091986e-01, T1 = 1.33333333333201242699e-01,
+               T2 = 5.39682539762260521377e-02, T3 = 2.18694882948595424599e-02,
+               T4 = 8.86323982359930005737e-03, T5 = 3.59207910759131235356e-03,
+               T6 = 1.45620945432529025516e-03, T7 = 5.88041240820264096874e-04,
+               T8 = 2.46463134818469906812e-04, T9 = 7.81794442939557092300e-05,
+               T10 = 7.14072491382608190305e-05, T11 = -1.85586374855275456654e-05,
+               T12 = 2.59073051863633712884e-05, pio4lo = 3.06161699786838301793e-17;
+  const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
+  *bad |= xhp >= 0x413921fbu;
+  const int small = xhp <= 0x3fe921fbu;
+  double r0, r1;
+  const int n = mpj_rem_pio2_sl(MPJ_SEL(small, 0.0, x), &r0, &r1);
+  const double xa = MPJ_SEL(small, x, r0), ya = MPJ_SEL(small, 0.0, r1);
+  const int iy = small ? 1 : 1 - ((n & 1) << 1);
+  /* k_tan(xa, ya, iy) */
+  const int32_t hx = (int32_t)mpj_hi(xa);
+  const int32_t ix = hx & 0x7fffffff;
+  const int big = ix >= 0x3FE59428;
+  const int neg = hx < 0;
+  const double xn = MPJ_SEL(neg, -xa, xa), yn = MPJ_SEL(neg, -ya, ya);
+  const double xb = (MPJ_PIO4 - xn) + (pio4lo - yn);
+  const double xx = MPJ_SEL(big, xb, xa), y = MPJ_SEL(big, 0.0, ya);
+  const double z = xx * xx;
+  const double w = z * z;
+  double r = mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, T11, T9), T7), T5), T3), T1);
+  const double v = z * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, T12, T10), T8), T6), T4), T2);
+  const double s = z * xx;
+  r = y + z * (s * (r + v) + y);
+  r += T0 * s;
+  const double ww = xx + r;
+  const double vy = (double)iy;
+  const double rb = (double)(1 - ((hx >> 30) & 2)) * (vy - 2.0 * (xx - (ww * ww / (ww + vy) - r)));
+  /* iy == -1, |xa| < 0.6744: -1/(x+r) with the zero-low-word correction */
+  const double zl = mpj_zero_lo(ww);
+  const double vl = r - (zl - xx);
+  const double a = -1.0 / ww;
+  const double t = mpj_zero_lo(a);
+  const double sl = 1.0 + t * zl;
+  const double rm = t + a * (sl + t * vl);
+  const double res = MPJ_SEL(big, rb, MPJ_SEL(iy == 1, ww, rm));
+  return MPJ_SEL(xhp < 0x3e400000u, x, res);
+}
+
 MPJ_FN double mpj_tan_bl(double x) {
   if (MPJ_ANY((mpj_hi(x) & 0x7fffffffu) > 0x3fe921fbu)) return mpj_tan(x);
   int bad = 0;

@@ -22,7 +22,14 @@ constexpr int ND = 58;  // derivative record: A16 B8 lx4 lu2 lxx16 luu4 lux8
 struct IlqrDev {
   int N, variant, max_iter, max_ls;
   double dT, eps, alpha_floor, tol;
+  int ls_cap;  // last trial index the halving loop can reach (max_ls - 1, or the alpha_floor stop)
 };
+
+// ILQR.jl:76-83 break tests after trial m (alpha is then 2^-(m+1)): the floor test first
+// (Parking_ILQR), then the max_ls safety cap.
+__host__ __device__ inline bool floor_stop(const IlqrDev& P, int m) {
+  return P.alpha_floor > 0 && ldexp(1.0, -(m + 1)) <= P.alpha_floor;
+}
 
 struct UPre {  // control-only part of Dynamics (Dynamics.jl:8-12)
   double tdl, beta, cb;
@@ -40,6 +47,11 @@ constexpr bool kFast = false;
 #else
 constexpr bool kFast = true;
 #endif
+// Per kernel (measured, gfx950, configs[2]): the straight-line cores pay off only in the Riccati
+// sweep (355 vs 382 us).  The derivative kernel (405,504 threads, lanes of a wave take the same
+// libm branches) runs the exact routines in 154 us vs 296 us, and the one-thread-per-instance
+// forward trial / roll out (64 waves, latency-bound: fewer instructions win) in 361 vs 690 us.
+constexpr bool kFastDeriv = false, kFastBwd = kFast, kFastFwd = false;
 #if defined(MP_ILQR_NOREDO)
 constexpr bool kRedo = false;
 #else
@@ -50,13 +62,13 @@ __device__ int g_nbad = 0;
 #endif
 template <> struct LM<true> {
 #if !defined(MP_ILQR_BADSTAT)
-  static __device__ __forceinline__ double tan(double x, int& b) { return mpj_tan_fast(x, &b); }
+  static __device__ __forceinline__ double tan(double x, int& b) { return mpj_tan_wide(x, &b); }
   static __device__ __forceinline__ double atan(double x, int&) { return mpj_atan_bl(x); }
   static __device__ __forceinline__ void sincos(double x, double* s, double* c, int& b) { mpj_sincos_wide(x, s, c, &b); }
   static __device__ __forceinline__ double exp(double x, int& b) { return mpj_exp_fast(x, &b); }
   static __device__ __forceinline__ double atan2(double y, double x, int& b) { return mpj_atan2_fast(y, x, &b); }
 #else
-  static __device__ double tan(double x, int& b) { int t = 0; double r = mpj_tan_fast(x, &t); if (t) { b |= 1; if (atomicAdd(&g_nbad, 1) < 8) printf("tan %.17g\n", x); } return r; }
+  static __device__ double tan(double x, int& b) { int t = 0; double r = mpj_tan_wide(x, &t); if (t) { b |= 1; if (atomicAdd(&g_nbad, 1) < 8) printf("tan %.17g\n", x); } return r; }
   static __device__ double atan(double x, int&) { return mpj_atan_bl(x); }
   static __device__ void sincos(double x, double* s, double* c, int& b) { int t = 0; mpj_sincos_wide(x, s, c, &t); if (t) { b |= 2; if (atomicAdd(&g_nbad, 1) < 8) printf("sincos %.17g\n", x); } }
   static __device__ double exp(double x, int& b) { int t = 0; double r = mpj_exp_fast(x, &t); if (t) { b |= 4; if (atomicAdd(&g_nbad, 1) < 8) printf("exp %.17g\n", x); } return r; }
@@ -279,8 +291,8 @@ __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const
   const double u[2] = {us[0], us[1]};
   double* out = D + (size_t)j * ND * B + b;
   int bad = 0;
-  knot_derivs<kFast>(P, s, u, out, (size_t)B, bad);
-  if (kFast && kRedo && __any(bad)) {  // some lane left a straight-line core's range: redo the wave exactly
+  knot_derivs<kFastDeriv>(P, s, u, out, (size_t)B, bad);
+  if (kFastDeriv && kRedo && __any(bad)) {  // some lane left a straight-line core's range: redo the wave exactly
     int d = 0;
     knot_derivs<false>(P, s, u, out, (size_t)B, d);
   }
@@ -473,8 +485,8 @@ __global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, con
   if (__all(!live)) return;
   const int b = b0 < B ? b0 : B - 1;
   int bad = 0;
-  backward_sweep<kFast>(P, B, b, live, X, D, kout, Kout, bad);
-  if (kFast && kRedo && __any(bad)) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
+  backward_sweep<kFastBwd>(P, B, b, live, X, D, kout, Kout, bad);
+  if (kFastBwd && kRedo && __any(bad)) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
     int d = 0;
     backward_sweep<false>(P, B, b, live, X, D, kout, Kout, d);
   }
@@ -553,9 +565,9 @@ __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, cons
   const size_t b = live ? b0 : B - 1;  // all lanes active (ballot-based libm); tail lanes store nothing
   const size_t N = P.N;
   int bad = 0;
-  double J = forward_trial<kFast>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
-                                 alpha[b], Xn + b * N * 4, Un + b * N * 2, live, bad);
-  if (kFast && kRedo && __any(bad)) {  // redo the wave's trials with the exact libm
+  double J = forward_trial<kFastFwd>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
+                                    alpha[b], Xn + b * N * 4, Un + b * N * 2, live, bad);
+  if (kFastFwd && kRedo && __any(bad)) {  // redo the wave's trials with the exact libm
     int d = 0;
     J = forward_trial<false>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha[b],
                              Xn + b * N * 4, Un + b * N * 2, live, d);
@@ -563,47 +575,60 @@ __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, cons
   if (live) Jn[b] = J;
 }
 
-// ILQR.jl:70-88 after the backward sweep: line search, accept, convergence test.
-// state[b]: J (cost at the start of this iteration, i.e. the previous J_new).
+// ILQR.jl:70-88 after the backward sweep: line search, accept, convergence test, with the
+// halving trials evaluated G at a time.  Trial m of the reference loop runs at alpha = 2^-m
+// (repeated halving of 1.0 is exact), so the m-th trial is a pure function of m and the G lanes
+// of an instance evaluate trials rG..rG+G-1 of round r concurrently, each into its own slot
+// (Xs/Us [G][B][N]).  The accepted trial is the first m that would end the sequential loop:
+// J_m < J (written !(J_m >= J), as the loop condition), or a break test (floor_stop, max_ls).
+// Identical results to the sequential search; one round instead of G trials of latency.
+// Jcur[b]: J at the start of this iteration (the previous J_new).
+template <int G>
 __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
-                                                         const double* Kg, double* Xn, double* Un, double* Jcur,
+                                                         const double* Kg, double* Xs, double* Us, double* Jcur,
                                                          int* active, int* iters, int* flags, int* n_active) {
-  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int IPW = 64 / G;  // instances per wave
+  const int lane = threadIdx.x, g = lane % G, sub = lane / G;
+  const int b0 = blockIdx.x * IPW + sub;
   const bool live = b0 < B && active[b0];
   if (__all(!live)) return;
   const size_t b = b0 < B ? b0 : B - 1;
   const size_t N = P.N;
   double* Xb = X + b * N * 4;
   double* Ub = U + b * N * 2;
-  double* Xnb = Xn + b * N * 4;
-  double* Unb = Un + b * N * 2;
+  double* Xg = Xs + ((size_t)g * B + b) * N * 4;
+  double* Ug = Us + ((size_t)g * B + b) * N * 2;
+  const double* kb = k + b * (N - 1) * 2;
+  const double* Kb = Kg + b * (N - 1) * 8;
   const double J = Jcur[b];
   double Jn = J;
-  double alpha = 1.0;
-  int ls = 0;
-  // The halving loop runs wave-uniformly (the libm selects with ballots): a lane whose search
-  // has ended keeps its accepted trial (stores predicated off) until the last lane is done.
-  bool searching = live && Jn >= J;
-  while (__any(searching)) {
-    int bad = 0;
-    double jt = forward_trial<kFast>(P, Xb, Ub, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha, Xnb, Unb, searching, bad);
-    if (kFast && kRedo && __any(bad)) {
+  int mw = -1;  // accepted trial index
+  bool searching = live;
+  for (int r = 0; __any(searching); r++) {
+    const int m = r * G + g;
+    const bool mine = searching && m <= P.ls_cap;
+    double jt = 0.0;
+    if (mine) {
       int d = 0;
-      jt = forward_trial<false>(P, Xb, Ub, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha, Xnb, Unb, searching, d);
+      jt = forward_trial<false>(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, d);
     }
-    if (searching) {  // ILQR.jl:76-83: the break tests run before the loop condition
-      Jn = jt;
-      alpha = alpha / 2;
-      ls++;
-      bool brk = false;
-      if (P.alpha_floor > 0 && alpha <= P.alpha_floor) brk = true;
-      else if (ls >= P.max_ls) { atomicOr(flags + b, 1); brk = true; }
-      searching = !brk && Jn >= J;
+    const bool stop = mine && (!(jt >= J) || m == P.ls_cap);
+    const unsigned long long bal = __ballot(stop);
+    const unsigned long long grp = (bal >> (sub * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1));
+    const int gw = grp ? __builtin_ctzll(grp) : 0;
+    const double jw = __shfl(jt, sub * G + gw);  // every lane takes part in the exchange
+    if (searching && grp) {
+      Jn = jw;
+      mw = r * G + gw;
+      searching = false;
+      if (g == gw) {  // the winning lane copies its own slot (its own writes: program order)
+        for (size_t i = 0; i < N * 4; i++) Xb[i] = Xg[i];
+        for (size_t i = 0; i < N * 2; i++) Ub[i] = Ug[i];
+      }
     }
   }
-  if (!live) return;
-  for (size_t i = 0; i < N * 4; i++) Xb[i] = Xnb[i];
-  for (size_t i = 0; i < N * 2; i++) Ub[i] = Unb[i];
+  if (!live || g != 0) return;
+  if (mw + 1 >= P.max_ls && !floor_stop(P, mw)) atomicOr(flags + b, 1);
   Jcur[b] = Jn;
   const int it = iters[b] + 1;
   iters[b] = it;
@@ -648,8 +673,8 @@ __global__ __launch_bounds__(64) void ilqr_rollout_kernel(IlqrDev P, int B, cons
   const size_t b = live ? b0 : B - 1;  // all lanes active (ballot-based libm)
   const size_t N = P.N;
   int bad = 0;
-  double Jb = rollout_one<kFast>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, bad);
-  if (kFast && kRedo && __any(bad)) {
+  double Jb = rollout_one<kFastFwd>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, bad);
+  if (kFastFwd && kRedo && __any(bad)) {
     int d = 0;
     Jb = rollout_one<false>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, d);
   }
@@ -682,6 +707,12 @@ int make_ilqr(mp_ctx* ctx, const mp_ilqr_params* p, int B, IlqrDev* D) {
   D->tol = p->tol;
   D->max_iter = p->max_iter > 0 ? p->max_iter : 1000;
   D->max_ls = p->max_ls > 0 ? p->max_ls : 200;
+  D->ls_cap = D->max_ls - 1;
+  for (int m = 0; m < D->max_ls - 1; m++)
+    if (floor_stop(*D, m)) {
+      D->ls_cap = m;
+      break;
+    }
   return MP_OK;
 }
 
@@ -818,8 +849,11 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   double* dU = (double*)mp_upload(ctx, WS_IO1, U, 2 * N * B, &st);
   double* dk = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * 2 * (N - 1) * B);
   double* dK = (double*)mp_ws(ctx, WS_IO3, sizeof(double) * 8 * (N - 1) * B);
-  double* dXn = (double*)mp_ws(ctx, WS_IO4, sizeof(double) * 4 * N * B);
-  double* dUn = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 2 * N * B);
+  // trial slots for the G-wide line search: G = 16 (1024 waves at B = 4096) while the slots stay
+  // within 1 GiB of HBM, else 4, else 1 (the sequential loop)
+  const int G = (size_t)16 * B * N * 48 <= ((size_t)1 << 30) ? 16 : (size_t)4 * B * N * 48 <= ((size_t)1 << 30) ? 4 : 1;
+  double* dXn = (double*)mp_ws(ctx, WS_IO4, sizeof(double) * 4 * N * B * G);
+  double* dUn = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 2 * N * B * G);
   double* dJ = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * B);
   int* dint = (int*)mp_ws(ctx, WS_IO7, sizeof(int) * (3 * (size_t)B + 1));
   if (st || !dk || !dK || !dXn || !dUn || !dJ || !dint) return st ? st : MP_ERR_NOMEM;
@@ -836,8 +870,13 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     if ((st = run_backward(ctx, D, B, dX, dU, dact, dk, dK))) return st;
     MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
     mp_time_begin(ctx);
-    hipLaunchKernelGGL(ilqr_search_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit,
-                       dfl, dn);
+    const dim3 gs((unsigned)((B + 64 / G - 1) / (64 / G)));
+    if (G == 16)
+      hipLaunchKernelGGL(ilqr_search_kernel<16>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn);
+    else if (G == 4)
+      hipLaunchKernelGGL(ilqr_search_kernel<4>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn);
+    else
+      hipLaunchKernelGGL(ilqr_search_kernel<1>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn);
     MP_HIP(ctx, hipGetLastError());
     mp_time_end(ctx);
     MP_HIP(ctx, hipMemcpyAsync(hn, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));

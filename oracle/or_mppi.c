@@ -352,6 +352,7 @@ double or_m_exp_bl(double x) { return mpj_exp_bl(x); }
 double or_m_sin_wide(double x) { double s, c; int b = 0; mpj_sincos_wide(x, &s, &c, &b); return b ? mpj_sin(x) : s; }
 double or_m_cos_wide(double x) { double s, c; int b = 0; mpj_sincos_wide(x, &s, &c, &b); return b ? mpj_cos(x) : c; }
 double or_m_tan_bl(double x) { return mpj_tan_bl(x); }
+double or_m_tan_wide(double x) { int b = 0; const double t = mpj_tan_wide(x, &b); return b ? mpj_tan(x) : t; }
 double or_m_atan_tab(double x) {
   static double tab[20];
   static int ready = 0;

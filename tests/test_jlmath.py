@@ -128,3 +128,18 @@ def test_sincos_wide_bitidentical():
         for fw, fe in (("sin_wide", "sin"), ("cos_wide", "cos")):
             a, b = oracle.m(fw, float(x)), oracle.m(fe, float(x))
             assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), (fw, x)
+
+
+def test_tan_wide_bitidentical():
+    """mpj_tan_wide (straight-line rem_pio2 + all k_tan forms, iLQR fast path) == mpj_tan on
+    |x| < 2^20*pi/2, incl. the reflected |x| >= 0.6744 form, iy = -1 and arguments next to k*pi/2."""
+    r = np.random.default_rng(13)
+    near = np.concatenate([k * np.pi / 4 + r.uniform(-3e-7, 3e-7, 200) for k in range(-16, 17)])
+    xs = np.concatenate([r.uniform(-1.2, 1.2, 20000), r.uniform(-10, 10, 20000), r.uniform(-1e6, 1e6, 3000), near,
+                         r.uniform(-1e-8, 1e-8, 300),
+                         [np.nextafter(k * np.pi / 2, d) for k in range(-40, 41) for d in (-np.inf, np.inf)],
+                         np.array([0.0, -0.0, 0.6744, -0.6744, 0.67434, np.pi / 4, -np.pi / 4, 0.81256429475748015,
+                                   -0.86181804974631371, 1.6e6, np.inf, -np.inf, np.nan])])
+    for x in xs:
+        a, b = oracle.m("tan_wide", float(x)), oracle.m("tan", float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), x
