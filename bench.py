@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 BASE = json.load(open(os.path.join(ROOT, "BASELINE.json")))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X fp64 vector (AMD spec)
+VALU_SIMDS, VALU_CLOCK_HZ, FP64_ISSUE_CYCLES = 1024, 2.4e9, 4  # 256 CUs x 4 SIMD-32; wave64 fp64 op = 4 cycles
 
 
 def parse():
@@ -188,6 +189,16 @@ def main():
     if tr is not None:
         out["roofline"]["traffic"] = tr["traffic_bytes"]
         out["roofline"]["traffic_source"] = tr["source"]
+        if tr.get("valu_insts"):
+            # the bound that binds: fp64 VALU issue.  A wave64 fp64 instruction occupies a SIMD-32
+            # for 4 cycles (78.6 TF fp64 vector = 1024 SIMDs x 2.4 GHz x 16 FMA lanes x 2), so the
+            # chip issues at most 1024 * 2.4e9 / 4 = 6.14e11 wave-level fp64 instructions per s.
+            peak = VALU_SIMDS * VALU_CLOCK_HZ / FP64_ISSUE_CYCLES
+            rate = tr["valu_insts"] / (kern_ms * 1e-3)
+            out["roofline"]["valu"] = {
+                "insts_per_launch": tr["valu_insts"], "achieved": rate, "peak": peak, "unit": "wave-insts/s",
+                "frac": rate / peak, "source": tr["source"] + " SQ_INSTS_VALU",
+            }
     if not a.no_single and S != 1:
         e1, k1, ok1, _, _, _ = run(a, 1, ctx, dev, world, rank, a.steps, a.warmup, 12)
         out["single_scene"] = {
@@ -217,7 +228,8 @@ def load_traffic(path, S, K, H):
     e = d.get("mppi_plan_kernel", {})
     if "traffic_bytes" not in e or d.get("config") != {"S": S, "K": K, "H": H}:
         return None
-    return {"traffic_bytes": e["traffic_bytes"], "source": os.path.relpath(path, ROOT)}
+    return {"traffic_bytes": e["traffic_bytes"], "valu_insts": e.get("SQ_INSTS_VALU"),
+            "source": os.path.relpath(path, ROOT)}
 
 
 def _sync_max(x, world, dev):

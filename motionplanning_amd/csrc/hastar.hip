@@ -350,7 +350,8 @@ struct IterArgs {
   const double* walls;   // [B][nw][5]
   const double* sc;      // [n_prim][3]
   const double* pc;      // [n_prim][n_col][3]
-  const int* scene_of;   // active slot -> scene index
+  const int* scene_of;   // active slot -> scene index (nullptr: slot = scene)
+  const int* active;     // per-scene live flag (device-resident search), nullptr = all
   int n_active;
   int do_rs, do_exp;
   // RS_connected outputs (per scene)
@@ -488,7 +489,8 @@ __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   if (item == 0 && !A.do_rs) return;
   if (item > 0 && !A.do_exp) return;
   const bool rs = item == 0;  // block-uniform role: RS_connected, else a 16-neighbour group
-  const int s = A.scene_of[slot];
+  const int s = A.scene_of ? A.scene_of[slot] : slot;
+  if (A.active && !A.active[s]) return;  // scene finished (device-resident search)
   const int tid = threadIdx.x, lane = tid & 63;
   HMARK(1);
   HTIME(0);
@@ -715,90 +717,253 @@ int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
   return MP_OK;
 }
 
-struct HNode {
-  long long parent;  // -1 = nothing
-  double st[3];
-  long long index;
-  double g, h, f;
+// ------------------------------------------------ device-resident search state
+// planHybridAstar! (hybrid_astar_utils.jl:235-296) bookkeeping on the device, one scene per
+// block, all arrays scene-major.  Nodes are numbered in creation order (as Dict insertion in
+// the reference / the oracle); nid is nodes_collection (Encode index -> node id).  The open
+// list is a compact array of (f, seq, id) entries; its order is the reference's: a stable
+// sort by f every iteration (`sort!` + `popfirst!`, :242-244) keeps equal-f nodes in list
+// order, i.e. the key (f, seq) where seq is the node's rank in the list order -- nodes whose
+// f decreased in place get fresh seqs in their previous list order, then the nodes appended
+// by push! in push order (FindNewNode :418-446).  popfirst! = the least (f, seq) key.
+struct HaSearch {
+  int C;                 // Encode cells per scene (ncell + 1: cell 0 holds an out-of-bounds start)
+  int mp;                // max_pops
+  long long* parent;     // [B][C] per node id: parent Encode index (-1: none)
+  double* st;            // [B][C][3]
+  long long* index;      // [B][C]
+  double *g, *h, *f;     // [B][C]
+  long long* seq;        // [B][C]
+  int* pos;              // [B][C] open-list position, -1 = not in the open list
+  int* nid;              // [B][C] cell -> node id, -1 = absent
+  double* of;            // [B][C] open entries: f, seq, node id
+  long long* oseq;
+  int* oid;
+  int* sc_i;             // [8][B] per-scene ints: n_nodes, n_open, loop, cur, active, found, n_states, rs_len
+  long long* ctr;        // [B] seq counter
+  long long* start_index;// [B]
+  long long* pop_seq;    // [B][mp]
+  double* states;        // [B][mp][3] hybrid_astar_states (goal side first)
+  double* node;          // [B][3] popped node state: the next iteration's input
+  int* live;             // [mp + 2] scenes still searching after iteration i
 };
+enum { SI_NNODES = 0, SI_NOPEN, SI_LOOP, SI_CUR, SI_ACTIVE, SI_FOUND, SI_NSTATES, SI_RSLEN, SI_N };
 
-// Fork-join pool for the per-scene host bookkeeping of mp_ha_plan: worker threads wait on a
-// generation counter (a short spin, then yield: the GPU phase between two joins is ~0.1 ms),
-// items are claimed in chunks from an atomic counter, each thread has its own scratch.
-template <class Scratch>
-class WorkPool {
- public:
-  explicit WorkPool(int n) : n_(n), scratch_(n) {
-    for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { loop(t); });
-  }
-  ~WorkPool() {
-    quit_.store(true, std::memory_order_release);
-    gen_.fetch_add(1, std::memory_order_release);
-    for (auto& t : th_) t.join();
-  }
-  template <class F>
-  void run(int count, F&& f, bool each = false) {
-    each_ = each;
-    for (auto& sc : scratch_) sc.term.clear();
-    fn_ = [&f](int i, Scratch& sc) { f(i, sc); };
-    count_ = count;
-    next_.store(0, std::memory_order_relaxed);
-    done_.store(0, std::memory_order_relaxed);
-    gen_.fetch_add(1, std::memory_order_release);
-    work(0);
-    while (done_.load(std::memory_order_acquire) != n_ - 1) __builtin_ia32_pause();
-  }
-  // every thread t (0 = the caller) runs f(t, scratch[t]) once: static partitions with affinity
-  template <class F>
-  void run_each(F&& f) {
-    run(n_, [&f](int t, Scratch& sc) { f(t, sc); }, true);
-  }
-  int size() const { return n_; }
-  std::vector<std::pair<int, int>> terminated() const {
-    std::vector<std::pair<int, int>> all;
-    for (const auto& sc : scratch_) all.insert(all.end(), sc.term.begin(), sc.term.end());
-    return all;
-  }
+// open-list order: a before c (Julia isless on f, then list position)
+__device__ __forceinline__ bool key_before(double af, long long as, double cf, long long cs) {
+  if (mpj_isless(af, cf)) return true;
+  if (mpj_isless(cf, af)) return false;
+  return as < cs;
+}
 
- private:
-  void loop(int t) {
-    unsigned long long seen = 0;
-    for (;;) {
-      unsigned long long g;
-      int spins = 0;
-      while ((g = gen_.load(std::memory_order_acquire)) == seen) {  // brief spin, then yield the core
-        if (++spins < 256) __builtin_ia32_pause();
-        else std::this_thread::yield();
+// popfirst! for scene b (one wave): the least (f, seq) open entry, removed by moving the last
+// entry into its place.  Returns false when the search ends here (open list empty / max_pops).
+__device__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int lane) {
+  const size_t base = (size_t)b * Q.C;
+  if (n_open == 0 || loop >= Q.mp) return false;
+  double bf = __builtin_inf();
+  long long bs = 0x7fffffffffffffffLL;
+  int bp = -1;
+  for (int p = lane; p < n_open; p += 64) {
+    const double fv = Q.of[base + p];
+    const long long sv = Q.oseq[base + p];
+    if (bp < 0 || key_before(fv, sv, bf, bs)) { bf = fv; bs = sv; bp = p; }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const double of_ = __shfl_xor(bf, o);
+    const long long os = __shfl_xor(bs, o);
+    const int op = __shfl_xor(bp, o);
+    if (op >= 0 && (bp < 0 || key_before(of_, os, bf, bs))) { bf = of_; bs = os; bp = op; }
+  }
+  const int id = Q.oid[base + bp];
+  if (lane == 0) {
+    const int last = n_open - 1;
+    if (bp != last) {
+      const int lid = Q.oid[base + last];
+      Q.of[base + bp] = Q.of[base + last];
+      Q.oseq[base + bp] = Q.oseq[base + last];
+      Q.oid[base + bp] = lid;
+      Q.pos[base + lid] = bp;
+    }
+    Q.pos[base + id] = -1;
+    Q.sc_i[SI_NOPEN * B + b] = last;
+    Q.sc_i[SI_LOOP * B + b] = loop + 1;
+    Q.sc_i[SI_CUR * B + b] = id;
+    Q.pop_seq[(size_t)b * Q.mp + loop] = Q.index[base + id];
+  }
+  if (lane < 3) Q.node[3 * b + lane] = Q.st[(base + id) * 3 + lane];
+  return true;
+}
+
+// starting node (setup.jl:112-121) and the first popfirst!; block b = scene b
+__global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B, const double* start) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t base = (size_t)b * Q.C;
+  for (int c = tid; c < Q.C; c += 256) Q.nid[base + c] = -1;
+  const double* s0 = start + 3 * b;
+  if (tid == 0) {
+    const long long si = encode(P, s0);  // 0 when the start is outside stbound
+    Q.parent[base] = -1;
+    for (int r = 0; r < 3; r++) Q.st[base * 3 + r] = s0[r];
+    Q.index[base] = si;
+    Q.g[base] = 0.0; Q.h[base] = 0.0; Q.f[base] = 0.0;
+    Q.seq[base] = 0;
+    Q.pos[base] = 0;
+    Q.of[base] = 0.0; Q.oseq[base] = 0; Q.oid[base] = 0;
+    Q.ctr[b] = 1;
+    Q.start_index[b] = si;
+    Q.sc_i[SI_NNODES * B + b] = 1;
+    Q.sc_i[SI_FOUND * B + b] = 0;
+    Q.sc_i[SI_NSTATES * B + b] = 0;
+    Q.sc_i[SI_RSLEN * B + b] = 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const long long si = Q.start_index[b];
+    if (si >= 0 && si < Q.C) Q.nid[base + si] = 0;
+  }
+  __syncthreads();
+  if (tid < 64) {  // wave 0
+    const bool go = ha_pop(Q, B, b, 1, 0, tid);
+    if (tid == 0) Q.sc_i[SI_ACTIVE * B + b] = go;
+  }
+}
+
+// One search iteration's bookkeeping for scene b (one wave), after ha_iter_kernel wrote the
+// scene's RS_connected result and the 62 neighbours (array mode): termination (:259-271) or
+// FindNewNode's Dict/open-list updates (:418-446), then the next popfirst!.
+__global__ __launch_bounds__(64) void ha_book_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
+  __shared__ long long s_idx[64];
+  __shared__ int s_first[64], s_chg[64];
+  __shared__ double s_of[64];
+  __shared__ long long s_os[64];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (!Q.sc_i[SI_ACTIVE * B + b]) return;
+  const size_t base = (size_t)b * Q.C;
+  const int np = P.n_prim;
+  const int cur = Q.sc_i[SI_CUR * B + b];
+  int n_open = Q.sc_i[SI_NOPEN * B + b];
+  const int loop = Q.sc_i[SI_LOOP * B + b];
+  if (A.rs_ok[b]) {  // RS_connected: path found -> hybrid_astar_states by the parent chain
+    if (lane == 0) {
+      Q.sc_i[SI_FOUND * B + b] = 1;
+      Q.sc_i[SI_ACTIVE * B + b] = 0;
+      Q.sc_i[SI_RSLEN * B + b] = A.rs_len[b];
+      double* so = Q.states + (size_t)b * Q.mp * 3;
+      int c = cur, ns = 0;
+      for (int r = 0; r < 3; r++) so[r] = Q.st[(base + c) * 3 + r];
+      ns++;
+      while (Q.parent[base + c] >= 0 && Q.index[base + c] != Q.start_index[b] && ns < Q.mp) {
+        const long long pc = Q.parent[base + c];
+        c = (pc >= 0 && pc < Q.C) ? Q.nid[base + pc] : -1;
+        if (c < 0) break;
+        for (int r = 0; r < 3; r++) so[3 * ns + r] = Q.st[(base + c) * 3 + r];
+        ns++;
       }
-      seen = g;
-      if (quit_.load(std::memory_order_acquire)) return;
-      work(t);
-      done_.fetch_add(1, std::memory_order_release);
+      Q.sc_i[SI_NSTATES * B + b] = ns;
+    }
+    return;
+  }
+  // ---- FindNewNode (:391-447): neighbour k on lane k; only the first valid occurrence of an
+  // Encode index in this expansion can change anything (every neighbour has the same tentative g)
+  const int k = lane;
+  const long long ix = k < np ? A.idx[(size_t)b * np + k] : 0;
+  const bool valid = k < np && ix != 0 && A.fr[(size_t)b * np + k];
+  s_idx[k] = valid ? ix : 0;
+  __syncthreads();
+  bool first = valid;
+  for (int j = 0; j < k && first; j++) first = s_idx[j] != ix;
+  const double tg = Q.g[base + cur] + P.expand_time;
+  const long long cidx = Q.index[base + cur];
+  double th = 0.0, tf = 0.0;
+  int id = -1;
+  bool chg = false, app = false, isnew = false;
+  double fo = 0.0;
+  long long so_ = 0;
+  if (first) {
+    const double hk = A.h[(size_t)b * np + k];
+    th = __builtin_fmax(hk, 0.0);
+    if (hk != hk) th = hk;
+    tf = tg + th;
+    const int hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
+    if (hit >= 0) {
+      id = hit;
+      if (tg < Q.g[base + id]) {
+        if (Q.pos[base + id] >= 0) {
+          chg = true;
+          fo = Q.f[base + id];
+          so_ = Q.seq[base + id];
+        } else {
+          app = true;
+        }
+      }
+    } else {
+      isnew = true;
+      app = true;
     }
   }
-  void work(int t) {
-    if (count_ == n_ && each_) {  // run_each: item t on thread t
-      fn_(t, scratch_[t]);
-      return;
+  const unsigned long long m_new = __ballot(isnew), m_chg = __ballot(chg), m_app = __ballot(app);
+  const unsigned long long below = (1ull << k) - 1;  // lanes < k
+  const int n_new = __popcll(m_new), n_chg = __popcll(m_chg), n_app = __popcll(m_app);
+  const int nn0 = Q.sc_i[SI_NNODES * B + b];
+  if (isnew) id = nn0 + __popcll(m_new & below);
+  s_chg[k] = chg;
+  s_of[k] = fo;
+  s_os[k] = so_;
+  __syncthreads();
+  const long long ctr = Q.ctr[b];
+  long long nseq = 0;
+  if (chg) {  // in-place updates keep their previous list order
+    int r = 0;
+    for (int j = 0; j < 64; j++)
+      if (s_chg[j] && key_before(s_of[j], s_os[j], fo, so_)) r++;
+    nseq = ctr + r;
+  } else if (app) {  // then push! in neighbour order
+    nseq = ctr + n_chg + __popcll(m_app & below);
+  }
+  if (chg || app) {
+    const size_t q = base + id;
+    if (isnew) {
+      Q.st[q * 3] = A.nb[((size_t)b * np + k) * 3];
+      Q.st[q * 3 + 1] = A.nb[((size_t)b * np + k) * 3 + 1];
+      Q.st[q * 3 + 2] = A.nb[((size_t)b * np + k) * 3 + 2];
+      Q.index[q] = ix;
+      if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
     }
-    constexpr int CH = 4;
-    for (;;) {
-      const int i = next_.fetch_add(CH, std::memory_order_relaxed);
-      if (i >= count_) break;
-      const int e = std::min(i + CH, count_);
-      for (int j = i; j < e; j++) fn_(j, scratch_[t]);
+    Q.g[q] = tg;
+    Q.h[q] = th;
+    Q.f[q] = tf;
+    Q.parent[q] = cidx;
+    Q.seq[q] = nseq;
+    if (chg) {
+      const int p = Q.pos[q];
+      Q.of[base + p] = tf;
+      Q.oseq[base + p] = nseq;
+    } else {
+      const int p = n_open + __popcll(m_app & below);
+      Q.of[base + p] = tf;
+      Q.oseq[base + p] = nseq;
+      Q.oid[base + p] = id;
+      Q.pos[q] = p;
     }
   }
-  int n_;
-  std::vector<Scratch> scratch_;
-  std::vector<std::thread> th_;
-  std::function<void(int, Scratch&)> fn_;
-  int count_ = 0;
-  bool each_ = false;
-  std::atomic<int> next_{0}, done_{0};
-  std::atomic<unsigned long long> gen_{0};
-  std::atomic<bool> quit_{false};
-};
+  n_open += n_app;
+  if (lane == 0) {
+    Q.sc_i[SI_NNODES * B + b] = nn0 + n_new;
+    Q.ctr[b] = ctr + n_chg + n_app;
+  }
+  __syncthreads();
+  // ---- next popfirst!
+  const bool go = ha_pop(Q, B, b, n_open, loop, lane);
+  if (lane == 0) {
+    if (go) atomicAdd(Q.live + it, 1);
+    else {
+      Q.sc_i[SI_ACTIVE * B + b] = 0;
+      Q.sc_i[SI_NOPEN * B + b] = n_open;
+    }
+  }
+}
 
 }  // namespace
 
@@ -959,274 +1124,143 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_CHECK(ctx, B >= 1 && start && goal && (walls || p->n_walls == 0) && found && pops && n_nodes && pop_seq &&
                n_states && states_out && rs_len && rs_path, "bad arguments");
   MP_CHECK(ctx, p->max_pops >= 1, "max_pops must be >= 1");
+  MP_CHECK(ctx, p->n_prim <= 64, "n_prim (%d) must be <= 64 (one neighbour per lane of the bookkeeping wave)",
+           p->n_prim);
   MP_HIP(ctx, hipSetDevice(ctx->device));
   const int np = p->n_prim, mp = p->max_pops;
-  IterArgs A{};
-  A.goal = mp_upload(ctx, WS_HA0, goal, 3 * (size_t)B, &st);
-  A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
-  // one packed input region (nodes, scene map) and per-slot output records, mirrored in
-  // pinned host memory: one H2D and one D2H copy (n_active records) per search iteration
-  const size_t in_bytes = sizeof(double) * 3 * B + sizeof(int) * B;
-  const int rb = (int)((sizeof(double) * 5 * np + sizeof(int) + 1 + np + 15) & ~(size_t)15);
-  const size_t out_bytes = (size_t)B * rb;
-  char* din = (char*)mp_ws(ctx, WS_IO0, in_bytes);
-  char* dout = (char*)mp_ws(ctx, WS_IO1, out_bytes);
-  A.rs_path = (double*)mp_ws(ctx, WS_IO3, sizeof(double) * B * MAXPATH * 3);
-  if (st || !din || !dout || !A.rs_path) return st ? st : MP_ERR_NOMEM;
-  double* dnode = (double*)din;
-  int* dso = (int*)(din + sizeof(double) * 3 * B);
-  A.rec = dout;
-  A.rb = rb;
-  A.node = dnode;
-  A.scene_of = dso;
-  A.sc = ctx->ha_states_candi;
-  A.pc = ctx->ha_paths_candi;
-  A.do_rs = 1;
-  A.do_exp = 1;
-  // pinned staging with the same packing
-  char* pin = (char*)mp_pinned(ctx, in_bytes + out_bytes + 64);
-  if (!pin) return mp_fail(ctx, MP_ERR_NOMEM, "pinned staging allocation failed");
-  double* h_node = (double*)pin;
-  int* h_so = (int*)(pin + sizeof(double) * 3 * B);
-  char* hout = pin + ((in_bytes + 63) & ~(size_t)63);
-
-  // per-scene search state (planHybridAstar!, hybrid_astar_utils.jl:235-296).
-  // The reference re-sorts its open list every iteration with a stable sort on f
-  // (`sort!` + `popfirst!`, :242-244) and scans it linearly for membership (InOpen,
-  // :298-305).  The same order is kept here in a binary heap keyed by (f, seq): f by
-  // Julia `isless`, seq = the node's rank in the list order that the stable sort
-  // preserves among equal f — nodes already in the list keep their seq; at the end of an
-  // iteration the nodes whose f decreased in place get fresh seqs in their previous list
-  // order, then the nodes appended by push! (in push order).  Membership is a flag.
-  struct OpenKey {
-    double f;
-    long long seq;
-    int id;
-  };
-  struct After {  // priority_queue comparator: true if a comes after b
-    bool operator()(const OpenKey& a, const OpenKey& c) const {
-      if (mpj_isless(a.f, c.f)) return false;
-      if (mpj_isless(c.f, a.f)) return true;
-      return a.seq > c.seq;
-    }
-  };
-  struct Scene {
-    std::vector<HNode> nd;
-    std::vector<long long> seq;       // current key seq per node
-    std::vector<unsigned char> in_open;
-    std::vector<int> dict;  // nodes_collection: Encode index (1..ncell) -> node id, -1 = absent
-    int get(long long i) const { return (i >= 0 && i < (long long)dict.size()) ? dict[i] : -1; }
-    std::priority_queue<OpenKey, std::vector<OpenKey>, After> open;
-    long long ctr = 0;
-    size_t n_open = 0;
-  };
-  std::vector<Scene> sc(B);
   // Encode range: 1 .. xnum*ynum*pnum (hybrid_astar_utils.jl:316-350)
   const long long ncell = (long long)(mpj_round((p->stbound[1] - p->stbound[0]) / p->res[0]) + 1) *
                           (long long)(mpj_round((p->stbound[3] - p->stbound[2]) / p->res[1]) + 1) *
                           (long long)(mpj_round((p->stbound[5] - p->stbound[4]) / p->res[2]) + 1);
-  MP_CHECK(ctx, ncell > 0 && ncell < (1LL << 31), "state lattice too large (%lld cells)", ncell);
-  std::vector<int> done(B, 0), cur(B, -1), loop(B, 0), popped(B, 0), slot_of(B, -1);
-  std::vector<long long> start_index(B);
+  MP_CHECK(ctx, ncell > 0 && ncell < (1LL << 26), "state lattice too large (%lld cells)", ncell);
+  const size_t C = (size_t)ncell + 1, nB = (size_t)B;
+  // search state: node arrays and open list indexed [scene][node / cell]
+  const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4;
+  char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 16) + nB * mp * 32 + nB * 24 +
+                                           sizeof(int) * (mp + 2) + 256 * 16);
+  if (!ws) return MP_ERR_NOMEM;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
+  HaSearch Q;
+  Q.C = (int)C;
+  Q.mp = mp;
+  Q.parent = (long long*)take(nB * C * 8);
+  Q.st = (double*)take(nB * C * 24);
+  Q.index = (long long*)take(nB * C * 8);
+  Q.g = (double*)take(nB * C * 8);
+  Q.h = (double*)take(nB * C * 8);
+  Q.f = (double*)take(nB * C * 8);
+  Q.seq = (long long*)take(nB * C * 8);
+  Q.pos = (int*)take(nB * C * 4);
+  Q.nid = (int*)take(nB * C * 4);
+  Q.of = (double*)take(nB * C * 8);
+  Q.oseq = (long long*)take(nB * C * 8);
+  Q.oid = (int*)take(nB * C * 4);
+  Q.sc_i = (int*)take(nB * SI_N * 4);
+  Q.ctr = (long long*)take(nB * 8);
+  Q.start_index = (long long*)take(nB * 8);
+  Q.pop_seq = (long long*)take(nB * mp * 8);
+  Q.states = (double*)take(nB * mp * 24);
+  Q.node = (double*)take(nB * 24);
+  Q.live = (int*)take(sizeof(int) * (mp + 2));
+  IterArgs A{};
+  A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
+  A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
+  const double* dstart = mp_upload(ctx, WS_IO0, start, 3 * nB, &st);
+  A.h = (double*)mp_ws(ctx, WS_IO1, sizeof(double) * nB * np);
+  A.nb = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * nB * np * 3);
+  A.idx = (long long*)mp_ws(ctx, WS_IO3, sizeof(long long) * nB * np);
+  A.fr = (unsigned char*)mp_ws(ctx, WS_IO4, nB * np);
+  A.rs_ok = (unsigned char*)mp_ws(ctx, WS_IO5, nB);
+  A.rs_len = (int*)mp_ws(ctx, WS_IO6, sizeof(int) * nB);
+  A.rs_path = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * nB * MAXPATH * 3);
+  if (st || !A.h || !A.nb || !A.idx || !A.fr || !A.rs_ok || !A.rs_len || !A.rs_path) return st ? st : MP_ERR_NOMEM;
+  A.node = Q.node;
+  A.scene_of = nullptr;  // slot = scene
+  A.active = Q.sc_i + SI_ACTIVE * B;
+  A.sc = ctx->ha_states_candi;
+  A.pc = ctx->ha_paths_candi;
+  A.do_rs = 1;
+  A.do_exp = 1;
+  A.n_active = B;
+  MP_HIP(ctx, hipMemsetAsync(Q.pop_seq, 0xff, nB * mp * 8, ctx->stream));  // -1 past each scene's pops
+  MP_HIP(ctx, hipMemsetAsync(Q.live, 0, sizeof(int) * (mp + 2), ctx->stream));
+  hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
+  MP_HIP(ctx, hipGetLastError());
+  // The whole search loop is enqueued without host round trips: iteration i = ha_iter_kernel
+  // (RS_connected + 62 neighbours of every live scene) then ha_book_kernel (bookkeeping + the
+  // next pop).  live[i] (scenes still searching after iteration i) is copied back once per
+  // chunk of CH iterations; the host stays at most two chunks ahead of the device and stops
+  // enqueueing when a copied count is 0 (at most every scene's max_pops iterations).
+  constexpr int CH = 16, NCK = 4;
+  int* hl = (int*)mp_pinned(ctx, sizeof(int) * NCK);
+  if (!hl) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
+  hipEvent_t ev[NCK];
+  for (int i = 0; i < NCK; i++) MP_HIP(ctx, hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  auto cleanup = [&] { for (int i = 0; i < NCK; i++) hipEventDestroy(ev[i]); };
+  const int per = 1 + (np + NBG - 1) / NBG;
+  int chunk = 0, checked = 0;
+  bool finished = false;
+  for (int it = 1; it <= mp && !finished; it++) {
+    mp_time_begin(ctx);
+    hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(B * per)), dim3(HT), 0, ctx->stream, D, A);
+    mp_time_end(ctx);
+    hipLaunchKernelGGL(ha_book_kernel, dim3(B), dim3(64), 0, ctx->stream, D, Q, A, B, it);
+    if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
+    if (it % CH == 0 || it == mp) {
+      const int slot = chunk % NCK;
+      if (hipMemcpyAsync(hl + slot, Q.live + it, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+          hipEventRecord(ev[slot], ctx->stream) != hipSuccess) {
+        cleanup();
+        return mp_fail(ctx, MP_ERR_HIP, "live-count copy failed");
+      }
+      chunk++;
+      // poll finished chunks without blocking; block only when two chunks ahead
+      while (checked < chunk) {
+        const int cs = checked % NCK;
+        const bool must = chunk - checked > 2;
+        const hipError_t q = must ? hipEventSynchronize(ev[cs]) : hipEventQuery(ev[cs]);
+        if (q == hipErrorNotReady) break;
+        if (q != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "event wait failed"); }
+        if (hl[cs] == 0) { finished = true; break; }
+        checked++;
+      }
+    }
+  }
+  // outputs: per-scene counters, then the used prefix of pop_seq / states / RS paths
+  std::vector<int> si(SI_N * nB);
+  if ((st = mp_download(ctx, si.data(), (const int*)Q.sc_i, SI_N * nB))) { cleanup(); return st; }
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "search failed"); }
+  cleanup();
+  int max_loop = 0, max_ns = 0, max_rs = 0;
   for (int b = 0; b < B; b++) {
-    found[b] = 0;
-    n_states[b] = 0;
-    rs_len[b] = 0;
-    for (int i = 0; i < mp; i++) pop_seq[(size_t)b * mp + i] = -1;
-    // starting node (setup.jl:112-121): Encode of the regulated start
-    const double* s0 = start + 3 * b;
-    const double* sbd = p->stbound;
-    double x = std::fmax(std::fmin(s0[0], sbd[1]), sbd[0]), y = std::fmax(std::fmin(s0[1], sbd[3]), sbd[2]);
-    double psi = std::fmax(std::fmin(mpj_modpi(s0[2]), sbd[5]), sbd[4]);
-    const double xid = mpj_round((x - sbd[0]) / p->res[0]) + 1, yid = mpj_round((y - sbd[2]) / p->res[1]) + 1;
-    const double pid = mpj_round((psi - sbd[4]) / p->res[2]) + 1;
-    const double ynum = mpj_round((sbd[3] - sbd[2]) / p->res[1]) + 1, pnum = mpj_round((sbd[5] - sbd[4]) / p->res[2]) + 1;
-    long long si = (long long)((xid - 1) * ynum * pnum + (yid - 1) * pnum + pid);
-    if (s0[0] < sbd[0] || s0[0] > sbd[1] || s0[1] < sbd[2] || s0[1] > sbd[3]) si = 0;
-    start_index[b] = si;
-    Scene& S = sc[b];
-    S.nd.push_back(HNode{-1, {s0[0], s0[1], s0[2]}, si, 0, 0, 0});
-    S.seq.push_back(S.ctr);
-    S.in_open.push_back(1);
-    S.dict.assign((size_t)ncell + 1, -1);
-    if (si >= 0 && si <= ncell) S.dict[si] = 0;
-    S.open.push(OpenKey{0.0, S.ctr++, 0});
-    S.n_open = 1;
+    found[b] = si[SI_FOUND * B + b];
+    pops[b] = si[SI_LOOP * B + b];
+    n_nodes[b] = si[SI_NNODES * B + b];
+    n_states[b] = si[SI_NSTATES * B + b];
+    rs_len[b] = found[b] ? si[SI_RSLEN * B + b] : 0;
+    max_loop = std::max(max_loop, pops[b]);
+    max_ns = std::max(max_ns, n_states[b]);
+    max_rs = std::max(max_rs, rs_len[b]);
   }
-  std::vector<int> act;
-  std::vector<std::pair<OpenKey, int>> changed;  // (pre-iteration key, id) of in-place f updates
-  std::vector<int> appended;
-  struct Scratch {
-    std::vector<std::pair<OpenKey, int>> changed;  // (pre-iteration key, id) of in-place f updates
-    std::vector<int> appended;
-    std::vector<std::pair<int, int>> term;         // (scene, slot) that terminated this iteration
-  };
-  const char* hout_c = hout;
-  auto book = [&](int slot, Scratch& W) {
-    const int b = act[slot];
-    const char* rq = hout_c + (size_t)slot * rb;  // this slot's record (see IterArgs::rec)
-    const double* h_h = (const double*)rq;
-    const double* h_nb = h_h + np;
-    const long long* h_idx = (const long long*)(h_nb + 3 * np);
-    const int h_len = *(const int*)(h_idx + np);
-    const unsigned char h_ok = *(const unsigned char*)((const int*)(h_idx + np) + 1);
-    const unsigned char* h_fr = (const unsigned char*)((const int*)(h_idx + np) + 1) + 1;
-    Scene& S = sc[b];
-    std::vector<HNode>& nd = S.nd;
-    if (h_ok) {  // termination (:259-271)
-      found[b] = 1;
-      done[b] = 1;
-      rs_len[b] = h_len;
-      W.term.push_back({b, slot});
-      int c = cur[b], ns = 0;
-      double* so = states_out + (size_t)b * mp * 3;
-      for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
-      ns++;
-      while (nd[c].parent >= 0 && nd[c].index != start_index[b] && ns < mp) {
-        c = S.get(nd[c].parent);
-        if (c < 0) break;
-        for (int r = 0; r < 3; r++) so[3 * ns + r] = nd[c].st[r];
-        ns++;
-      }
-      n_states[b] = ns;
-      return;
-    }
-    // FindNewNode bookkeeping (:418-446), neighbours in order
-    auto& changed = W.changed;
-    auto& appended = W.appended;
-    changed.clear();
-    appended.clear();
-    const HNode cn = nd[cur[b]];
-    for (int k = 0; k < np; k++) {
-      if (h_idx[k] == 0 || !h_fr[k]) continue;
-      const double tg = cn.g + p->expand_time;
-      double th = std::fmax(h_h[k], 0.0);
-      if (h_h[k] != h_h[k]) th = h_h[k];
-      const double tf = tg + th;
-      const int hit = S.get(h_idx[k]);
-      int id;
-      bool upd = false;
-      if (hit >= 0) {
-        id = hit;
-        if (tg < nd[id].g) {
-          if (S.in_open[id] == 1) {  // first in-place update this iteration: remember the list position
-            changed.push_back({OpenKey{nd[id].f, S.seq[id], id}, id});
-            S.in_open[id] = 3;
-          }
-          nd[id].g = tg; nd[id].h = th; nd[id].f = tf; nd[id].parent = cn.index;
-          upd = true;
-        }
-      } else {
-        id = (int)nd.size();
-        nd.push_back(HNode{cn.index, {h_nb[3 * k], h_nb[3 * k + 1], h_nb[3 * k + 2]}, h_idx[k], tg, th, tf});
-        S.seq.push_back(-1);
-        S.in_open.push_back(0);
-        if (h_idx[k] > 0 && h_idx[k] <= ncell) S.dict[h_idx[k]] = id;
-        upd = true;
-      }
-      if (upd && !S.in_open[id]) {  // !InOpen -> push! (appended at the list end)
-        S.in_open[id] = 2;            // 2: appended this iteration
-        appended.push_back(id);
-        S.n_open++;
-      }
-    }
-    // re-key: in-place updates in their previous list order (first update's old key), then appends
-    std::sort(changed.begin(), changed.end(), [](const std::pair<OpenKey, int>& u, const std::pair<OpenKey, int>& v) {
-      return After()(v.first, u.first);
-    });
-    for (const auto& ck : changed) {
-      const int id = ck.second;
-      S.in_open[id] = 1;
-      S.seq[id] = S.ctr++;
-      S.open.push(OpenKey{nd[id].f, S.seq[id], id});
-    }
-    for (int id : appended) {
-      S.in_open[id] = 1;
-      S.seq[id] = S.ctr++;
-      S.open.push(OpenKey{nd[id].f, S.seq[id], id});
-    }
-  };
-  // a small spin-synchronised pool for the per-scene bookkeeping (scenes are independent)
-  const int hw = (int)std::thread::hardware_concurrency();
-  const char* ev = getenv("MPGPU_HA_THREADS");
-  int nthreads = ev ? atoi(ev) : std::min(16, std::max(1, hw));
-  nthreads = std::max(1, std::min(nthreads, B / 16 > 0 ? B / 16 : 1));
-  WorkPool<Scratch> pool(nthreads);
-  static const bool prof = getenv("MPGPU_HA_PROFILE") != nullptr;  // host/device time split
-  double t_pop = 0, t_gpu = 0, t_book = 0;
-  long long n_iter = 0;
-  auto now = [] { return std::chrono::steady_clock::now(); };
-  // popfirst! of scene b (:242-244): the least live (f, seq) key; scene b always on pool thread
-  // b % T (with its bookkeeping), so its heap stays in that core's cache
-  auto pop = [&](int b) {
-    popped[b] = 0;
-    if (done[b]) return;
-    Scene& S = sc[b];
-    if (S.n_open == 0 || loop[b] >= mp) { done[b] = 1; return; }
-    loop[b]++;
-    for (;;) {
-      const OpenKey k = S.open.top();
-      S.open.pop();
-      if (S.in_open[k.id] && S.seq[k.id] == k.seq) { cur[b] = k.id; break; }
-    }
-    S.in_open[cur[b]] = 0;
-    S.n_open--;
-    pop_seq[(size_t)b * mp + loop[b] - 1] = S.nd[cur[b]].index;
-    for (int r = 0; r < 3; r++) h_node[3 * b + r] = S.nd[cur[b]].st[r];
-    popped[b] = 1;
-  };
-  bool first = true;
-  auto t_a = now();
-  for (;;) {
-    if (prof) t_a = now();
-    if (first) {  // the first popfirst! (later ones run with the previous iteration's bookkeeping)
-      pool.run_each([&](int t, Scratch&) {
-        for (int b = t; b < B; b += nthreads) pop(b);
-      });
-      first = false;
-    }
-    act.clear();
-    for (int b = 0; b < B; b++)
-      if (popped[b]) {
-        slot_of[b] = (int)act.size();
-        h_so[(int)act.size()] = b;
-        act.push_back(b);
-      }
-    if (act.empty()) break;
-    const int na = (int)act.size();
-    auto t_b = now();
-    MP_HIP(ctx, hipMemcpyAsync(din, h_node, in_bytes, hipMemcpyHostToDevice, ctx->stream));
-    A.n_active = na;
-    if ((st = launch_iter(ctx, D, A))) return st;
-    MP_HIP(ctx, hipMemcpyAsync(hout, dout, (size_t)na * rb, hipMemcpyDeviceToHost, ctx->stream));
-    MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    auto t_c = now();
-    // bookkeeping per active scene (independent scenes: spread over the worker pool)
-    pool.run_each([&](int t, Scratch& W) {  // bookkeeping, then the next iteration's pop
-      for (int b = t; b < B; b += nthreads) {
-        if (popped[b]) book(slot_of[b], W);
-        pop(b);
-      }
-    });
-    for (const auto& tm : pool.terminated()) {  // RS path of scenes that terminated
-      MP_HIP(ctx, hipMemcpy(rs_path + (size_t)tm.first * MAXPATH * 3, A.rs_path + (size_t)tm.second * MAXPATH * 3,
-                            sizeof(double) * 3 * rs_len[tm.first], hipMemcpyDeviceToHost));
-    }
-    if (prof) {
-      const auto t_d = now();
-      t_pop += std::chrono::duration<double>(t_b - t_a).count();
-      t_gpu += std::chrono::duration<double>(t_c - t_b).count();
-      t_book += std::chrono::duration<double>(t_d - t_c).count();
-      n_iter++;
-    }
+  for (size_t i = 0; i < nB * mp; i++) pop_seq[i] = -1;
+  if (max_loop > 0)
+    MP_HIP(ctx, hipMemcpy2DAsync(pop_seq, sizeof(int64_t) * mp, Q.pop_seq, sizeof(long long) * mp,
+                                 sizeof(long long) * max_loop, nB, hipMemcpyDeviceToHost, ctx->stream));
+  if (max_ns > 0)
+    MP_HIP(ctx, hipMemcpy2DAsync(states_out, sizeof(double) * 3 * mp, Q.states, sizeof(double) * 3 * mp,
+                                 sizeof(double) * 3 * max_ns, nB, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<double> rsb;
+  if (max_rs > 0) {
+    rsb.resize(nB * max_rs * 3);
+    MP_HIP(ctx, hipMemcpy2DAsync(rsb.data(), sizeof(double) * 3 * max_rs, A.rs_path, sizeof(double) * 3 * MAXPATH,
+                                 sizeof(double) * 3 * max_rs, nB, hipMemcpyDeviceToHost, ctx->stream));
   }
-  if (prof)
-    fprintf(stderr, "[mp_ha_plan] B=%d iterations %lld: host pop %.1f ms, launch+kernel+copies %.1f ms, host bookkeeping %.1f ms\n",
-            B, n_iter, t_pop * 1e3, t_gpu * 1e3, t_book * 1e3);
-  for (int b = 0; b < B; b++) {
-    pops[b] = loop[b];
-    n_nodes[b] = (int)sc[b].nd.size();
-  }
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (int b = 0; b < B; b++)
+    if (found[b])
+      std::copy(rsb.begin() + (size_t)b * max_rs * 3, rsb.begin() + ((size_t)b * max_rs + rs_len[b]) * 3,
+                rs_path + (size_t)b * MAXPATH * 3);
   return MP_OK;
 }
 
