@@ -352,6 +352,7 @@ struct IterArgs {
   const double* pc;      // [n_prim][n_col][3]
   const int* scene_of;   // active slot -> scene index (nullptr: slot = scene)
   const int* active;     // per-scene live flag (device-resident search), nullptr = all
+  const double* wtab;    // [B][nw][34] wall corners (10) + SAT tables (24), nullptr = compute
   int n_active;
   int do_rs, do_exp;
   // RS_connected outputs (per scene)
@@ -410,7 +411,9 @@ constexpr int HW = HT / 64;
 // its lanes' candidates (lane&3 = variant of the state in `s`), the per-wave winners are
 // combined in LDS in word order with the same total order (rs_before).  Every wave returns
 // the block-wide winner for its lanes; *best_id is the winning candidate id.
-__device__ __forceinline__ double rs_best_split(const double* s, int tid, int* best_id, double* sh_c, int* sh_i) {
+template <bool CMD>
+__device__ __forceinline__ double rs_best_split(const double* s, int tid, int* best_id, double* sh_c, int* sh_i,
+                                                double* cmd_out = nullptr) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, var = lane & 3;
   double q[3];
   rs_variant(s, var, q);
@@ -418,13 +421,19 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   HTIME(12);
   double bc = __builtin_inf();
   int bi = 1 << 20;
+  Cmd cb;  // CMD: the commands of this lane's best word (its variant, this wave's words)
 #pragma unroll 1
   for (int w = 3 * wave + 1; w <= 3 * wave + 3; w++) {
     Cmd c;
     const double cost = rs_word(w, R, &c);
     const int id = 4 * (w - 1) + var;
-    if (rs_before(cost, id, bc, bi)) { bc = cost; bi = id; }
+    if (rs_before(cost, id, bc, bi)) {
+      bc = cost;
+      bi = id;
+      if (CMD) cb = c;
+    }
   }
+  int own = bi;  // this lane's own best (before the lane exchange)
 #pragma unroll
   for (int o = 2; o >= 1; o >>= 1) {
     const double ov = __shfl_xor(bc, o);
@@ -443,39 +452,33 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
     if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; }
   }
   *best_id = ix;
-  return v;
-}
-
-// the winner's commands (re-evaluated, wave-uniform) with allpath's gear/steer flips
-__device__ __forceinline__ void rs_commands(const double* s, int bi, double* cm) {
-  const int wv = __builtin_amdgcn_readfirstlane(bi & 3);
-  bi = __builtin_amdgcn_readfirstlane(bi);
-  double qw[3];
-  rs_variant(s, wv, qw);
-  Cmd c;
-  const double cost = rs_word(bi / 4 + 1, rs_pre(qw), &c);
-  const int n = cost < __builtin_inf() ? c.n : 0;
+  if (CMD && own == ix && tid == 64 * ((ix / 4) / 3) + (ix & 3)) {
+    // the lane that evaluated the winning candidate stores its commands with allpath's
+    // gear/steer flips (timeflip: gear, reflect: steer, reverse: both), as rs_commands does
+    const int n = v < __builtin_inf() ? cb.n : 0;
 #pragma unroll
-  for (int r = 0; r < 5; r++) {
-    double ge = 0.0, st = 0.0, tr = 0.0;
-    if (r < n) {
-      tr = c.tr[r];
-      ge = c.ge[r];
-      st = c.st[r];
-      if (wv == 1 || wv == 3) ge = -1 * ge;
-      if (wv == 2 || wv == 3) st = -1 * st;
+    for (int r = 0; r < 5; r++) {
+      double ge = 0.0, st = 0.0, tr = 0.0;
+      if (r < n) {
+        tr = cb.tr[r];
+        ge = cb.ge[r];
+        st = cb.st[r];
+        if (var == 1 || var == 3) ge = -1 * ge;
+        if (var == 2 || var == 3) st = -1 * st;
+      }
+      cmd_out[r * 3 + 0] = tr;
+      cmd_out[r * 3 + 1] = ge;
+      cmd_out[r * 3 + 2] = st;
     }
-    cm[r * 3 + 0] = tr;
-    cm[r * 3 + 1] = ge;
-    cm[r * 3 + 2] = st;
   }
+  return v;
 }
 
 __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   __shared__ double wp[MAXW * 10];
   __shared__ double wpre[MAXW * 24];
   __shared__ double cmd[15];
-  __shared__ double psi_s[101], ix_s[101], iy_s[101];
+  __shared__ double psi_s[MAXPATH], ix_s[MAXPATH], iy_s[MAXPATH];
   __shared__ double path_s[MAXPATH * 3];
   __shared__ double red_c[HT];
   __shared__ int red_i[HT];
@@ -499,11 +502,21 @@ __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   const double* goal = A.goal + 3 * s;
   const OutRef R = out_ref(A, s, slot, P.n_prim);
   const int k0 = rs ? 0 : (item - 1) * NBG, nk = rs ? 0 : min(NBG, P.n_prim - k0);
-  // wall corners (Block2Pts) and their SAT tables in LDS
-  for (int i = tid; i < nw; i += HT) {
-    const double* wl = A.walls + ((size_t)s * nw + i) * 5;
-    rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], wp + 10 * i);
-    sat_base_pre(wp + 10 * i, wpre + 24 * i);
+  // wall corners (Block2Pts) and their SAT tables in LDS: precomputed once per plan
+  // (ha_wall_kernel) or evaluated here
+  if (A.wtab) {
+    for (int i = tid; i < nw * 34; i += HT) {
+      const double v = A.wtab[(size_t)s * nw * 34 + i];
+      const int w = i / 34, e = i - 34 * w;
+      if (e < 10) wp[10 * w + e] = v;
+      else wpre[24 * w + e - 10] = v;
+    }
+  } else {
+    for (int i = tid; i < nw; i += HT) {
+      const double* wl = A.walls + ((size_t)s * nw + i) * 5;
+      rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], wp + 10 * i);
+      sat_base_pre(wp + 10 * i, wpre + 24 * i);
+    }
   }
   if (tid < NBG) g_free[tid] = 1;
   if (tid < nk) {  // transform + regulate_states + Encode of the group's neighbours (:396-405)
@@ -532,69 +545,69 @@ __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   else change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
   HTIME(2);
   int best;
-  const double cb = rs_best_split(ns, tid, &best, red_c, red_i);
+  const double cb = rs ? rs_best_split<true>(ns, tid, &best, red_c, red_i, cmd)
+                       : rs_best_split<false>(ns, tid, &best, red_c, red_i);
   HTIME(3);
   int npose;
   if (rs) {
-    // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment
-    {  // every thread evaluates the winner (no divergent region); thread 0 stores it
-      double cm[15];
-      rs_commands(ns, best, cm);
-      if (tid == 0)
-        for (int i = 0; i < 15; i++) cmd[i] = cm[i];
-    }
-    __syncthreads();
+    // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment, all segments
+    // at once -- the heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt over every step (one lane),
+    // the per-step increments (all lanes), then the x and y running sums (one lane each, two
+    // waves): the same operations in the same order as segment by segment
+    __syncthreads();  // cmd (written by the winning lane) visible
     int nseg = 0;
     for (int i = 0; i < 5; i++) {
       if (cmd[i * 3 + 1] == 0) break;
       nseg++;
     }
-    double sx = node[0], sy = node[1], sp = node[2];
-    if (tid == 0) { path_s[0] = sx; path_s[1] = sy; path_s[2] = sp; }
-    for (int seg = 0; seg < nseg; seg++) {
-      const double dt = __builtin_fabs(cmd[seg * 3]) / 100;
-      const double v = cmd[seg * 3 + 1], st = cmd[seg * 3 + 2];
-      if (tid == 0) {  // heading recurrence ψ_{k+1} = ψ_k + (st*v)*dt (adds only)
-        psi_s[0] = sp;
-        double q = sp;
+    const int nst = 100 * nseg;
+    if (tid == 0) {
+      double q = node[2];
+      psi_s[0] = q;
+      for (int seg = 0; seg < nseg; seg++) {
+        const double dt = __builtin_fabs(cmd[seg * 3]) / 100;
+        const double c = (cmd[seg * 3 + 2] * cmd[seg * 3 + 1]) * dt;
         for (int k = 0; k < 100; k++) {
-          q = q + (st * v) * dt;
-          psi_s[k + 1] = q;
+          q = q + c;
+          psi_s[seg * 100 + k + 1] = q;
         }
       }
-      __syncthreads();
-      if (tid < 100) {  // per-step increments
-        double sn, cs;
-        mpj_sincos_bl(psi_s[tid], &sn, &cs);
-        double d0 = v * cs, d1 = v * sn;
-        d0 = d0 * P.minR;
-        d1 = d1 * P.minR;
-        ix_s[tid] = d0 * dt;
-        iy_s[tid] = d1 * dt;
-      }
-      __syncthreads();
-      if (tid == 0) {  // running sums in order
-#pragma unroll 10
-        for (int k = 0; k < 100; k++) {
-          sx = sx + ix_s[k];
-          sy = sy + iy_s[k];
-          double* o = path_s + 3 * (1 + seg * 100 + k);
-          o[0] = sx;
-          o[1] = sy;
-          o[2] = psi_s[k + 1];
-        }
-        ix_s[100] = sx;
-        iy_s[100] = sy;
-      }
-      __syncthreads();
-      sx = ix_s[100];
-      sy = iy_s[100];
-      sp = psi_s[100];
-      HMARK(10 + seg);
-      HTIME(4 + seg);
-      __syncthreads();
     }
-    const int n = 100 * nseg + 1;
+    __syncthreads();
+    for (int t = tid; t < nst; t += HT) {  // per-step increments
+      const int seg = t / 100;
+      const double dt = __builtin_fabs(cmd[seg * 3]) / 100, v = cmd[seg * 3 + 1];
+      double sn, cs;
+      mpj_sincos_bl(psi_s[t], &sn, &cs);
+      double d0 = v * cs, d1 = v * sn;
+      d0 = d0 * P.minR;
+      d1 = d1 * P.minR;
+      ix_s[t] = d0 * dt;
+      iy_s[t] = d1 * dt;
+      path_s[3 * (t + 1) + 2] = psi_s[t + 1];
+    }
+    __syncthreads();
+    if (tid == 0 || tid == 64) {  // running sums in order: x on wave 0, y on wave 1
+      const int c = tid == 0 ? 0 : 1;
+      const double* inc = c == 0 ? ix_s : iy_s;
+      double acc = node[c];
+      path_s[c] = acc;
+      // batches of 20 increments into registers first: the LDS reads then pipeline instead of
+      // each waiting behind the previous path store (the compiler cannot disprove aliasing)
+      for (int t0 = 0; t0 < nst; t0 += 20) {  // nst is a multiple of 100
+        double v[20];
+#pragma unroll
+        for (int u = 0; u < 20; u++) v[u] = inc[t0 + u];
+#pragma unroll
+        for (int u = 0; u < 20; u++) {
+          acc = acc + v[u];
+          path_s[3 * (t0 + u + 1) + c] = acc;
+        }
+      }
+    }
+    if (tid == 0) path_s[2] = node[2];
+    __syncthreads();
+    const int n = nst + 1;
     for (int i = tid; i < 3 * n; i += HT) R.path[i] = path_s[i];
     npose = n > 5 ? (n - 1) / 5 + 1 : 1;  // block_collision_check on poses 1:5:end
     if (tid == 0) sh_n = n;
@@ -608,6 +621,7 @@ __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   for (int t = tid; t < total; t += HT) {
     const int jn = rs ? 0 : t / npose, jp = rs ? t : t - jn * npose;
     if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
+    if (!g_free[jn]) continue;  // already colliding: block_collision_check stops at its first hit
     double q[3];
     if (rs) {
       q[0] = path_s[3 * (jp * 5)];
@@ -717,6 +731,16 @@ int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
   return MP_OK;
 }
 
+// Block2Pts + the wall-side SAT tables (pose independent) once per plan: [B][nw][34]
+__global__ __launch_bounds__(64) void ha_wall_kernel(HaDev P, int B, const double* walls, double* wtab) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= B * P.n_walls) return;
+  const double* wl = walls + (size_t)i * 5;
+  double* o = wtab + (size_t)i * 34;
+  rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], o);
+  sat_base_pre(o, o + 10);
+}
+
 // ------------------------------------------------ device-resident search state
 // planHybridAstar! (hybrid_astar_utils.jl:235-296) bookkeeping on the device, one scene per
 // block, all arrays scene-major.  Nodes are numbered in creation order (as Dict insertion in
@@ -736,9 +760,14 @@ struct HaSearch {
   long long* seq;        // [B][C]
   int* pos;              // [B][C] open-list position, -1 = not in the open list
   int* nid;              // [B][C] cell -> node id, -1 = absent
-  double* of;            // [B][C] open entries: f, seq, node id
-  long long* oseq;
+  double* of;            // [B][C] open entries: f, seq, node id, and the node's g, Encode
+  long long* oseq;       // index and state (so popfirst! needs no second dependent load)
   int* oid;
+  double* og;
+  long long* oix;
+  double* ost;           // [B][C][3]
+  double* cur_g;         // [B] popped node's g and Encode index
+  long long* cur_ix;
   int* sc_i;             // [8][B] per-scene ints: n_nodes, n_open, loop, cur, active, found, n_states, rs_len
   long long* ctr;        // [B] seq counter
   long long* start_index;// [B]
@@ -756,18 +785,36 @@ __device__ __forceinline__ bool key_before(double af, long long as, double cf, l
   return as < cs;
 }
 
-// popfirst! for scene b (one wave): the least (f, seq) open entry, removed by moving the last
-// entry into its place.  Returns false when the search ends here (open list empty / max_pops).
-__device__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int lane) {
+// popfirst! for scene b (a 256-thread block): the least (f, seq) open entry, found by a
+// strided scan (4 independent entry loads in flight per thread) and a wave then block
+// reduction (the key order is total, so the reduction order does not matter); wave 0 removes
+// it by moving the last entry into its place.  Returns false (block-uniform) when the search
+// ends here (open list empty / max_pops).
+constexpr int BKT = 256;
+__device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int tid) {
+  __shared__ double r_f[BKT / 64];
+  __shared__ long long r_s[BKT / 64];
+  __shared__ int r_p[BKT / 64];
   const size_t base = (size_t)b * Q.C;
   if (n_open == 0 || loop >= Q.mp) return false;
+  const int lane = tid & 63, wave = tid >> 6;
   double bf = __builtin_inf();
   long long bs = 0x7fffffffffffffffLL;
   int bp = -1;
-  for (int p = lane; p < n_open; p += 64) {
-    const double fv = Q.of[base + p];
-    const long long sv = Q.oseq[base + p];
-    if (bp < 0 || key_before(fv, sv, bf, bs)) { bf = fv; bs = sv; bp = p; }
+  for (int p0 = tid; p0 < n_open; p0 += 4 * BKT) {
+    double fv[4];
+    long long sv[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int p = p0 + u * BKT;
+      fv[u] = p < n_open ? Q.of[base + p] : 0.0;
+      sv[u] = p < n_open ? Q.oseq[base + p] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int p = p0 + u * BKT;
+      if (p < n_open && (bp < 0 || key_before(fv[u], sv[u], bf, bs))) { bf = fv[u]; bs = sv[u]; bp = p; }
+    }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) {
@@ -776,23 +823,47 @@ __device__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, in
     const int op = __shfl_xor(bp, o);
     if (op >= 0 && (bp < 0 || key_before(of_, os, bf, bs))) { bf = of_; bs = os; bp = op; }
   }
+  if (lane == 0) { r_f[wave] = bf; r_s[wave] = bs; r_p[wave] = bp; }
+  __syncthreads();
+  if (tid >= 64) return true;
+  for (int w = 1; w < BKT / 64; w++) {
+    const int op = r_p[w];
+    if (op >= 0 && (bp < 0 || key_before(r_f[w], r_s[w], bf, bs))) { bf = r_f[w]; bs = r_s[w]; bp = op; }
+  }
+  // the winning entry (one dependent load) and the last entry (moved into its place)
+  const int last = n_open - 1;
   const int id = Q.oid[base + bp];
-  if (lane == 0) {
-    const int last = n_open - 1;
-    if (bp != last) {
-      const int lid = Q.oid[base + last];
-      Q.of[base + bp] = Q.of[base + last];
-      Q.oseq[base + bp] = Q.oseq[base + last];
+  const double gw = Q.og[base + bp];
+  const long long iw = Q.oix[base + bp];
+  double stw = 0.0, stl = 0.0;
+  if (lane < 3) {
+    stw = Q.ost[(base + bp) * 3 + lane];
+    stl = Q.ost[(base + last) * 3 + lane];
+  }
+  const double fl = Q.of[base + last], gl = Q.og[base + last];
+  const long long sl = Q.oseq[base + last], il = Q.oix[base + last];
+  const int lid = Q.oid[base + last];
+  if (bp != last) {
+    if (lane == 0) {
+      Q.of[base + bp] = fl;
+      Q.oseq[base + bp] = sl;
       Q.oid[base + bp] = lid;
+      Q.og[base + bp] = gl;
+      Q.oix[base + bp] = il;
       Q.pos[base + lid] = bp;
     }
+    if (lane < 3) Q.ost[(base + bp) * 3 + lane] = stl;
+  }
+  if (lane == 0) {
     Q.pos[base + id] = -1;
     Q.sc_i[SI_NOPEN * B + b] = last;
     Q.sc_i[SI_LOOP * B + b] = loop + 1;
     Q.sc_i[SI_CUR * B + b] = id;
-    Q.pop_seq[(size_t)b * Q.mp + loop] = Q.index[base + id];
+    Q.pop_seq[(size_t)b * Q.mp + loop] = iw;
+    Q.cur_g[b] = gw;
+    Q.cur_ix[b] = iw;
   }
-  if (lane < 3) Q.node[3 * b + lane] = Q.st[(base + id) * 3 + lane];
+  if (lane < 3) Q.node[3 * b + lane] = stw;
   return true;
 }
 
@@ -811,6 +882,8 @@ __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B
     Q.seq[base] = 0;
     Q.pos[base] = 0;
     Q.of[base] = 0.0; Q.oseq[base] = 0; Q.oid[base] = 0;
+    Q.og[base] = 0.0; Q.oix[base] = si;
+    for (int r = 0; r < 3; r++) Q.ost[base * 3 + r] = s0[r];
     Q.ctr[b] = 1;
     Q.start_index[b] = si;
     Q.sc_i[SI_NNODES * B + b] = 1;
@@ -824,34 +897,28 @@ __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B
     if (si >= 0 && si < Q.C) Q.nid[base + si] = 0;
   }
   __syncthreads();
-  if (tid < 64) {  // wave 0
-    const bool go = ha_pop(Q, B, b, 1, 0, tid);
-    if (tid == 0) Q.sc_i[SI_ACTIVE * B + b] = go;
-  }
+  const bool go = ha_pop(Q, B, b, 1, 0, tid);
+  if (tid == 0) Q.sc_i[SI_ACTIVE * B + b] = go;
 }
 
-// One search iteration's bookkeeping for scene b (one wave), after ha_iter_kernel wrote the
-// scene's RS_connected result and the 62 neighbours (array mode): termination (:259-271) or
-// FindNewNode's Dict/open-list updates (:418-446), then the next popfirst!.
-__global__ __launch_bounds__(64) void ha_book_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
-  __shared__ long long s_idx[64];
-  __shared__ int s_first[64], s_chg[64];
-  __shared__ double s_of[64];
-  __shared__ long long s_os[64];
-  const int b = blockIdx.x, lane = threadIdx.x;
+// One search iteration's bookkeeping for scene b, after ha_iter_kernel wrote the scene's
+// RS_connected result and the 62 neighbours (array mode): termination (:259-271) or
+// FindNewNode's Dict/open-list updates (:418-446) on wave 0 (neighbour k on lane k), then the
+// next popfirst! (whole block).
+__global__ __launch_bounds__(BKT) void ha_book_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
+  __shared__ int s_nopen;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   if (!Q.sc_i[SI_ACTIVE * B + b]) return;
   const size_t base = (size_t)b * Q.C;
   const int np = P.n_prim;
-  const int cur = Q.sc_i[SI_CUR * B + b];
-  int n_open = Q.sc_i[SI_NOPEN * B + b];
   const int loop = Q.sc_i[SI_LOOP * B + b];
   if (A.rs_ok[b]) {  // RS_connected: path found -> hybrid_astar_states by the parent chain
-    if (lane == 0) {
+    if (tid == 0) {
       Q.sc_i[SI_FOUND * B + b] = 1;
       Q.sc_i[SI_ACTIVE * B + b] = 0;
       Q.sc_i[SI_RSLEN * B + b] = A.rs_len[b];
       double* so = Q.states + (size_t)b * Q.mp * 3;
-      int c = cur, ns = 0;
+      int c = Q.sc_i[SI_CUR * B + b], ns = 0;
       for (int r = 0; r < 3; r++) so[r] = Q.st[(base + c) * 3 + r];
       ns++;
       while (Q.parent[base + c] >= 0 && Q.index[base + c] != Q.start_index[b] && ns < Q.mp) {
@@ -865,98 +932,119 @@ __global__ __launch_bounds__(64) void ha_book_kernel(HaDev P, HaSearch Q, IterAr
     }
     return;
   }
-  // ---- FindNewNode (:391-447): neighbour k on lane k; only the first valid occurrence of an
-  // Encode index in this expansion can change anything (every neighbour has the same tentative g)
-  const int k = lane;
-  const long long ix = k < np ? A.idx[(size_t)b * np + k] : 0;
-  const bool valid = k < np && ix != 0 && A.fr[(size_t)b * np + k];
-  s_idx[k] = valid ? ix : 0;
-  __syncthreads();
-  bool first = valid;
-  for (int j = 0; j < k && first; j++) first = s_idx[j] != ix;
-  const double tg = Q.g[base + cur] + P.expand_time;
-  const long long cidx = Q.index[base + cur];
-  double th = 0.0, tf = 0.0;
-  int id = -1;
-  bool chg = false, app = false, isnew = false;
-  double fo = 0.0;
-  long long so_ = 0;
-  if (first) {
-    const double hk = A.h[(size_t)b * np + k];
-    th = __builtin_fmax(hk, 0.0);
-    if (hk != hk) th = hk;
-    tf = tg + th;
-    const int hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
-    if (hit >= 0) {
-      id = hit;
-      if (tg < Q.g[base + id]) {
-        if (Q.pos[base + id] >= 0) {
-          chg = true;
-          fo = Q.f[base + id];
-          so_ = Q.seq[base + id];
-        } else {
-          app = true;
+  if (tid < 64) {
+    // ---- FindNewNode (:391-447): only the first valid occurrence of an Encode index in this
+    // expansion can change anything (every neighbour has the same tentative g)
+    int n_open = Q.sc_i[SI_NOPEN * B + b];
+    const int k = lane;
+    const long long ix = k < np ? A.idx[(size_t)b * np + k] : 0;
+    const bool valid = k < np && ix != 0 && A.fr[(size_t)b * np + k];
+    const long long vix = valid ? ix : 0;
+    bool dup = false;
+#pragma unroll 16
+    for (int j = 0; j < 64; j++) {  // lane exchange (no LDS round trip), loads independent of k
+      const long long oj = __shfl(vix, j);
+      dup = dup | (j < k && oj == ix);
+    }
+    const bool first = valid && !dup;
+    const double tg = Q.cur_g[b] + P.expand_time;
+    const long long cidx = Q.cur_ix[b];
+    double th = 0.0, tf = 0.0;
+    int id = -1;
+    bool chg = false, app = false, isnew = false;
+    double fo = 0.0;
+    long long so_ = 0;
+    double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;  // the node's state and Encode index (its open entry)
+    long long nix = ix;
+    if (first) {
+      const double hk = A.h[(size_t)b * np + k];
+      th = __builtin_fmax(hk, 0.0);
+      if (hk != hk) th = hk;
+      tf = tg + th;
+      const int hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
+      if (hit >= 0) {
+        id = hit;
+        const double go = Q.g[base + id];
+        const int po = Q.pos[base + id];
+        const double fo_ = Q.f[base + id];
+        const long long so0 = Q.seq[base + id], io = Q.index[base + id];
+        nst0 = Q.st[(base + id) * 3];
+        nst1 = Q.st[(base + id) * 3 + 1];
+        nst2 = Q.st[(base + id) * 3 + 2];
+        nix = io;
+        if (tg < go) {
+          if (po >= 0) {
+            chg = true;
+            fo = fo_;
+            so_ = so0;
+          } else {
+            app = true;
+          }
         }
+      } else {
+        isnew = true;
+        app = true;
+        nst0 = A.nb[((size_t)b * np + k) * 3];
+        nst1 = A.nb[((size_t)b * np + k) * 3 + 1];
+        nst2 = A.nb[((size_t)b * np + k) * 3 + 2];
       }
-    } else {
-      isnew = true;
-      app = true;
     }
-  }
-  const unsigned long long m_new = __ballot(isnew), m_chg = __ballot(chg), m_app = __ballot(app);
-  const unsigned long long below = (1ull << k) - 1;  // lanes < k
-  const int n_new = __popcll(m_new), n_chg = __popcll(m_chg), n_app = __popcll(m_app);
-  const int nn0 = Q.sc_i[SI_NNODES * B + b];
-  if (isnew) id = nn0 + __popcll(m_new & below);
-  s_chg[k] = chg;
-  s_of[k] = fo;
-  s_os[k] = so_;
-  __syncthreads();
-  const long long ctr = Q.ctr[b];
-  long long nseq = 0;
-  if (chg) {  // in-place updates keep their previous list order
+    const unsigned long long m_new = __ballot(isnew), m_chg = __ballot(chg), m_app = __ballot(app);
+    const unsigned long long below = (1ull << k) - 1;  // lanes < k
+    const int n_new = __popcll(m_new), n_chg = __popcll(m_chg), n_app = __popcll(m_app);
+    const int nn0 = Q.sc_i[SI_NNODES * B + b];
+    if (isnew) id = nn0 + __popcll(m_new & below);
+    const long long ctr = Q.ctr[b];
+    // in-place updates keep their previous list order: rank by the old key among the changed
     int r = 0;
-    for (int j = 0; j < 64; j++)
-      if (s_chg[j] && key_before(s_of[j], s_os[j], fo, so_)) r++;
-    nseq = ctr + r;
-  } else if (app) {  // then push! in neighbour order
-    nseq = ctr + n_chg + __popcll(m_app & below);
-  }
-  if (chg || app) {
-    const size_t q = base + id;
-    if (isnew) {
-      Q.st[q * 3] = A.nb[((size_t)b * np + k) * 3];
-      Q.st[q * 3 + 1] = A.nb[((size_t)b * np + k) * 3 + 1];
-      Q.st[q * 3 + 2] = A.nb[((size_t)b * np + k) * 3 + 2];
-      Q.index[q] = ix;
-      if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
+    for (unsigned long long m = m_chg; m; m &= m - 1) {
+      const int j = __builtin_ctzll(m);
+      const double fj = __shfl(fo, j);
+      const long long sj = __shfl(so_, j);
+      r += chg && key_before(fj, sj, fo, so_);
     }
-    Q.g[q] = tg;
-    Q.h[q] = th;
-    Q.f[q] = tf;
-    Q.parent[q] = cidx;
-    Q.seq[q] = nseq;
-    if (chg) {
-      const int p = Q.pos[q];
+    long long nseq = 0;
+    if (chg) nseq = ctr + r;
+    else if (app) nseq = ctr + n_chg + __popcll(m_app & below);  // then push! in neighbour order
+    if (chg || app) {
+      const size_t q = base + id;
+      if (isnew) {
+        Q.st[q * 3] = nst0;
+        Q.st[q * 3 + 1] = nst1;
+        Q.st[q * 3 + 2] = nst2;
+        Q.index[q] = ix;
+        if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
+      }
+      Q.g[q] = tg;
+      Q.h[q] = th;
+      Q.f[q] = tf;
+      Q.parent[q] = cidx;
+      Q.seq[q] = nseq;
+      const int p = chg ? Q.pos[q] : n_open + __popcll(m_app & below);
       Q.of[base + p] = tf;
       Q.oseq[base + p] = nseq;
-    } else {
-      const int p = n_open + __popcll(m_app & below);
-      Q.of[base + p] = tf;
-      Q.oseq[base + p] = nseq;
-      Q.oid[base + p] = id;
-      Q.pos[q] = p;
+      Q.og[base + p] = tg;
+      if (!chg) {
+        Q.oid[base + p] = id;
+        Q.oix[base + p] = nix;
+        Q.ost[(base + p) * 3] = nst0;
+        Q.ost[(base + p) * 3 + 1] = nst1;
+        Q.ost[(base + p) * 3 + 2] = nst2;
+        Q.pos[q] = p;
+      }
+    }
+    n_open += n_app;
+    if (lane == 0) {
+      Q.sc_i[SI_NNODES * B + b] = nn0 + n_new;
+      Q.ctr[b] = ctr + n_chg + n_app;
+      s_nopen = n_open;
     }
   }
-  n_open += n_app;
-  if (lane == 0) {
-    Q.sc_i[SI_NNODES * B + b] = nn0 + n_new;
-    Q.ctr[b] = ctr + n_chg + n_app;
-  }
-  __syncthreads();
+  __syncthreads();  // the open-list writes of wave 0 before the block-wide scan
+  const int n_open = s_nopen;
   // ---- next popfirst!
-  const bool go = ha_pop(Q, B, b, n_open, loop, lane);
-  if (lane == 0) {
+  const bool go = ha_pop(Q, B, b, n_open, loop, tid);
+  if (tid == 0) {
     if (go) atomicAdd(Q.live + it, 1);
     else {
       Q.sc_i[SI_ACTIVE * B + b] = 0;
@@ -1135,9 +1223,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_CHECK(ctx, ncell > 0 && ncell < (1LL << 26), "state lattice too large (%lld cells)", ncell);
   const size_t C = (size_t)ncell + 1, nB = (size_t)B;
   // search state: node arrays and open list indexed [scene][node / cell]
-  const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4;
-  char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 16) + nB * mp * 32 + nB * 24 +
-                                           sizeof(int) * (mp + 2) + 256 * 16);
+  const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24;
+  char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 24 +
+                                           sizeof(int) * (mp + 2) + 256 * 32);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -1156,6 +1244,11 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.of = (double*)take(nB * C * 8);
   Q.oseq = (long long*)take(nB * C * 8);
   Q.oid = (int*)take(nB * C * 4);
+  Q.og = (double*)take(nB * C * 8);
+  Q.oix = (long long*)take(nB * C * 8);
+  Q.ost = (double*)take(nB * C * 24);
+  Q.cur_g = (double*)take(nB * 8);
+  Q.cur_ix = (long long*)take(nB * 8);
   Q.sc_i = (int*)take(nB * SI_N * 4);
   Q.ctr = (long long*)take(nB * 8);
   Q.start_index = (long long*)take(nB * 8);
@@ -1175,6 +1268,13 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.rs_len = (int*)mp_ws(ctx, WS_IO6, sizeof(int) * nB);
   A.rs_path = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * nB * MAXPATH * 3);
   if (st || !A.h || !A.nb || !A.idx || !A.fr || !A.rs_ok || !A.rs_len || !A.rs_path) return st ? st : MP_ERR_NOMEM;
+  if (p->n_walls) {
+    double* wt = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * nB * p->n_walls * 34);
+    if (!wt) return MP_ERR_NOMEM;
+    hipLaunchKernelGGL(ha_wall_kernel, dim3((unsigned)((B * p->n_walls + 63) / 64)), dim3(64), 0, ctx->stream, D, B,
+                       A.walls, wt);
+    A.wtab = wt;
+  }
   A.node = Q.node;
   A.scene_of = nullptr;  // slot = scene
   A.active = Q.sc_i + SI_ACTIVE * B;
@@ -1205,7 +1305,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     mp_time_begin(ctx);
     hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(B * per)), dim3(HT), 0, ctx->stream, D, A);
     mp_time_end(ctx);
-    hipLaunchKernelGGL(ha_book_kernel, dim3(B), dim3(64), 0, ctx->stream, D, Q, A, B, it);
+    hipLaunchKernelGGL(ha_book_kernel, dim3(B), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
     if (it % CH == 0 || it == mp) {
       const int slot = chunk % NCK;

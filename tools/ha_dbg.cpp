@@ -42,8 +42,8 @@ int main() {
   th.join();
   {
     const unsigned long long* t = reinterpret_cast<const unsigned long long*>(buf + 64 * 64);
-    printf("RS block phase cycles from start:");
-    for (int i = 1; i <= 14; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
+    printf("RS block stamps (cycles from [0]):");
+    for (int i = 1; i < 16; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
     printf("\n");
   }
   printf("st %d ok %d len %d end %g %g %g\n", st, ok, len, path[3 * (len - 1)], path[3 * (len - 1) + 1], path[3 * (len - 1) + 2]);
@@ -61,10 +61,11 @@ int main() {
     uint8_t fr[62];
     printf("expand %d\n", mp_ha_expand(ctx, &p, 1, node, goal, walls, nb, idx, fr, hh));
     const unsigned long long* t = reinterpret_cast<const unsigned long long*>(buf + 64 * 64);
-    for (int blk = 1; blk <= 4; blk++)
-      printf("expand block %d: walls %lld encode %lld collision %lld heuristic %lld\n", blk,
-             (long long)(t[blk * 16 + 1] - t[blk * 16]), (long long)(t[blk * 16 + 11] - t[blk * 16 + 1]),
-             (long long)(t[blk * 16 + 12] - t[blk * 16 + 11]), (long long)(t[blk * 16 + 13] - t[blk * 16 + 12]));
+    for (int blk = 1; blk <= 4; blk++) {
+      printf("expand block %d stamps:", blk);
+      for (int i = 1; i < 16; i++) printf(" [%d]%lld", i, t[blk * 16 + i] ? (long long)(t[blk * 16 + i] - t[blk * 16]) : -1LL);
+      printf("\n");
+    }
   }
   mp_ctx_destroy(ctx);
   return 0;
