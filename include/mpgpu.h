@@ -260,9 +260,11 @@ int mp_ha_allpath(mp_ctx* ctx, int32_t B, const double* norm_states, double* cos
                   double* cmds, int32_t* best);
 
 /* Whole planHybridAstar! search loop (hybrid_astar_utils.jl:235-296) for B
- * scenes in lockstep: the open-list / Dict bookkeeping runs on the host (C++),
- * every expansion and RS-connect runs on the device, one fused launch per
- * iteration.  start[B][3], goal[B][3] already regulated (setup.jl:110-112).
+ * scenes in lockstep, entirely on the device: per iteration one fused
+ * RS-connect + expansion launch and one bookkeeping launch (Dict, open list in
+ * the reference's stable-sort order, popfirst!), enqueued without host round
+ * trips.  n_prim <= 64.  start[B][3], goal[B][3] already regulated
+ * (setup.jl:110-112).
  * out: found[B], pops[B] (loop_count), n_nodes[B] (length(nodes_collection)),
  *      pop_seq[B][max_pops] (Encode index of each popped node, -1 padded),
  *      n_states[B] and states_out[B][max_pops][3] (hybrid_astar_states, goal→start order),
@@ -277,8 +279,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
  * (bit-exactness check against the CPU build).  fn: 0 sin, 1 cos, 2 tan, 3 atan,
  * 4 atan2(x, y), 5 asin, 6 acos, 7 exp, 8 log, 9 modpi, 10 sqrt; the branch-free
  * variants of the hot kernels: 11 modpi_bl, 12 atan_bl, 13 atan_tab, 14 sin (sincos_bl),
- * 15 cos (sincos_bl), 16 exp_bl, 17 tan_bl, 18 atan2_sel(x, y), 19 sin / 20 cos (sincos_wide) — each must equal its exact
- * routine bit for bit. */
+ * 15 cos (sincos_bl), 16 exp_bl, 17 tan_bl, 18 atan2_sel(x, y), 19 sin / 20 cos (sincos_wide),
+ * 21 tan_wide — each must equal its exact routine bit for bit. */
 int mp_math_eval(mp_ctx* ctx, int32_t fn, int64_t n, const double* x, const double* y, double* out);
 
 #ifdef __cplusplus

@@ -10,17 +10,12 @@
 //                     on 16 lanes, the (neighbour, pose) SAT collision sweep across all
 //                     lanes, then the 48-candidate rs_heuristic of all 16 neighbours at once
 //                     (lanes 4j..4j+3 = the four variants of neighbour j, word loop uniform).
-// The open list / Dict bookkeeping of planHybridAstar! runs on the host (mp_ha_plan).
+// ha_book_kernel: the open list / Dict bookkeeping of planHybridAstar! and the next pop, on the
+// device (mp_ha_plan enqueues the whole search without host round trips).
 #include <algorithm>
-#include <atomic>
-#include <functional>
-#include <thread>
-#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
-#include <queue>
-#include <unordered_map>
 #include <vector>
 
 // the libm routines run under divergent control flow here (per-lane early returns, partial
@@ -364,14 +359,9 @@ struct IterArgs {
   long long* idx;        // [B][n_prim]
   unsigned char* fr;     // [B][n_prim]
   double* h;             // [B][n_prim]
-  // record mode (mp_ha_plan): all per-iteration outputs of active slot i packed in one record
-  // at rec + i*rb (h[n_prim] | nb[n_prim][3] | idx[n_prim] | len | ok | fr[n_prim]), so one
-  // D2H copy of n_active records returns an iteration's results; rs_path by slot as well
-  char* rec;
-  int rb;
 };
 
-// output addressing: per scene (array mode) or per active slot (record mode)
+// output addressing: per scene
 struct OutRef {
   double* h;
   double* nb;
@@ -381,26 +371,15 @@ struct OutRef {
   unsigned char* fr;
   double* path;
 };
-__device__ __forceinline__ OutRef out_ref(const IterArgs& A, int s, int slot, int n_prim) {
+__device__ __forceinline__ OutRef out_ref(const IterArgs& A, int s, int n_prim) {
   OutRef r;
-  if (A.rec) {
-    char* q = A.rec + (size_t)slot * A.rb;
-    r.h = (double*)q;
-    r.nb = r.h + n_prim;
-    r.idx = (long long*)(r.nb + 3 * n_prim);
-    r.len = (int*)(r.idx + n_prim);
-    r.ok = (unsigned char*)(r.len + 1);
-    r.fr = r.ok + 1;
-    r.path = A.rs_path + (size_t)slot * MAXPATH * 3;
-  } else {
-    r.h = A.h ? A.h + (size_t)s * n_prim : nullptr;
-    r.nb = A.nb ? A.nb + (size_t)s * n_prim * 3 : nullptr;
-    r.idx = A.idx ? A.idx + (size_t)s * n_prim : nullptr;
-    r.len = A.rs_len ? A.rs_len + s : nullptr;
-    r.ok = A.rs_ok ? A.rs_ok + s : nullptr;
-    r.fr = A.fr ? A.fr + (size_t)s * n_prim : nullptr;
-    r.path = A.rs_path ? A.rs_path + (size_t)s * MAXPATH * 3 : nullptr;
-  }
+  r.h = A.h ? A.h + (size_t)s * n_prim : nullptr;
+  r.nb = A.nb ? A.nb + (size_t)s * n_prim * 3 : nullptr;
+  r.idx = A.idx ? A.idx + (size_t)s * n_prim : nullptr;
+  r.len = A.rs_len ? A.rs_len + s : nullptr;
+  r.ok = A.rs_ok ? A.rs_ok + s : nullptr;
+  r.fr = A.fr ? A.fr + (size_t)s * n_prim : nullptr;
+  r.path = A.rs_path ? A.rs_path + (size_t)s * MAXPATH * 3 : nullptr;
   return r;
 }
 
@@ -500,7 +479,7 @@ __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   const int nw = P.n_walls;
   const double* node = A.node + 3 * s;
   const double* goal = A.goal + 3 * s;
-  const OutRef R = out_ref(A, s, slot, P.n_prim);
+  const OutRef R = out_ref(A, s, P.n_prim);
   const int k0 = rs ? 0 : (item - 1) * NBG, nk = rs ? 0 : min(NBG, P.n_prim - k0);
   // wall corners (Block2Pts) and their SAT tables in LDS: precomputed once per plan
   // (ha_wall_kernel) or evaluated here
