@@ -51,7 +51,11 @@ constexpr bool kFast = true;
 // sweep (355 vs 382 us).  The derivative kernel (405,504 threads, lanes of a wave take the same
 // libm branches) runs the exact routines in 154 us vs 296 us, and the one-thread-per-instance
 // forward trial / roll out (64 waves, latency-bound: fewer instructions win) in 361 vs 690 us.
+#if defined(MP_ILQR_FASTFWD)  // A/B build (measured slower: forward 689 vs 363 us, roll out 341 vs 277 us)
+constexpr bool kFastDeriv = false, kFastBwd = kFast, kFastFwd = kFast;
+#else
 constexpr bool kFastDeriv = false, kFastBwd = kFast, kFastFwd = false;
+#endif
 #if defined(MP_ILQR_NOREDO)
 constexpr bool kRedo = false;
 #else

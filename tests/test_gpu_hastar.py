@@ -74,9 +74,31 @@ def test_scenario_batch_lockstep_bitexact(ctx, n, seed):
     for h in hs:
         ref = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
         same = (h.r.found == ref["found"] and h.r.loop_count == ref["pops"] and h.r.n_nodes == ref["n_nodes"]
-                and np.array_equal(h.r.pop_sequence, ref["pop_seq"]))
+                and np.array_equal(h.r.pop_sequence, ref["pop_seq"])
+                and np.array_equal(h.r.hybrid_astar_states.T, ref["states"])
+                and np.array_equal(h.r.RSpath_final.T, ref["rs_path"]))
         mism += not same
     assert mism == 0
+
+
+@pytest.mark.parametrize("max_pops", [1, 7, 40])
+def test_max_pops_and_out_of_bounds_start_bitexact(ctx, max_pops):
+    """Device-resident search edge cases vs the oracle: the max_pops stop (pop_seq truncated,
+    not found), a start outside stbound (Encode 0 -> the start node sits in cell 0), and a start
+    on the lattice boundary, in one lockstep batch with ordinary scenes."""
+    hs = ha.scenario_batch(6, seed=9)
+    hs.append(ha.driver_searcher(ha.PERPENDICULAR, [11.0, 4.0, ha.PI / 2]))   # x > stbound: Encode 0
+    hs.append(ha.driver_searcher(ha.PARALLEL, [10.0, 10.0, -ha.PI / 2]))    # corner of the lattice
+    _, p, sc, pc = _setup(ctx)
+    ha.plan_batch(hs, ctx=ctx, max_pops=max_pops)
+    q = ha.params_of(hs[0], max_pops)
+    for h in hs:
+        ref = oracle.ha_plan(q, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+        assert h.r.loop_count == ref["pops"] <= max_pops
+        assert h.r.found == ref["found"] and h.r.n_nodes == ref["n_nodes"]
+        assert np.array_equal(h.r.pop_sequence, ref["pop_seq"])
+        assert np.array_equal(h.r.hybrid_astar_states.T, ref["states"])
+        assert np.array_equal(h.r.RSpath_final.T, ref["rs_path"])
 
 
 def test_allpath_bitexact(ctx):
