@@ -383,10 +383,18 @@ __device__ __forceinline__ OutRef out_ref(const IterArgs& A, int s, int n_prim) 
   return r;
 }
 
-constexpr int HT = 256;   // threads per block of ha_iter_kernel (4 waves)
-constexpr int HW = HT / 64;
+// threads per block of ha_iter_kernel: 4 waves, three Reeds–Shepp words per wave (HA_WAVES=6 or 12:
+// two words or one per wave: measured slower, 55 / 53 ms vs 45 ms per 256-scenario plan -- the
+// per-wave Reeds–Shepp set-up is repeated and the launch is already issue-bound).
+#ifndef HA_WAVES
+#define HA_WAVES 4
+#endif
+constexpr int HW = HA_WAVES;
+constexpr int HT = 64 * HW;
+constexpr int WPW = 12 / HW;  // Reeds–Shepp words per wave
+static_assert(12 % HW == 0, "HA_WAVES must divide the 12 Reeds-Shepp words");
 
-// allpath + findmin split over the block's 4 waves: wave w evaluates words 3w+1..3w+3 for
+// allpath + findmin split over the block's HW waves: wave w evaluates words WPW·w+1..WPW·(w+1) for
 // its lanes' candidates (lane&3 = variant of the state in `s`), the per-wave winners are
 // combined in LDS in word order with the same total order (rs_before).  Every wave returns
 // the block-wide winner for its lanes; *best_id is the winning candidate id.
@@ -402,7 +410,7 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   int bi = 1 << 20;
   Cmd cb;  // CMD: the commands of this lane's best word (its variant, this wave's words)
 #pragma unroll 1
-  for (int w = 3 * wave + 1; w <= 3 * wave + 3; w++) {
+  for (int w = WPW * wave + 1; w <= WPW * wave + WPW; w++) {
     Cmd c;
     const double cost = rs_word(w, R, &c);
     const int id = 4 * (w - 1) + var;
@@ -431,7 +439,7 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
     if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; }
   }
   *best_id = ix;
-  if (CMD && own == ix && tid == 64 * ((ix / 4) / 3) + (ix & 3)) {
+  if (CMD && own == ix && tid == 64 * ((ix / 4) / WPW) + (ix & 3)) {
     // the lane that evaluated the winning candidate stores its commands with allpath's
     // gear/steer flips (timeflip: gear, reflect: steer, reverse: both), as rs_commands does
     const int n = v < __builtin_inf() ? cb.n : 0;

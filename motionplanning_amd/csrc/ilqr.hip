@@ -480,19 +480,255 @@ __device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, b
   }
 }
 
+// Exchange a double with the other lane of the pair (DPP quad_perm [1,0,3,2]).
+__device__ __forceinline__ double dswap(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// pinv2 on a lane pair: the two square roots, the two atan2, the two sincos and the two
+// reciprocals of the closed-form SVD are the same operations on lane-selected operands (side 0
+// the first of each, side 1 the second), exchanged with one DPP swap each.  Every value is
+// computed exactly as in pinv2 (same operands, same operation), so Pm is bit-identical.
+template <bool FT>
+__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int side, int& bad) {
+  const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
+  const double a = side ? F : E, c = side ? G : H;
+  const double r0 = mpj_sqrt(a * a + c * c), r1 = dswap(r0);
+  const double Q = side ? r1 : r0, R = side ? r0 : r1;
+  const double sx = Q + R, sy = Q - R;
+  const double t0 = LM<FT>::atan2(side ? H : G, side ? E : F, bad), t1 = dswap(t0);
+  const double a1 = side ? t1 : t0, a2 = side ? t0 : t1;
+  const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
+  double sn, cs;
+  LM<FT>::sincos(side ? ph : th, &sn, &cs, bad);
+  const double so = dswap(sn), co = dswap(cs);
+  const double st = side ? so : sn, ct = side ? co : cs, sp = side ? sn : so, cp = side ? cs : co;
+  const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
+  const double tol = 4.440892098500626e-16 * smax;
+  const double sv = side ? sy : sx;
+  const double i0 = __builtin_fabs(sv) > tol ? 1.0 / sv : 0.0, io = dswap(i0);
+  const double i1 = side ? io : i0, i2 = side ? i0 : io;
+  Pm[0] = ct * i1 * cp - st * i2 * sp;
+  Pm[1] = ct * i1 * sp + st * i2 * cp;
+  Pm[2] = -st * i1 * cp - ct * i2 * sp;
+  Pm[3] = -st * i1 * sp + ct * i2 * cp;
+}
+
+// ILQR.jl:46-67 on a LANE PAIR per instance (side = lane & 1): the pair splits every matrix
+// product by rows (4x4: rows 2s, 2s+1; 2x4: row s), the pinv, Qu and the stores, and swaps the
+// halves the next product needs (DPP): Quu, KK, Vx and Vxx each step.  Each entry is computed
+// by exactly the operations of backward_sweep (same order), so the gains are bit-identical;
+// a lane issues ~60 % of the single-lane sweep's instructions and 2x the waves run.
+template <bool FT>
+__device__ __forceinline__ void backward_sweep_pair(const IlqrDev& P, int B, int b, int side, bool live,
+                                                    const double* X, const double* D, double* kout, double* Kout,
+                                                    int& bad) {
+  const int N = P.N;
+  const double e = P.eps;
+  const int V = P.variant;
+  const size_t ks = (size_t)ND * B;
+  const double* Db = D + b;
+  double cur[ND];
+#pragma unroll
+  for (int q = 0; q < ND; q++) cur[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
+  double Vx[4], Vxx[16];
+  {  // terminal FD (both lanes, once per sweep)
+    const double* xs = X + ((size_t)b * N + N - 1) * 4;
+    const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
+    double sp[4], sm[4], t1[4], t2[4], t3[4], t4[4];
+    const double c12 = 1 / (12 * (e * e)), c4 = 1 / (4 * (e * e));
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
+      sp[i] = s[i] + e;
+      sm[i] = s[i] - e;
+      Vx[i] = (terminal(V, sp) - terminal(V, sm)) / (2 * e);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) { t1[r] = s[r]; t2[r] = s[r]; t3[r] = s[r]; t4[r] = s[r]; }
+        if (i == j) {
+          t1[i] = s[i] + 2 * e; t2[i] = s[i] + e; t3[i] = s[i] - e; t4[i] = s[i] - 2 * e;
+          Vxx[4 * i + j] = c12 * (-terminal(V, t1) + 16 * terminal(V, t2) - 30 * terminal(V, s) +
+                                  16 * terminal(V, t3) - terminal(V, t4));
+        } else {
+          t1[i] = s[i] + e; t1[j] = s[j] + e;
+          t2[i] = s[i] - e; t2[j] = s[j] - e;
+          t3[i] = s[i] + e; t3[j] = s[j] - e;
+          t4[i] = s[i] - e; t4[j] = s[j] + e;
+          Vxx[4 * i + j] = c4 * (terminal(V, t1) + terminal(V, t2) - terminal(V, t3) - terminal(V, t4));
+        }
+      }
+  }
+  for (int j = N - 2; j >= 0; j--) {
+    double nxt[ND];
+    const size_t jn = j > 0 ? (size_t)(j - 1) : 0;
+#pragma unroll
+    for (int q = 0; q < ND; q++) nxt[q] = Db[jn * ks + (size_t)q * B];
+    const double* A = cur;
+    const double* Bm = cur + 16;
+    const double* lx = cur + 24;
+    const double* lu = cur + 28;
+    const double* lxx = cur + 30;
+    const double* luu = cur + 46;
+    const double* lux = cur + 50;
+    // own rows: i0 = 2*side, i0+1 of the 4-row products; row `side` of the 2-row ones
+    double Qx[2], Qxx[8], T44[8], T24[4], Qux_own[4], Quu_own[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int i = 2 * side + h;
+      double acc = A[0 * 4 + i] * Vx[0];
+#pragma unroll
+      for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vx[k];
+      Qx[h] = lx[i] + acc;
+    }
+    double Qu[2];
+    {
+      const int i = side;
+      double acc = Bm[0 * 2 + i] * Vx[0];
+#pragma unroll
+      for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vx[k];
+      const double q0 = lu[i] + acc, q1 = dswap(q0);
+      Qu[0] = side ? q1 : q0;
+      Qu[1] = side ? q0 : q1;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int i = 2 * side + h;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        double acc = A[0 * 4 + i] * Vxx[0 * 4 + c];
+#pragma unroll
+        for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vxx[k * 4 + c];
+        T44[4 * h + c] = acc;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        double acc = T44[4 * h + 0] * A[0 * 4 + c];
+#pragma unroll
+        for (int k = 1; k < 4; k++) acc = acc + T44[4 * h + k] * A[k * 4 + c];
+        Qxx[4 * h + c] = lxx[4 * i + c] + acc;
+      }
+    }
+    {
+      const int i = side;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        double acc = Bm[0 * 2 + i] * Vxx[0 * 4 + c];
+#pragma unroll
+        for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vxx[k * 4 + c];
+        T24[c] = acc;
+      }
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        double acc = T24[0] * Bm[0 * 2 + c];
+#pragma unroll
+        for (int k = 1; k < 4; k++) acc = acc + T24[k] * Bm[k * 2 + c];
+        Quu_own[c] = luu[2 * i + c] + acc;
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        double acc = T24[0] * A[0 * 4 + c];
+#pragma unroll
+        for (int k = 1; k < 4; k++) acc = acc + T24[k] * A[k * 4 + c];
+        Qux_own[c] = lux[4 * i + c] + acc;
+      }
+    }
+    double Quu[4];
+    {
+      const double o0 = dswap(Quu_own[0]), o1 = dswap(Quu_own[1]);
+      Quu[0] = side ? o0 : Quu_own[0];
+      Quu[1] = side ? o1 : Quu_own[1];
+      Quu[2] = side ? Quu_own[0] : o0;
+      Quu[3] = side ? Quu_own[1] : o1;
+    }
+    double Pm[4];
+    pinv2_pair<FT>(Quu, Pm, side, bad);
+    double kk[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) kk[i] = (-Pm[2 * i + 0]) * Qu[0] + (-Pm[2 * i + 1]) * Qu[1];
+    // KK row `side` needs both Qux rows: swap the own row, then the other half of KK
+    double KK[8];
+    {
+      double Qo[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) Qo[c] = dswap(Qux_own[c]);
+      const int i = side;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const double q0 = side ? Qo[c] : Qux_own[c], q1 = side ? Qux_own[c] : Qo[c];
+        const double kv = (-Pm[2 * i + 0]) * q0 + (-Pm[2 * i + 1]) * q1;
+        const double ko = dswap(kv);
+        KK[0 * 4 + c] = side ? ko : kv;
+        KK[1 * 4 + c] = side ? kv : ko;
+      }
+    }
+    if (live) {
+      double* ko = kout + ((size_t)b * (N - 1) + j) * 2;
+      double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8;
+      ko[side] = kk[side];
+#pragma unroll
+      for (int c = 0; c < 4; c++) Ko[2 * c + side] = KK[4 * side + c];
+    }
+    double qk[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) qk[i] = Quu[2 * i + 0] * kk[0] + Quu[2 * i + 1] * kk[1];
+    double vx[2], vxx[8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int i = 2 * side + h;
+      vx[h] = Qx[h] - (KK[0 * 4 + i] * qk[0] + KK[1 * 4 + i] * qk[1]);
+      double KQ[2];
+#pragma unroll
+      for (int c = 0; c < 2; c++) KQ[c] = KK[0 * 4 + i] * Quu[0 * 2 + c] + KK[1 * 4 + i] * Quu[1 * 2 + c];
+#pragma unroll
+      for (int c = 0; c < 4; c++) vxx[4 * h + c] = Qxx[4 * h + c] - (KQ[0] * KK[0 * 4 + c] + KQ[1] * KK[1 * 4 + c]);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const double o = dswap(vx[h]);
+      Vx[h] = side ? o : vx[h];
+      Vx[2 + h] = side ? vx[h] : o;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const double o = dswap(vxx[q]);
+      Vxx[q] = side ? o : vxx[q];
+      Vxx[8 + q] = side ? vxx[q] : o;
+    }
+#pragma unroll
+    for (int q = 0; q < ND; q++) cur[q] = nxt[q];
+  }
+}
+
+#if defined(MP_ILQR_PAIR)  // A/B build: a lane pair per instance (measured slower: 391 vs 354 us)
+constexpr int kBwdLanes = 2;
+#else
+constexpr int kBwdLanes = 1;
+#endif
 __global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, const double* X, const double* D,
                                                            const int* active, double* kout, double* Kout) {
-  // every lane stays active (the straight-line libm selects with wave ballots): lanes past B or
+  // kBwdLanes = 2: a lane pair per instance (32 instances per wave).  Every lane stays active
+  // (the straight-line libm selects with wave ballots, the pair swaps are DPP): lanes past B or
   // of converged instances recompute a live instance's sweep and store nothing
-  const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b0 = blockIdx.x * (64 / kBwdLanes) + (int)threadIdx.x / kBwdLanes;
+  const int side = kBwdLanes == 2 ? (threadIdx.x & 1) : 0;
   const bool live = b0 < B && (!active || active[b0]);
   if (__all(!live)) return;
   const int b = b0 < B ? b0 : B - 1;
   int bad = 0;
-  backward_sweep<kFastBwd>(P, B, b, live, X, D, kout, Kout, bad);
+  if (kBwdLanes == 2) backward_sweep_pair<kFastBwd>(P, B, b, side, live, X, D, kout, Kout, bad);
+  else backward_sweep<kFastBwd>(P, B, b, live, X, D, kout, Kout, bad);
   if (kFastBwd && kRedo && __any(bad)) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
     int d = 0;
-    backward_sweep<false>(P, B, b, live, X, D, kout, Kout, d);
+    if (kBwdLanes == 2) backward_sweep_pair<false>(P, B, b, side, live, X, D, kout, Kout, d);
+    else backward_sweep<false>(P, B, b, live, X, D, kout, Kout, d);
   }
 }
 
@@ -729,7 +965,8 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
   hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
                      active, dD);
   MP_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, dX, dD, active, dk,
+  const int ipb = 64 / kBwdLanes;  // instances per 64-thread block
+  hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + ipb - 1) / ipb), dim3(64), 0, ctx->stream, D, B, dX, dD, active, dk,
                      dK);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
