@@ -524,19 +524,36 @@ __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
   HMARK(6);
   HTIME(1);
   __syncthreads();
-  // allpath + findmin (one call site for both roles): RS_connected's optimal command from the
-  // popped node, or rs_heuristic of the 16 neighbours (lanes 4j..4j+3 = variants of neighbour j)
   const int j = lane >> 2;
-  double ns[3];
-  if (rs) change_basis(node, goal, P.minR, ns);
-  else change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
-  HTIME(2);
+  // collision sweep: (neighbour, pose) pairs of this group, or the RS path's poses
+  auto sweep = [&](int npose) {
+    double nsn = 0.0, ncs = 1.0;
+    if (!rs) mpj_sincos_bl(node[2], &nsn, &ncs);
+    const int total = rs ? npose : nk * npose;
+    for (int t = tid; t < total; t += HT) {
+      const int jn = rs ? 0 : t / npose, jp = rs ? t : t - jn * npose;
+      if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
+      if (!g_free[jn]) continue;  // already colliding: block_collision_check stops at its first hit
+      double q[3];
+      if (rs) {
+        q[0] = path_s[3 * (jp * 5)];
+        q[1] = path_s[3 * (jp * 5) + 1];
+        q[2] = path_s[3 * (jp * 5) + 2];
+      } else {
+        transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
+      }
+      if (!pose_free(P, q, wp, wpre, nw)) g_free[jn] = 0;  // every writer stores 0
+    }
+  };
+  double cb = 0.0;
   int best;
-  const double cb = rs ? rs_best_split<true>(ns, tid, &best, red_c, red_i, cmd)
-                       : rs_best_split<false>(ns, tid, &best, red_c, red_i);
-  HTIME(3);
-  int npose;
   if (rs) {
+    // allpath + findmin: RS_connected's optimal command from the popped node
+    double ns[3];
+    change_basis(node, goal, P.minR, ns);
+    HTIME(2);
+    cb = rs_best_split<true>(ns, tid, &best, red_c, red_i, cmd);
+    HTIME(3);
     // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment, all segments
     // at once -- the heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt over every step (one lane),
     // the per-step increments (all lanes), then the x and y running sums (one lane each, two
@@ -596,28 +613,22 @@ __global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) {
     __syncthreads();
     const int n = nst + 1;
     for (int i = tid; i < 3 * n; i += HT) R.path[i] = path_s[i];
-    npose = n > 5 ? (n - 1) / 5 + 1 : 1;  // block_collision_check on poses 1:5:end
     if (tid == 0) sh_n = n;
+    sweep(n > 5 ? (n - 1) / 5 + 1 : 1);  // block_collision_check on poses 1:5:end
   } else {
-    npose = P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1;  // dg_cost: primitive poses 1:5:n_col
-  }
-  // one collision sweep for both roles: (neighbour, pose) pairs or the RS path's poses
-  double nsn = 0.0, ncs = 1.0;
-  if (!rs) mpj_sincos_bl(node[2], &nsn, &ncs);
-  const int total = rs ? npose : nk * npose;
-  for (int t = tid; t < total; t += HT) {
-    const int jn = rs ? 0 : t / npose, jp = rs ? t : t - jn * npose;
-    if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
-    if (!g_free[jn]) continue;  // already colliding: block_collision_check stops at its first hit
-    double q[3];
-    if (rs) {
-      q[0] = path_s[3 * (jp * 5)];
-      q[1] = path_s[3 * (jp * 5) + 1];
-      q[2] = path_s[3 * (jp * 5) + 2];
-    } else {
-      transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
+    // dg_cost first (primitive poses 1:5:n_col): rs_heuristic is only used for neighbours that
+    // are collision-free and in bounds, so a group without one skips the 48 RS candidates
+    sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
+    __syncthreads();
+    int any = 0;
+    for (int q = 0; q < nk; q++) any |= (g_ix[q] != 0) & g_free[q];
+    if (any) {  // block-uniform
+      double ns[3];
+      change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
+      HTIME(2);
+      cb = rs_best_split<false>(ns, tid, &best, red_c, red_i);
+      HTIME(3);
     }
-    if (!pose_free(P, q, wp, wpre, nw)) g_free[jn] = 0;  // every writer stores 0
   }
   HMARK(20);
   HTIME(10);
@@ -1289,9 +1300,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   int chunk = 0, checked = 0;
   bool finished = false;
   for (int it = 1; it <= mp && !finished; it++) {
-    mp_time_begin(ctx);
     hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(B * per)), dim3(HT), 0, ctx->stream, D, A);
-    mp_time_end(ctx);
     hipLaunchKernelGGL(ha_book_kernel, dim3(B), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
     if (it % CH == 0 || it == mp) {

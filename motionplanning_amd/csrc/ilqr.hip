@@ -326,17 +326,24 @@ __device__ __forceinline__ void pinv2(const double* M, double* Pm, int& bad) {
 // ILQR.jl:46-67 for instance b: one thread per instance (the sweep is a serial chain in j).
 // The derivative record of knot j-1 is loaded while knot j is processed (coalesced: the
 // records are component-major, instance fastest), so the chain never waits on memory.
-template <bool FT>
+// LDS barrier between the compute wave and the loader wave of a staged block: LDS traffic
+// retired, no vmcnt wait (the compute wave's gain stores and the loader's in-flight record
+// loads stay outstanding across it), and a compiler barrier for memory.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <bool FT, bool STAGED = false>
 __device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, bool live, const double* X,
-                                               const double* D, double* kout, double* Kout, int& bad) {
+                                               const double* D, double* kout, double* Kout, int& bad,
+                                               const double* lds = nullptr, int lane = 0) {
   const int N = P.N;
   const double e = P.eps;
   const int V = P.variant;
   const size_t ks = (size_t)ND * B;  // knot stride of the records
   const double* Db = D + b;
   double cur[ND];
+  if (!STAGED)
 #pragma unroll
-  for (int q = 0; q < ND; q++) cur[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
+    for (int q = 0; q < ND; q++) cur[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
   double Vx[4], Vxx[16];
   {  // CalculateMatrix(StatesList[:, end], [0 0], TerminalCost): only lx, lxx are used
     const double* xs = X + ((size_t)b * N + N - 1) * 4;
@@ -370,11 +377,18 @@ __device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, b
         }
       }
   }
-  for (int j = N - 2; j >= 0; j--) {
+  for (int j = N - 2, t = 0; j >= 0; j--, t++) {
     double nxt[ND];
-    const size_t jn = j > 0 ? (size_t)(j - 1) : 0;
+    if (STAGED) {  // knot j's records, staged by the loader wave before barrier t
+      lds_barrier();
+      const double* bf = lds + (size_t)(t & 1) * ND * 64 + lane;
 #pragma unroll
-    for (int q = 0; q < ND; q++) nxt[q] = Db[jn * ks + (size_t)q * B];
+      for (int q = 0; q < ND; q++) cur[q] = bf[q * 64];
+    } else {
+      const size_t jn = j > 0 ? (size_t)(j - 1) : 0;
+#pragma unroll
+      for (int q = 0; q < ND; q++) nxt[q] = Db[jn * ks + (size_t)q * B];
+    }
     const double* A = cur;        // [4][4]
     const double* Bm = cur + 16;  // [4][2]
     const double* lx = cur + 24;
@@ -475,8 +489,32 @@ __device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, b
 #pragma unroll
       for (int c = 0; c < 4; c++)
         Vxx[4 * i + c] = Qxx[4 * i + c] - (KQ[2 * i + 0] * KK[0 * 4 + c] + KQ[2 * i + 1] * KK[1 * 4 + c]);
+    if (!STAGED)
 #pragma unroll
-    for (int q = 0; q < ND; q++) cur[q] = nxt[q];
+      for (int q = 0; q < ND; q++) cur[q] = nxt[q];
+  }
+}
+
+// The loader wave of a staged block: knot j's records (component-major, the 64 instances of
+// the block contiguous per component: coalesced 512-B loads) into LDS buffer t&1 before barrier
+// t, with knot j-1's loads already in flight across that barrier and the compute wave's step.
+__device__ __forceinline__ void record_loader(const IlqrDev& P, int B, int b, const double* D, double* lds,
+                                              int lane) {
+  const int N = P.N;
+  const size_t ks = (size_t)ND * B;
+  const double* Db = D + b;
+  double v[ND];
+#pragma unroll
+  for (int q = 0; q < ND; q++) v[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
+  for (int j = N - 2, t = 0; j >= 0; j--, t++) {
+    double* bf = lds + (size_t)(t & 1) * ND * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < ND; q++) bf[q * 64] = v[q];
+    if (j > 0) {
+#pragma unroll
+      for (int q = 0; q < ND; q++) v[q] = Db[(size_t)(j - 1) * ks + (size_t)q * B];
+    }
+    lds_barrier();
   }
 }
 
@@ -707,6 +745,37 @@ __device__ __forceinline__ void backward_sweep_pair(const IlqrDev& P, int B, int
   }
 }
 
+// Riccati sweep with LDS-staged records (default): block = compute wave + loader wave for 64
+// instances.  The single-wave sweep spent ~2 us of its ~3.6 us per knot waiting on the knot's
+// 58 record loads (the compiler sinks prefetches to cut register pressure); here the compute
+// wave reads them from LDS and the loader wave keeps the next knot's loads in flight.
+__global__ __launch_bounds__(128) void ilqr_backward_staged_kernel(IlqrDev P, int B, const double* X,
+                                                                  const double* D, const int* active, double* kout,
+                                                                  double* Kout) {
+  extern __shared__ double recs[];  // [2][ND][64]
+  __shared__ int sh_redo;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int b0 = blockIdx.x * 64 + lane;
+  const bool live = b0 < B && (!active || active[b0]);
+  if (__all(!live)) return;  // the same 64 instances in both waves: block-uniform
+  const int b = b0 < B ? b0 : B - 1;
+  if (wave == 1) {
+    record_loader(P, B, b, D, recs, lane);
+    lds_barrier();  // the compute wave's redo decision
+    if (kFastBwd && kRedo && sh_redo) record_loader(P, B, b, D, recs, lane);
+    return;
+  }
+  int bad = 0;
+  backward_sweep<kFastBwd, true>(P, B, b, live, X, D, kout, Kout, bad, recs, lane);
+  const bool redo = kFastBwd && kRedo && __any(bad);
+  if (lane == 0) sh_redo = redo;
+  lds_barrier();
+  if (redo) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
+    int d = 0;
+    backward_sweep<false, true>(P, B, b, live, X, D, kout, Kout, d, recs, lane);
+  }
+}
+
 #if defined(MP_ILQR_PAIR)  // A/B build: a lane pair per instance (measured slower: 391 vs 354 us)
 constexpr int kBwdLanes = 2;
 #else
@@ -732,7 +801,9 @@ __global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, con
   }
 }
 
-// ILQR.jl:72-80: one closed-loop roll out at step size alpha; returns TotalCost.  The rolled
+// ILQR.jl:72-80: one closed-loop roll out at step size alpha; returns TotalCost.  (Staging the
+// per-knot inputs through LDS as the Riccati sweep does measured no gain here, 371 vs 365 us: the
+// one-knot-ahead prefetch already covers the loads under the knot's ~8k-cycle RK4 chain.)  The rolled
 // state stays in registers (Xn is only written), the next knot's reference state, gains and
 // nominal control are loaded one knot ahead, and TotalCost (Cost.jl:1-8) is accumulated in
 // the loop in the reference's order (J = J + stage_i, then + terminal).
@@ -965,9 +1036,14 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
   hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
                      active, dD);
   MP_HIP(ctx, hipGetLastError());
+#if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR)
+  hipLaunchKernelGGL(ilqr_backward_staged_kernel, dim3((B + 63) / 64), dim3(128), sizeof(double) * 2 * ND * 64,
+                     ctx->stream, D, B, dX, dD, active, dk, dK);
+#else
   const int ipb = 64 / kBwdLanes;  // instances per 64-thread block
   hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + ipb - 1) / ipb), dim3(64), 0, ctx->stream, D, B, dX, dD, active, dk,
                      dK);
+#endif
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
   return MP_OK;
