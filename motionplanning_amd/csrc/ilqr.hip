@@ -69,7 +69,11 @@ template <> struct LM<true> {
   static __device__ __forceinline__ double tan(double x, int& b) { return mpj_tan_wide(x, &b); }
   static __device__ __forceinline__ double atan(double x, int&) { return mpj_atan_bl(x); }
   static __device__ __forceinline__ void sincos(double x, double* s, double* c, int& b) { mpj_sincos_wide(x, s, c, &b); }
+#if defined(MP_ILQR_EXPBL)  // A/B: exp with a per-call wave-uniform exact fallback (with FASTFWD: forward 351 vs exact 365 us, roll out 361 vs 277 us)
+  static __device__ __forceinline__ double exp(double x, int&) { return mpj_exp_bl(x); }
+#else
   static __device__ __forceinline__ double exp(double x, int& b) { return mpj_exp_fast(x, &b); }
+#endif
   static __device__ __forceinline__ double atan2(double y, double x, int& b) { return mpj_atan2_fast(y, x, &b); }
 #else
   static __device__ double tan(double x, int& b) { int t = 0; double r = mpj_tan_wide(x, &t); if (t) { b |= 1; if (atomicAdd(&g_nbad, 1) < 8) printf("tan %.17g\n", x); } return r; }
