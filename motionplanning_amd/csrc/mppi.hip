@@ -653,8 +653,13 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   const char* lpr_s = getenv("MPGPU_LPR");  // 1 / 2 forces the layout (tests, comparisons)
   const int lpr_env = lpr_s ? atoi(lpr_s) : 0;
   const int LPR = lpr_env == 1 || lpr_env == 2 ? lpr_env : ((size_t)S * K >= 131072 ? 1 : 2);
-  const int BT = LPR == 1 ? ((size_t)S * ((K + 511) / 512) >= 256 ? 512 : 256)
-                          : ((size_t)S * ((K + 255) / 256) >= 256 ? 512 : 256);
+  int BT = LPR == 1 ? ((size_t)S * ((K + 511) / 512) >= 256 ? 512 : 256)
+                    : ((size_t)S * ((K + 255) / 256) >= 256 ? 512 : 256);
+  // MPGPU_BT = 128 / 256 / 512 forces the block size (A/B runs).  Single scene (64 blocks):
+  // BT 128 (2 waves per CU on 128 CUs) 0.278 ms vs BT 256 (4 waves, one per SIMD, on 64 CUs)
+  // 0.242 ms -- a CU's four SIMDs each holding one wave beat half-filled CUs.
+  const char* bt_s = getenv("MPGPU_BT");
+  if (bt_s && (atoi(bt_s) == 128 || atoi(bt_s) == 256 || atoi(bt_s) == 512)) BT = atoi(bt_s);
   const int RPBh = BT / LPR;
   const int nb = (K + RPBh - 1) / RPBh;
   const int pstride = 4 + 2 * H;
@@ -729,6 +734,10 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
     MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<512, 1>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<128, 2>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
+    MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<128, 1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
     attr_set = true;
   }
   // deferred final rollout: snapshot ring slot of this call, free once the final rollout of
@@ -762,7 +771,11 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   hipEvent_t t_start, t_stop;
   mp_time_pair(ctx, &t_start, &t_stop);
   const dim3 grd(S * nb);
-  if (LPR == 1 && BT == 512)
+  if (LPR == 2 && BT == 128)
+    hipExtLaunchKernelGGL(mppi_plan_kernel<128, 2>, grd, dim3(128), shmem, ctx->stream, t_start, t_stop, 0, D, A);
+  else if (LPR == 1 && BT == 128)
+    hipExtLaunchKernelGGL(mppi_plan_kernel<128, 1>, grd, dim3(128), shmem, ctx->stream, t_start, t_stop, 0, D, A);
+  else if (LPR == 1 && BT == 512)
     hipExtLaunchKernelGGL(mppi_plan_kernel<512, 1>, grd, dim3(512), shmem, ctx->stream, t_start, t_stop, 0, D, A);
   else if (LPR == 1)
     hipExtLaunchKernelGGL(mppi_plan_kernel<256, 1>, grd, dim3(256), shmem, ctx->stream, t_start, t_stop, 0, D, A);
