@@ -51,6 +51,20 @@ constexpr bool kFast = true;
 // sweep (355 vs 382 us).  The derivative kernel (405,504 threads, lanes of a wave take the same
 // libm branches) runs the exact routines in 154 us vs 296 us, and the one-thread-per-instance
 // forward trial / roll out (64 waves, latency-bound: fewer instructions win) in 361 vs 690 us.
+// A/B (-DMP_ILQR_FASTSC): the forward trial / roll out's four RK4 stage sincos on the
+// straight-line core (rk4_ilp, independent of each other) with an exact redo for arguments out
+// of range.  Measured slower: forward 386 vs 361 us, roll out 356 vs 276 us (a lone wave is
+// issue-limited: the straight-line core's extra instructions cost more than the overlap gains).
+#if defined(MP_ILQR_NOQUAD) || defined(MP_ILQR_FASTFWD)
+constexpr bool kFwdQuad = false;
+#else
+constexpr bool kFwdQuad = true;  // ilqr_forward_quad_kernel: a lane quad per instance
+#endif
+#if defined(MP_ILQR_FASTSC)
+constexpr bool kFastSC = true;
+#else
+constexpr bool kFastSC = false;
+#endif
 #if defined(MP_ILQR_FASTFWD)  // A/B build (measured slower: forward 689 vs 363 us, roll out 341 vs 277 us)
 constexpr bool kFastDeriv = false, kFastBwd = kFast, kFastFwd = kFast;
 #else
@@ -128,6 +142,34 @@ __device__ __forceinline__ void rk4(const double* s, double ax, const UPre& q, d
 #pragma unroll
   for (int i = 0; i < 4; i++) x4[i] = s[i] + dT * k3[i];
   dyn<F>(x4, ax, q, k4, bad);
+#pragma unroll
+  for (int i = 0; i < 4; i++) o[i] = 1.0 / 6 * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]) * dT + s[i];
+}
+
+// RK4Integration with the four stage headings computed first.  The stage speed and heading
+// (dyn's d[2] = ax, d[3] = s2·cb·tδ/L) never depend on a sine or cosine, so the four stage
+// sincos are independent of each other: with the straight-line core (SC = true) the scheduler
+// overlaps them instead of running four dependent libm chains.  The same operations on the
+// same operands as rk4, so the same bits.
+template <bool SC>
+__device__ __forceinline__ void rk4_ilp(const double* s, double ax, const UPre& q, double dT, double* o, int& bad) {
+  const double la = 1.56, lb = 1.64;
+  const double k1_3 = s[2] * q.cb * q.tdl / (la + lb);
+  const double x2_2 = s[2] + dT / 2 * ax, x2_3 = s[3] + dT / 2 * k1_3;
+  const double k2_3 = x2_2 * q.cb * q.tdl / (la + lb);
+  const double x3_2 = s[2] + dT / 2 * ax, x3_3 = s[3] + dT / 2 * k2_3;
+  const double k3_3 = x3_2 * q.cb * q.tdl / (la + lb);
+  const double x4_2 = s[2] + dT * ax, x4_3 = s[3] + dT * k3_3;
+  const double k4_3 = x4_2 * q.cb * q.tdl / (la + lb);
+  double s1, c1, s2, c2, s3, c3, s4, c4;
+  LM<SC>::sincos(s[3] + q.beta, &s1, &c1, bad);
+  LM<SC>::sincos(x2_3 + q.beta, &s2, &c2, bad);
+  LM<SC>::sincos(x3_3 + q.beta, &s3, &c3, bad);
+  LM<SC>::sincos(x4_3 + q.beta, &s4, &c4, bad);
+  const double k1[4] = {s[2] * c1, s[2] * s1, ax, k1_3};
+  const double k2[4] = {x2_2 * c2, x2_2 * s2, ax, k2_3};
+  const double k3[4] = {x3_2 * c3, x3_2 * s3, ax, k3_3};
+  const double k4[4] = {x4_2 * c4, x4_2 * s4, ax, k4_3};
 #pragma unroll
   for (int i = 0; i < 4; i++) o[i] = 1.0 / 6 * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]) * dT + s[i];
 }
@@ -811,7 +853,7 @@ __global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, con
 // state stays in registers (Xn is only written), the next knot's reference state, gains and
 // nominal control are loaded one knot ahead, and TotalCost (Cost.jl:1-8) is accumulated in
 // the loop in the reference's order (J = J + stage_i, then + terminal).
-template <bool F>
+template <bool F, bool SC = F>
 __device__ double forward_trial(const IlqrDev& P, const double* X, const double* U, const double* k,
                                 const double* Kg, double alpha, double* Xn, double* Un, bool wr, int& bad) {
   const int N = P.N;
@@ -853,7 +895,7 @@ __device__ double forward_trial(const IlqrDev& P, const double* X, const double*
     J = J + stage<F>(P.variant, x, u, bad);
     const UPre q = upre<F>(u[1], bad);
     double xn[4];
-    rk4<F>(x, u[0], q, P.dT, xn, bad);
+    rk4_ilp<SC>(x, u[0], q, P.dT, xn, bad);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       x[r] = xn[r];
@@ -872,6 +914,103 @@ __device__ double forward_trial(const IlqrDev& P, const double* X, const double*
   return J + terminal(P.variant, x);
 }
 
+// Broadcast lane j of each quad to the quad (DPP quad_perm [j,j,j,j]).
+template <int J>
+__device__ __forceinline__ double quad_bcast(double v) {
+  constexpr int c = J * 85;
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), c, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), c, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// The forward trial (ILQR.jl:72-80) on a QUAD of lanes per instance (sub = lane & 3), exact
+// FDLIBM.  The knot's independent transcendentals are spread over the quad as one instruction
+// stream with lane-selected operands: the four sigmoid exponentials of StageCost (ax: c1, c2;
+// δ: c1, c2; Cost.jl:42-49) and the four RK4 stage sincos (the stage headings never depend on a
+// sine or cosine, see rk4_ilp); each lane computes one of each, four DPP broadcasts share them.
+// tan/atan/sincos(β) of the control run on all four lanes.  Same operations on the same
+// operands as forward_trial: bit-identical.
+__device__ double forward_trial_quad(const IlqrDev& P, const double* X, const double* U, const double* k,
+                                     const double* Kg, double alpha, double* Xn, double* Un, bool wr, int sub) {
+  const int N = P.N;
+  const double la = 1.56, lb = 1.64, dT = P.dT;
+  int bad = 0;
+  double x[4] = {X[0], X[1], X[2], X[3]};
+  if (wr && sub == 0)
+#pragma unroll
+    for (int r = 0; r < 4; r++) Xn[r] = x[r];
+  double J = 0.0;
+  for (int i = 0; i < N - 1; i++) {
+    double xr[4], Kr[8], kr[2], ur[2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) xr[r] = X[4 * i + r];
+#pragma unroll
+    for (int r = 0; r < 8; r++) Kr[r] = Kg[8 * i + r];
+    kr[0] = k[2 * i]; kr[1] = k[2 * i + 1];
+    ur[0] = U[2 * i]; ur[1] = U[2 * i + 1];
+    double dx[4], u[2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) dx[r] = x[r] - xr[r];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      double acc = Kr[2 * 0 + r] * dx[0];
+#pragma unroll
+      for (int c = 1; c < 4; c++) acc = acc + Kr[2 * c + r] * dx[c];
+      u[r] = (ur[r] + alpha * kr[r]) + acc;
+    }
+    if (wr && sub < 2) Un[2 * i + sub] = u[sub];
+    // StageCost: sigmoid_boundary(ax; -2, 2) on subs 0/1, sigmoid_boundary(δ; -π/6, π/6) on 2/3
+    {
+      const double slope = 10, mag = 100;
+      const double st = sub < 2 ? u[0] : u[1];
+      const double mn = sub < 2 ? -2.0 : -MPJ_PI / 6, mx = sub < 2 ? 2.0 : MPJ_PI / 6;
+      const double ci = (sub & 1) ? 1 / (1 + mpj_exp(slope * (st - mn))) : 1 / (1 + mpj_exp(-slope * (st - mx)));
+      const double a1 = quad_bcast<0>(ci), a2 = quad_bcast<1>(ci), d1 = quad_bcast<2>(ci), d2 = quad_bcast<3>(ci);
+      const double sa = mag * (a1 + a2), sd = mag * (d1 + d2);
+      J = J + stage_pre(P.variant, x, u[0], u[1], sd, sa);
+    }
+    // RK4Integration with the stage sincos spread over the quad
+    const UPre q = upre<false>(u[1], bad);
+    const double ax = u[0];
+    const double k1_3 = x[2] * q.cb * q.tdl / (la + lb);
+    const double x2_2 = x[2] + dT / 2 * ax, x2_3 = x[3] + dT / 2 * k1_3;
+    const double k2_3 = x2_2 * q.cb * q.tdl / (la + lb);
+    const double x3_2 = x[2] + dT / 2 * ax, x3_3 = x[3] + dT / 2 * k2_3;
+    const double k3_3 = x3_2 * q.cb * q.tdl / (la + lb);
+    const double x4_2 = x[2] + dT * ax, x4_3 = x[3] + dT * k3_3;
+    const double k4_3 = x4_2 * q.cb * q.tdl / (la + lb);
+    const double hd = sub == 0 ? x[3] : sub == 1 ? x2_3 : sub == 2 ? x3_3 : x4_3;
+    double sn, cs;
+    mpj_sincos(hd + q.beta, &sn, &cs);
+    const double s1 = quad_bcast<0>(sn), c1 = quad_bcast<0>(cs), s2 = quad_bcast<1>(sn), c2 = quad_bcast<1>(cs);
+    const double s3 = quad_bcast<2>(sn), c3 = quad_bcast<2>(cs), s4 = quad_bcast<3>(sn), c4 = quad_bcast<3>(cs);
+    const double k1[4] = {x[2] * c1, x[2] * s1, ax, k1_3};
+    const double k2[4] = {x2_2 * c2, x2_2 * s2, ax, k2_3};
+    const double k3[4] = {x3_2 * c3, x3_2 * s3, ax, k3_3};
+    const double k4[4] = {x4_2 * c4, x4_2 * s4, ax, k4_3};
+    double xn[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) xn[r] = 1.0 / 6 * (k1[r] + 2 * k2[r] + 2 * k3[r] + k4[r]) * dT + x[r];
+#pragma unroll
+    for (int r = 0; r < 4; r++) x[r] = xn[r];
+    if (wr) Xn[4 * (i + 1) + sub] = xn[sub];
+  }
+  if (wr && sub < 2) Un[2 * (N - 1) + sub] = 0.0;
+  return J + terminal(P.variant, x);
+}
+
+__global__ __launch_bounds__(64) void ilqr_forward_quad_kernel(IlqrDev P, int B, const double* X, const double* U,
+                                                               const double* k, const double* Kg, const double* alpha,
+                                                               double* Xn, double* Un, double* Jn) {
+  const int b0 = blockIdx.x * 16 + (threadIdx.x >> 2), sub = threadIdx.x & 3;
+  const bool live = b0 < B;
+  const size_t b = live ? b0 : B - 1;  // all lanes active (DPP quads); tail quads store nothing
+  const size_t N = P.N;
+  const double J = forward_trial_quad(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
+                                      alpha[b], Xn + b * N * 4, Un + b * N * 2, live, sub);
+  if (live && sub == 0) Jn[b] = J;
+}
+
 __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                           const double* k, const double* Kg, const double* alpha,
                                                           double* Xn, double* Un, double* Jn) {
@@ -880,9 +1019,9 @@ __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, cons
   const size_t b = live ? b0 : B - 1;  // all lanes active (ballot-based libm); tail lanes store nothing
   const size_t N = P.N;
   int bad = 0;
-  double J = forward_trial<kFastFwd>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
-                                    alpha[b], Xn + b * N * 4, Un + b * N * 2, live, bad);
-  if (kFastFwd && kRedo && __any(bad)) {  // redo the wave's trials with the exact libm
+  double J = forward_trial<kFastFwd, kFastSC>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2,
+                                             Kg + b * (N - 1) * 8, alpha[b], Xn + b * N * 4, Un + b * N * 2, live, bad);
+  if ((kFastFwd || kFastSC) && kRedo && __any(bad)) {  // redo the wave's trials with the exact libm
     int d = 0;
     J = forward_trial<false>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8, alpha[b],
                              Xn + b * N * 4, Un + b * N * 2, live, d);
@@ -957,7 +1096,7 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
 }
 
 // Initial guess roll out (ILQR.jl:31-37) with TotalCost accumulated in order.
-template <bool F>
+template <bool F, bool SC = F>
 __device__ __forceinline__ double rollout_one(const IlqrDev& P, const double* x0, const double* Ub, double* Xb,
                                               bool live, int& bad) {
   const size_t N = P.N;
@@ -971,7 +1110,7 @@ __device__ __forceinline__ double rollout_one(const IlqrDev& P, const double* x0
     Jb = Jb + stage<F>(P.variant, x, u, bad);
     const UPre q = upre<F>(u[1], bad);
     double xn[4];
-    rk4<F>(x, u[0], q, P.dT, xn, bad);
+    rk4_ilp<SC>(x, u[0], q, P.dT, xn, bad);
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       x[r] = xn[r];
@@ -988,8 +1127,8 @@ __global__ __launch_bounds__(64) void ilqr_rollout_kernel(IlqrDev P, int B, cons
   const size_t b = live ? b0 : B - 1;  // all lanes active (ballot-based libm)
   const size_t N = P.N;
   int bad = 0;
-  double Jb = rollout_one<kFastFwd>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, bad);
-  if (kFastFwd && kRedo && __any(bad)) {
+  double Jb = rollout_one<kFastFwd, kFastSC>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, bad);
+  if ((kFastFwd || kFastSC) && kRedo && __any(bad)) {
     int d = 0;
     Jb = rollout_one<false>(P, x0 + 4 * b, U + b * N * 2, X + b * N * 4, live, d);
   }
@@ -1120,8 +1259,12 @@ int mp_ilqr_forward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const doubl
   double* dJ = mp_alloc_out(ctx, WS_IO7, Jnew, (size_t)B, &st);
   if (st) return st;
   mp_time_begin(ctx);
-  hipLaunchKernelGGL(ilqr_forward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, dX, dU, dk, dK, da,
-                     dXn, dUn, dJ);
+  if (kFwdQuad)
+    hipLaunchKernelGGL(ilqr_forward_quad_kernel, dim3((B + 15) / 16), dim3(64), 0, ctx->stream, D, B, dX, dU, dk, dK,
+                       da, dXn, dUn, dJ);
+  else
+    hipLaunchKernelGGL(ilqr_forward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, dX, dU, dk, dK, da,
+                       dXn, dUn, dJ);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
   if ((st = mp_download(ctx, Xnew, (const double*)dXn, 4 * N * B))) return st;
@@ -1150,8 +1293,12 @@ int mp_ilqr_forward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const d
   if (st) return st;
   MP_CHECK(ctx, X && U && k && Kg && alpha && Xnew && Unew && Jnew, "required pointer is NULL");
   mp_time_begin(ctx);
-  hipLaunchKernelGGL(ilqr_forward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, X, U, k, Kg, alpha,
-                     Xnew, Unew, Jnew);
+  if (kFwdQuad)
+    hipLaunchKernelGGL(ilqr_forward_quad_kernel, dim3((B + 15) / 16), dim3(64), 0, ctx->stream, D, B, X, U, k, Kg,
+                       alpha, Xnew, Unew, Jnew);
+  else
+    hipLaunchKernelGGL(ilqr_forward_kernel, dim3((B + 63) / 64), dim3(64), 0, ctx->stream, D, B, X, U, k, Kg, alpha,
+                       Xnew, Unew, Jnew);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
   return MP_OK;
