@@ -369,6 +369,42 @@ __device__ __forceinline__ void pinv2(const double* M, double* Pm, int& bad) {
   Pm[3] = -st * i1 * sp + ct * i2 * cp;
 }
 
+// Exchange a double with the other lane of the pair (DPP quad_perm [1,0,3,2]).
+__device__ __forceinline__ double dswap(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// pinv2 on a lane pair: the two square roots, the two atan2, the two sincos and the two
+// reciprocals of the closed-form SVD are the same operations on lane-selected operands (side 0
+// the first of each, side 1 the second), exchanged with one DPP swap each.  Every value is
+// computed exactly as in pinv2 (same operands, same operation), so Pm is bit-identical.
+template <bool FT>
+__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int side, int& bad) {
+  const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
+  const double a = side ? F : E, c = side ? G : H;
+  const double r0 = mpj_sqrt(a * a + c * c), r1 = dswap(r0);
+  const double Q = side ? r1 : r0, R = side ? r0 : r1;
+  const double sx = Q + R, sy = Q - R;
+  const double t0 = LM<FT>::atan2(side ? H : G, side ? E : F, bad), t1 = dswap(t0);
+  const double a1 = side ? t1 : t0, a2 = side ? t0 : t1;
+  const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
+  double sn, cs;
+  LM<FT>::sincos(side ? ph : th, &sn, &cs, bad);
+  const double so = dswap(sn), co = dswap(cs);
+  const double st = side ? so : sn, ct = side ? co : cs, sp = side ? sn : so, cp = side ? cs : co;
+  const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
+  const double tol = 4.440892098500626e-16 * smax;
+  const double sv = side ? sy : sx;
+  const double i0 = __builtin_fabs(sv) > tol ? 1.0 / sv : 0.0, io = dswap(i0);
+  const double i1 = side ? io : i0, i2 = side ? i0 : io;
+  Pm[0] = ct * i1 * cp - st * i2 * sp;
+  Pm[1] = ct * i1 * sp + st * i2 * cp;
+  Pm[2] = -st * i1 * cp - ct * i2 * sp;
+  Pm[3] = -st * i1 * sp + ct * i2 * cp;
+}
+
 // ILQR.jl:46-67 for instance b: one thread per instance (the sweep is a serial chain in j).
 // The derivative record of knot j-1 is loaded while knot j is processed (coalesced: the
 // records are component-major, instance fastest), so the chain never waits on memory.
@@ -377,10 +413,10 @@ __device__ __forceinline__ void pinv2(const double* M, double* Pm, int& bad) {
 // loads stay outstanding across it), and a compiler barrier for memory.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <bool FT, bool STAGED = false>
+template <bool FT, bool STAGED = false, bool PP = false>
 __device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, bool live, const double* X,
                                                const double* D, double* kout, double* Kout, int& bad,
-                                               const double* lds = nullptr, int lane = 0) {
+                                               const double* lds = nullptr, int lane = 0, int side = 0) {
   const int N = P.N;
   const double e = P.eps;
   const int V = P.variant;
@@ -502,7 +538,8 @@ __device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, b
         for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * A[k * 4 + c];
         Qux[4 * i + c] = lux[4 * i + c] + acc;
       }
-    pinv2<FT>(Quu, Pm, bad);
+    if (PP) pinv2_pair<FT>(Quu, Pm, side, bad);  // the lane pair splits the pinv's libm calls
+    else pinv2<FT>(Quu, Pm, bad);
     double kk[2], KK[8];
 #pragma unroll
     for (int i = 0; i < 2; i++) kk[i] = (-Pm[2 * i + 0]) * Qu[0] + (-Pm[2 * i + 1]) * Qu[1];
@@ -510,7 +547,7 @@ __device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, b
     for (int i = 0; i < 2; i++)
 #pragma unroll
       for (int c = 0; c < 4; c++) KK[4 * i + c] = (-Pm[2 * i + 0]) * Qux[0 * 4 + c] + (-Pm[2 * i + 1]) * Qux[1 * 4 + c];
-    if (live) {
+    if (live && side == 0) {
       double* ko = kout + ((size_t)b * (N - 1) + j) * 2;
       double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8;
       ko[0] = kk[0];
@@ -562,42 +599,6 @@ __device__ __forceinline__ void record_loader(const IlqrDev& P, int B, int b, co
     }
     lds_barrier();
   }
-}
-
-// Exchange a double with the other lane of the pair (DPP quad_perm [1,0,3,2]).
-__device__ __forceinline__ double dswap(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
-}
-
-// pinv2 on a lane pair: the two square roots, the two atan2, the two sincos and the two
-// reciprocals of the closed-form SVD are the same operations on lane-selected operands (side 0
-// the first of each, side 1 the second), exchanged with one DPP swap each.  Every value is
-// computed exactly as in pinv2 (same operands, same operation), so Pm is bit-identical.
-template <bool FT>
-__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int side, int& bad) {
-  const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
-  const double a = side ? F : E, c = side ? G : H;
-  const double r0 = mpj_sqrt(a * a + c * c), r1 = dswap(r0);
-  const double Q = side ? r1 : r0, R = side ? r0 : r1;
-  const double sx = Q + R, sy = Q - R;
-  const double t0 = LM<FT>::atan2(side ? H : G, side ? E : F, bad), t1 = dswap(t0);
-  const double a1 = side ? t1 : t0, a2 = side ? t0 : t1;
-  const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
-  double sn, cs;
-  LM<FT>::sincos(side ? ph : th, &sn, &cs, bad);
-  const double so = dswap(sn), co = dswap(cs);
-  const double st = side ? so : sn, ct = side ? co : cs, sp = side ? sn : so, cp = side ? cs : co;
-  const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
-  const double tol = 4.440892098500626e-16 * smax;
-  const double sv = side ? sy : sx;
-  const double i0 = __builtin_fabs(sv) > tol ? 1.0 / sv : 0.0, io = dswap(i0);
-  const double i1 = side ? io : i0, i2 = side ? i0 : io;
-  Pm[0] = ct * i1 * cp - st * i2 * sp;
-  Pm[1] = ct * i1 * sp + st * i2 * cp;
-  Pm[2] = -st * i1 * cp - ct * i2 * sp;
-  Pm[3] = -st * i1 * sp + ct * i2 * cp;
 }
 
 // ILQR.jl:46-67 on a LANE PAIR per instance (side = lane & 1): the pair splits every matrix
@@ -795,32 +796,46 @@ __device__ __forceinline__ void backward_sweep_pair(const IlqrDev& P, int B, int
 // instances.  The single-wave sweep spent ~2 us of its ~3.6 us per knot waiting on the knot's
 // 58 record loads (the compiler sinks prefetches to cut register pressure); here the compute
 // wave reads them from LDS and the loader wave keeps the next knot's loads in flight.
-__global__ __launch_bounds__(128) void ilqr_backward_staged_kernel(IlqrDev P, int B, const double* X,
-                                                                  const double* D, const int* active, double* kout,
-                                                                  double* Kout) {
+template <int LANES>
+__global__ __launch_bounds__(64 * (LANES + 1)) void ilqr_backward_staged_kernel(IlqrDev P, int B, const double* X,
+                                                                               const double* D, const int* active,
+                                                                               double* kout, double* Kout) {
   extern __shared__ double recs[];  // [2][ND][64]
   __shared__ int sh_redo;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int b0 = blockIdx.x * 64 + lane;
+  const int tid = threadIdx.x;
+  const bool loader = tid >= 64 * LANES;  // the last wave
+  const int il = loader ? tid - 64 * LANES : tid / LANES;  // instance within the block's 64
+  const int side = LANES == 2 ? (tid & 1) : 0;
+  const int b0 = blockIdx.x * 64 + il;
   const bool live = b0 < B && (!active || active[b0]);
-  if (__all(!live)) return;  // the same 64 instances in both waves: block-uniform
+  if (!__syncthreads_or(live)) return;  // block-uniform
   const int b = b0 < B ? b0 : B - 1;
-  if (wave == 1) {
-    record_loader(P, B, b, D, recs, lane);
-    lds_barrier();  // the compute wave's redo decision
-    if (kFastBwd && kRedo && sh_redo) record_loader(P, B, b, D, recs, lane);
+  if (tid == 0) sh_redo = 0;  // read only after the sweep's barriers
+  if (loader) {
+    record_loader(P, B, b, D, recs, il);
+    lds_barrier();  // the compute waves' redo decision
+    if (kFastBwd && kRedo && sh_redo) record_loader(P, B, b, D, recs, il);
     return;
   }
   int bad = 0;
-  backward_sweep<kFastBwd, true>(P, B, b, live, X, D, kout, Kout, bad, recs, lane);
-  const bool redo = kFastBwd && kRedo && __any(bad);
-  if (lane == 0) sh_redo = redo;
-  lds_barrier();
-  if (redo) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
+  backward_sweep<kFastBwd, true, LANES == 2>(P, B, b, live, X, D, kout, Kout, bad, recs, il, side);
+  if (kFastBwd && kRedo && __any(bad) && (tid & 63) == 0) sh_redo = 1;  // any compute wave
+  lds_barrier();  // matches the loader's redo-decision barrier
+  if (sh_redo) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
     int d = 0;
-    backward_sweep<false, true>(P, B, b, live, X, D, kout, Kout, d, recs, lane);
+    backward_sweep<false, true, LANES == 2>(P, B, b, live, X, D, kout, Kout, d, recs, il, side);
   }
 }
+
+// Two compute lanes per instance: the whole sweep runs on both (the matrix products need no
+// exchange) except the closed-form pinv, whose sqrt / atan2 / sincos / reciprocal pairs are
+// split over the pair (pinv2_pair).  Measured: 247 us vs 294 us for one lane (the pinv's libm
+// chains dominate a lone wave's issue), vs 566 us when the matrix rows were split as well.
+#if defined(MP_ILQR_SINGLEPINV)
+constexpr int kBwdStagedLanes = 1;
+#else
+constexpr int kBwdStagedLanes = 2;
+#endif
 
 #if defined(MP_ILQR_PAIR)  // A/B build: a lane pair per instance (measured slower: 391 vs 354 us)
 constexpr int kBwdLanes = 2;
@@ -1180,8 +1195,9 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
                      active, dD);
   MP_HIP(ctx, hipGetLastError());
 #if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR)
-  hipLaunchKernelGGL(ilqr_backward_staged_kernel, dim3((B + 63) / 64), dim3(128), sizeof(double) * 2 * ND * 64,
-                     ctx->stream, D, B, dX, dD, active, dk, dK);
+  hipLaunchKernelGGL(ilqr_backward_staged_kernel<kBwdStagedLanes>, dim3((B + 63) / 64),
+                     dim3(64 * (kBwdStagedLanes + 1)), sizeof(double) * 2 * ND * 64, ctx->stream, D, B, dX, dD,
+                     active, dk, dK);
 #else
   const int ipb = 64 / kBwdLanes;  // instances per 64-thread block
   hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + ipb - 1) / ipb), dim3(64), 0, ctx->stream, D, B, dX, dD, active, dk,
