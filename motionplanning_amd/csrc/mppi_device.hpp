@@ -41,11 +41,20 @@ __device__ __forceinline__ double pair_swap(double v) {
 // ---------------------------------------------------------------- dynamics
 // VehicleDynamics for a lane pair.  side = lane & 1 (0: front tire, 1: rear).
 // atab: the mpj_atan_tab range table (LDS).
+__device__ __forceinline__ void dyn_pair_sc(const double* x, double sr, double ax, double* d, int side,
+                                            const double* atab, double sp, double cp);
 __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side, const double* atab) {
+  double sp, cp;
+  mpj_sincos_bl(x[4], &sp, &cp);
+  dyn_pair_sc(x, sr, ax, d, side, atab, sp, cp);
+}
+// dyn_pair with sin/cos(ψ) supplied (rollout_pair evaluates both RK2 stages' in one call)
+__device__ __forceinline__ void dyn_pair_sc(const double* x, double sr, double ax, double* d, int side,
+                                            const double* atab, double sp, double cp) {
   const double la = 1.56, lb = 1.64, M = 2020.0, Izz = 4095.0, g = 9.81, mu = 0.8;
   const double KFZF = 1018.28 / 2, KFZR = 963.34 / 2, KFZX = 186.22;
   const double B = -10.4 / mu, C = 1.3, E = 0.1556;
-  const double v = x[2], r = x[3], psi = x[4], ux = x[5], sa = x[6];
+  const double v = x[2], r = x[3], ux = x[5], sa = x[6];
   const double t = (ax - r * v) * KFZX;
   // front: 2*(KFZF*g - t);  rear: 2*(KFZR*g + t)   (vehicledynamics.jl:30-31)
   const double FZ = 2 * ((side ? KFZR : KFZF) * g + (side ? t : -t));
@@ -56,8 +65,6 @@ __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, 
   const double FYo = pair_swap(FY);
   const double FY1 = side ? FYo : FY, FY2 = side ? FY : FYo;
   const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);  // (:40-42)
-  double sp, cp;
-  mpj_sincos_bl(psi, &sp, &cp);
   d[0] = uxc * cp - v * sp;
   d[1] = uxc * sp + v * cp;
   // the two force divisions (:45-46) split across the pair: even lane (FY1+FY2)/M, odd lane
@@ -141,17 +148,20 @@ __device__ __forceinline__ double obstacle_cost(const MppiDev& P, const double* 
 // BoundEvaluation, MPPIUtils.jl:135-151 (branch-free, same accumulation order)
 __device__ __forceinline__ double bound_cost(const MppiDev& P, const double* x, int* ok) {
   int viol = 0;
-  double c = 0.0;
 #pragma unroll
-  for (int i = 0; i < 7; i++) {
-    const int lo = x[i] < P.XL[i], hi = x[i] > P.XU[i];
-    viol |= lo | hi;
-    const double vl = c + P.slack * __builtin_fabs(x[i] - P.XL[i]);
-    c = lo ? vl : c;
-    const double vh = c + P.slack * __builtin_fabs(x[i] - P.XU[i]);
-    c = hi ? vh : c;
-  }
+  for (int i = 0; i < 7; i++) viol |= (x[i] < P.XL[i]) | (x[i] > P.XU[i]);
   *ok &= !viol;
+  double c = 0.0;
+  if (__any(viol)) {  // wave-uniform: with no violation in the wave every lane's sum is exactly 0.0
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      const int lo = x[i] < P.XL[i], hi = x[i] > P.XU[i];
+      const double vl = c + P.slack * __builtin_fabs(x[i] - P.XL[i]);
+      c = lo ? vl : c;
+      const double vh = c + P.slack * __builtin_fabs(x[i] - P.XU[i]);
+      c = hi ? vh : c;
+    }
+  }
   return c;
 }
 
@@ -269,12 +279,24 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     }
     const double pc = run_cost(x, u[0], u[1]);
     double k1[7], k2[7], x2[7];
-    if (LPR == 2) dyn_pair(x, u[0], u[1], k1, side, atab);
-    else dyn_lane(x, u[0], u[1], k1, atab);
+    if (LPR == 2) {
+      // sin/cos(ψ) of both RK2 stages in ONE call on the pair: the second stage's heading
+      // x2[4] = x[4] + k1[4]·dt with k1[4] = r = x[3] needs no tyre force, so the even lane
+      // evaluates stage 1's and the odd lane stage 2's, then they swap (same operands, same bits)
+      const double psi2 = x[4] + x[3] * P.dt;
+      double sn, cs;
+      mpj_sincos_bl(side ? psi2 : x[4], &sn, &cs);
+      const double so = pair_swap(sn), co = pair_swap(cs);
+      dyn_pair_sc(x, u[0], u[1], k1, side, atab, side ? so : sn, side ? co : cs);
 #pragma unroll
-    for (int i = 0; i < 7; i++) x2[i] = x[i] + k1[i] * P.dt;
-    if (LPR == 2) dyn_pair(x2, u[0], u[1], k2, side, atab);
-    else dyn_lane(x2, u[0], u[1], k2, atab);
+      for (int i = 0; i < 7; i++) x2[i] = x[i] + k1[i] * P.dt;
+      dyn_pair_sc(x2, u[0], u[1], k2, side, atab, side ? sn : so, side ? cs : co);
+    } else {
+      dyn_lane(x, u[0], u[1], k1, atab);
+#pragma unroll
+      for (int i = 0; i < 7; i++) x2[i] = x[i] + k1[i] * P.dt;
+      dyn_lane(x2, u[0], u[1], k2, atab);
+    }
 #pragma unroll
     for (int i = 0; i < 7; i++) x[i] = x[i] + P.dt * (k1[i] + k2[i]) / 2;
     double cj = pc + cb + cc;
