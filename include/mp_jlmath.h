@@ -639,9 +639,11 @@ MPJ_FN double mpj_atan_tab(double x, const double* tab) {
   const double s2 = w * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT9, aT7), aT5), aT3), aT1);
   const double r = hi - ((ax * (s1 + s2) - lo) - ax);
   const double rs = mpj_flip(r, hx & 0x80000000u);
+  /* FDLIBM's |x| < 2^-27 case needs no select here: with id 0 (ax = a) the polynomial term is
+   * below half an ulp of a, so r == a exactly and the flip returns x (±0 and subnormals
+   * included; tests/test_jlmath.py).  |x| >= 2^66 keeps its select (±Inf would give 0·Inf). */
   const double big = 1.57079632679489655800e+00 + 6.12323399573676603587e-17;
-  const double rb = MPJ_SEL(ix >= 0x44100000u && x == x, MPJ_SEL(hx >> 31, -big, big), rs);
-  return MPJ_SEL(ix < 0x3e400000u, x, rb);
+  return MPJ_SEL(ix >= 0x44100000u && x == x, MPJ_SEL(hx >> 31, -big, big), rs);
 }
 
 /* mpj_atan2 with the branch-free atan core (bit-identical: mpj_atan_bl == mpj_atan). */

@@ -41,41 +41,57 @@ __device__ __forceinline__ double pair_swap(double v) {
 // ---------------------------------------------------------------- dynamics
 // VehicleDynamics for a lane pair.  side = lane & 1 (0: front tire, 1: rear).
 // atab: the mpj_atan_tab range table (LDS).
-__device__ __forceinline__ void dyn_pair_sc(const double* x, double sr, double ax, double* d, int side,
-                                            const double* atab, double sp, double cp);
-__device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side, const double* atab) {
-  double sp, cp;
-  mpj_sincos_bl(x[4], &sp, &cp);
-  dyn_pair_sc(x, sr, ax, d, side, atab, sp, cp);
+//
+// Lane constants of the pair, fixed for a rollout (kept in registers instead of selected every
+// call): the axle load constant, the sign of t, the slip lever arm, the force-division operands.
+struct PairK {
+  double kfz, tsg, lr, cown, cother, div;
+};
+__device__ __forceinline__ PairK pair_k(int side) {
+  const double la = 1.56, lb = 1.64, M = 2020.0, Izz = 4095.0;
+  const double KFZF = 1018.28 / 2, KFZR = 963.34 / 2;
+  PairK k;
+  k.kfz = side ? KFZR : KFZF;
+  k.tsg = side ? 1.0 : -1.0;
+  k.lr = side ? -lb : la;
+  k.cown = side ? -lb : 1.0;
+  k.cother = side ? la : 1.0;
+  k.div = side ? Izz : M;
+  return k;
 }
 // dyn_pair with sin/cos(ψ) supplied (rollout_pair evaluates both RK2 stages' in one call)
 __device__ __forceinline__ void dyn_pair_sc(const double* x, double sr, double ax, double* d, int side,
-                                            const double* atab, double sp, double cp) {
-  const double la = 1.56, lb = 1.64, M = 2020.0, Izz = 4095.0, g = 9.81, mu = 0.8;
-  const double KFZF = 1018.28 / 2, KFZR = 963.34 / 2, KFZX = 186.22;
+                                            const double* atab, double sp, double cp, const PairK& pk) {
+  const double g = 9.81, mu = 0.8, KFZX = 186.22;
   const double B = -10.4 / mu, C = 1.3, E = 0.1556;
   const double v = x[2], r = x[3], ux = x[5], sa = x[6];
   const double t = (ax - r * v) * KFZX;
-  // front: 2*(KFZF*g - t);  rear: 2*(KFZR*g + t)   (vehicledynamics.jl:30-31)
-  const double FZ = 2 * ((side ? KFZR : KFZF) * g + (side ? t : -t));
+  // front: 2*(KFZF*g - t);  rear: 2*(KFZR*g + t)   (vehicledynamics.jl:30-31); t·(∓1) is exact
+  const double FZ = 2 * (pk.kfz * g + t * pk.tsg);
   // front: (v + la*r) ... - sa;  rear: (v - lb*r) ... [(-lb)*r == -(lb*r) exactly]  (:32-33)
-  const double alpha = mpj_atan_tab((v + (side ? -lb : la) * r) / (ux + 0.01), atab) - (side ? 0.0 : sa);
+  const double alpha = mpj_atan_tab((v + pk.lr * r) / (ux + 0.01), atab) - (side ? 0.0 : sa);
   const double X1 = B * alpha;
   const double FY = mu * FZ * 1.0 * mpj_sin_bl(C * mpj_atan_tab(X1 - E * (X1 - mpj_atan_tab(X1, atab)), atab));  // (:35-38)
   const double FYo = pair_swap(FY);
-  const double FY1 = side ? FYo : FY, FY2 = side ? FY : FYo;
   const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);  // (:40-42)
   d[0] = uxc * cp - v * sp;
   d[1] = uxc * sp + v * cp;
   // the two force divisions (:45-46) split across the pair: even lane (FY1+FY2)/M, odd lane
-  // (FY1*la - FY2*lb)/Izz, exchanged with one DPP swap (same operands, same bits)
-  const double q = (side ? FY1 * la - FY2 * lb : FY1 + FY2) / (side ? Izz : M);
+  // (FY1*la - FY2*lb)/Izz, exchanged with one DPP swap.  The numerator is own·cown + other·cother:
+  // the same two rounded products (x·1.0 = x, y·(-lb) = -(y·lb)) summed commutatively, so the
+  // same bits as the reference expression without selecting FY1/FY2 per lane.
+  const double q = (FY * pk.cown + FYo * pk.cother) / pk.div;
   const double qo = pair_swap(q);
   d[2] = (side ? qo : q) - r * uxc;
   d[3] = side ? q : qo;
   d[4] = r;
   d[5] = ax;
   d[6] = sr;
+}
+__device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side, const double* atab) {
+  double sp, cp;
+  mpj_sincos_bl(x[4], &sp, &cp);
+  dyn_pair_sc(x, sr, ax, d, side, atab, sp, cp, pair_k(side));
 }
 
 // VehicleDynamics for one lane holding the whole rollout: the front and rear tire chains of
@@ -264,6 +280,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
   double x[7];
 #pragma unroll
   for (int i = 0; i < 7; i++) x[i] = X0[i];
+  const PairK pk = pair_k(side);
   if (traj.p) store_state<LPR>(traj, 0, x, side);
   double sum = 0.0;
   int ok_all = 1;
@@ -287,10 +304,10 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
       double sn, cs;
       mpj_sincos_bl(side ? psi2 : x[4], &sn, &cs);
       const double so = pair_swap(sn), co = pair_swap(cs);
-      dyn_pair_sc(x, u[0], u[1], k1, side, atab, side ? so : sn, side ? co : cs);
+      dyn_pair_sc(x, u[0], u[1], k1, side, atab, side ? so : sn, side ? co : cs, pk);
 #pragma unroll
       for (int i = 0; i < 7; i++) x2[i] = x[i] + k1[i] * P.dt;
-      dyn_pair_sc(x2, u[0], u[1], k2, side, atab, side ? sn : so, side ? cs : co);
+      dyn_pair_sc(x2, u[0], u[1], k2, side, atab, side ? sn : so, side ? cs : co, pk);
     } else {
       dyn_lane(x, u[0], u[1], k1, atab);
 #pragma unroll

@@ -53,7 +53,12 @@ def test_branchless_variants_bitidentical():
     xs = np.concatenate([r.uniform(-10, 10, 20000), r.uniform(-7.1, 7.1, 20000), r.uniform(-1e-7, 1e-7, 2000),
                          np.pi / 2 * np.arange(-6, 7) + r.uniform(-1e-9, 1e-9, 13),
                          np.array([0.0, -0.0, 0.4375, 0.6875, 1.1875, 2.4375, math.pi / 2, math.pi, 3.9, -3.9,
-                                   math.pi / 4, 2.356194490192345, 1e-9, 2e20, np.inf, -np.inf])])
+                                   math.pi / 4, 2.356194490192345, 1e-9, 2e20, np.inf, -np.inf]),
+                         # atan_tab's special ranges handled by the general formula: tiny and huge
+                         np.array([2.0 ** -27, -(2.0 ** -27), np.nextafter(2.0 ** -27, 0), 2.0 ** -28, 1e-30, -1e-300,
+                                   5e-324, -5e-324, 2.2250738585072014e-308, 1e-310, 2.0 ** 66,
+                                   np.nextafter(2.0 ** 66, 0), -(2.0 ** 66), 1e300, -1e300, 1.7976931348623157e308]),
+                         np.exp(r.uniform(-700, 700, 5000)) * np.sign(r.uniform(-1, 1, 5000))])
     for x in xs:
         x = float(x)
         b = oracle.m("atan", x)
