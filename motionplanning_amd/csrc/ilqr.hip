@@ -1090,9 +1090,28 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
       Jn = jw;
       mw = r * G + gw;
       searching = false;
-      if (g == gw) {  // the winning lane copies its own slot (its own writes: program order)
-        for (size_t i = 0; i < N * 4; i++) Xb[i] = Xg[i];
-        for (size_t i = 0; i < N * 2; i++) Ub[i] = Ug[i];
+      // the instance's G lanes copy the winning slot together, 8 loads in flight per lane before
+      // the stores (instead of the winner alone, one dependent load->store at a time): the
+      // winner's slot stores are released at workgroup scope (the same wave) and L1 is
+      // invalidated before the reads
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const double* Xw = Xs + ((size_t)gw * B + b) * N * 4;
+      const double* Uw = Us + ((size_t)gw * B + b) * N * 2;
+      const size_t nx = N * 4, nt = N * 6;
+      for (size_t i0 = (size_t)g; i0 < nt; i0 += 8 * G) {
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const size_t i = i0 + (size_t)e * G;
+          v[e] = i < nx ? Xw[i] : i < nt ? Uw[i - nx] : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const size_t i = i0 + (size_t)e * G;
+          if (i < nx) Xb[i] = v[e];
+          else if (i < nt) Ub[i - nx] = v[e];
+        }
       }
     }
   }
