@@ -1052,10 +1052,30 @@ __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, cons
 // J_m < J (written !(J_m >= J), as the loop condition), or a break test (floor_stop, max_ls).
 // Identical results to the sequential search; one round instead of G trials of latency.
 // Jcur[b]: J at the start of this iteration (the previous J_new).
+// The end of ILQR.jl's iteration for instance b once trial mw (cost Jn) is accepted: the
+// max_ls flag, J, the iteration count and the convergence test.
+__device__ __forceinline__ void search_accept(const IlqrDev& P, size_t b, double J, double Jn, int mw, double* Jcur,
+                                              int* active, int* iters, int* flags, int* n_active) {
+  if (mw + 1 >= P.max_ls && !floor_stop(P, mw)) atomicOr(flags + b, 1);
+  Jcur[b] = Jn;
+  const int it = iters[b] + 1;
+  iters[b] = it;
+  bool go = __builtin_fabs((Jn - J) / J) > P.tol;
+  if (go && it > P.max_iter) {
+    atomicOr(flags + b, 2);
+    go = false;
+  }
+  active[b] = go;
+  if (go) atomicAdd(n_active, 1);
+}
+
+// one_round: stop after round 0 and mark the instances still searching in pending[] (their
+// trials G..ls_cap then run all at once in ilqr_search_rest_kernel).
 template <int G>
 __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
                                                          const double* Kg, double* Xs, double* Us, double* Jcur,
-                                                         int* active, int* iters, int* flags, int* n_active) {
+                                                         int* active, int* iters, int* flags, int* n_active,
+                                                         int one_round, int* pending) {
   constexpr int IPW = 64 / G;  // instances per wave
   const int lane = threadIdx.x, g = lane % G, sub = lane / G;
   const int b0 = blockIdx.x * IPW + sub;
@@ -1073,7 +1093,7 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   double Jn = J;
   int mw = -1;  // accepted trial index
   bool searching = live;
-  for (int r = 0; __any(searching); r++) {
+  for (int r = 0; __any(searching) && !(one_round && r > 0); r++) {
     const int m = r * G + g;
     const bool mine = searching && m <= P.ls_cap;
     double jt = 0.0;
@@ -1116,17 +1136,49 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
     }
   }
   if (!live || g != 0) return;
-  if (mw + 1 >= P.max_ls && !floor_stop(P, mw)) atomicOr(flags + b, 1);
-  Jcur[b] = Jn;
-  const int it = iters[b] + 1;
-  iters[b] = it;
-  bool go = __builtin_fabs((Jn - J) / J) > P.tol;
-  if (go && it > P.max_iter) {
-    atomicOr(flags + b, 2);
-    go = false;
+  if (searching) {  // one_round only: trials G..ls_cap follow in ilqr_search_rest_kernel
+    pending[b] = 1;
+    return;
   }
-  active[b] = go;
-  if (go) atomicAdd(n_active, 1);
+  search_accept(P, b, J, Jn, mw, Jcur, active, iters, flags, n_active);
+}
+
+// Trials G..ls_cap of the instances still searching after round 0, all at once: block (b, w)
+// runs trials m = G + 64w + lane into slots [b][m-G] (Xs2/Us2/Jt), and the first stopping
+// trial is the least m whose loop test would end the reference's halving loop (atomicMin).
+template <int G>
+__global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, const double* X, const double* U,
+                                                              const double* k, const double* Kg, const double* Jcur,
+                                                              const int* pending, double* Xs2, double* Us2,
+                                                              double* Jt, int* winm) {
+  const int b = blockIdx.x, m = G + 64 * (int)blockIdx.y + (int)threadIdx.x;
+  if (!pending[b] || m > P.ls_cap) return;
+  const size_t N = P.N, T2 = (size_t)(P.ls_cap + 1 - G), t = (size_t)(m - G);
+  int d = 0;
+  const double jt = forward_trial<false>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
+                                         ldexp(1.0, -m), Xs2 + ((size_t)b * T2 + t) * N * 4,
+                                         Us2 + ((size_t)b * T2 + t) * N * 2, true, d);
+  Jt[(size_t)b * T2 + t] = jt;
+  if (!(jt >= Jcur[b]) || m == P.ls_cap) atomicMin(winm + b, m);
+}
+
+// Accept the winning trial of each pending instance: 64 lanes copy its slot into X/U.
+template <int G>
+__global__ __launch_bounds__(64) void ilqr_search_finish_kernel(IlqrDev P, int B, double* X, double* U,
+                                                                const int* pending, const double* Xs2,
+                                                                const double* Us2, const double* Jt, const int* winm,
+                                                                double* Jcur, int* active, int* iters, int* flags,
+                                                                int* n_active) {
+  const size_t b = blockIdx.x;
+  if (!pending[b]) return;
+  const size_t N = P.N, T2 = (size_t)(P.ls_cap + 1 - G);
+  const int mw = winm[b];
+  const size_t t = (size_t)(mw - G);
+  const double* Xw = Xs2 + ((size_t)b * T2 + t) * N * 4;
+  const double* Uw = Us2 + ((size_t)b * T2 + t) * N * 2;
+  for (size_t i = threadIdx.x; i < N * 4; i += 64) X[b * N * 4 + i] = Xw[i];
+  for (size_t i = threadIdx.x; i < N * 2; i += 64) U[b * N * 2 + i] = Uw[i];
+  if (threadIdx.x == 0) search_accept(P, b, Jcur[b], Jt[(size_t)b * T2 + t], mw, Jcur, active, iters, flags, n_active);
 }
 
 // Initial guess roll out (ILQR.jl:31-37) with TotalCost accumulated in order.
@@ -1364,6 +1416,19 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   int* dit = dint + B;
   int* dfl = dint + 2 * B;
   int* dn = dint + 3 * B;
+  // trials G..ls_cap in one pass for the instances still searching after round 0 (G = 16 only),
+  // while their slots fit in 8 GiB; else the G-wide kernel runs its rounds to the end
+  const size_t T2 = G == 16 && D.ls_cap + 1 > G ? (size_t)(D.ls_cap + 1 - G) : 0;
+  const bool rest = T2 > 0 && T2 * B * N * 48 <= ((size_t)8 << 30);
+  double *dXs2 = nullptr, *dUs2 = nullptr, *dJt = nullptr;
+  int* dpw = nullptr;  // pending[B], winm[B]
+  if (rest) {
+    dXs2 = (double*)mp_ws(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2);
+    dUs2 = (double*)mp_ws(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2);
+    dJt = (double*)mp_ws(ctx, WS_IO12, sizeof(double) * B * T2);
+    dpw = (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 2 * (size_t)B);
+    if (!dXs2 || !dUs2 || !dJt || !dpw) return MP_ERR_NOMEM;
+  }
   const dim3 g1((B + 63) / 64), b1(64);
   hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl);
   MP_HIP(ctx, hipGetLastError());
@@ -1374,13 +1439,28 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
     mp_time_begin(ctx);
     const dim3 gs((unsigned)((B + 64 / G - 1) / (64 / G)));
+    if (rest) {
+      MP_HIP(ctx, hipMemsetAsync(dpw, 0, sizeof(int) * B, ctx->stream));             // pending
+      MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));      // winm = 0x7f7f7f7f
+    }
     if (G == 16)
-      hipLaunchKernelGGL(ilqr_search_kernel<16>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn);
+      hipLaunchKernelGGL(ilqr_search_kernel<16>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn,
+                         rest ? 1 : 0, dpw);
     else if (G == 4)
-      hipLaunchKernelGGL(ilqr_search_kernel<4>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn);
+      hipLaunchKernelGGL(ilqr_search_kernel<4>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn,
+                         0, dpw);
     else
-      hipLaunchKernelGGL(ilqr_search_kernel<1>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn);
+      hipLaunchKernelGGL(ilqr_search_kernel<1>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn,
+                         0, dpw);
     MP_HIP(ctx, hipGetLastError());
+    if (rest) {
+      hipLaunchKernelGGL(ilqr_search_rest_kernel<16>, dim3((unsigned)B, (unsigned)((T2 + 63) / 64)), b1, 0, ctx->stream, D,
+                         B, dX, dU, dk, dK, dJ, dpw, dXs2, dUs2, dJt, dpw + B);
+      MP_HIP(ctx, hipGetLastError());
+      hipLaunchKernelGGL(ilqr_search_finish_kernel<16>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dpw, dXs2,
+                         dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn);
+      MP_HIP(ctx, hipGetLastError());
+    }
     mp_time_end(ctx);
     MP_HIP(ctx, hipMemcpyAsync(hn, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
