@@ -287,14 +287,16 @@ def bench_ilqr(ctx, world, rank, cpu=False, reps=20, B=4096, N=100):
     if cpu:
         import oracle
 
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < 3.0:
-            ko, Ko = oracle.ilqr_backward(p, X[n % B], U[n % B])
-            oracle.ilqr_forward(p, X[n % B], U[n % B], ko, Ko, 1.0)
-            n += 1
-        dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": n * (N - 1) / dt, "unit": "instance-knots/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} instances (backward + forward, H=100) in {dt:.1f} s, scalar C oracle"}
+        def work(i):
+            ko, Ko = oracle.ilqr_backward(p, X[i % B], U[i % B])
+            oracle.ilqr_forward(p, X[i % B], U[i % B], ko, Ko, 1.0)
+            return N - 1
+
+        T = cpu_threads()
+        u, n, dt = timed_pool(work, 3.0, T)
+        out["cpu_baseline"] = {"value": u / dt, "unit": "instance-knots/s", "cores": T, "kind": "port",
+                               "sample": f"{n} instances (backward + forward, H=100) in {dt:.1f} s on {T} threads, "
+                                         "scalar C oracle"}
     return out
 
 
@@ -330,37 +332,81 @@ def bench_hastar(ctx, world, rank, cpu=False):
         h0 = hs[0]
         p = ha.params_of(h0)
         sc, pc = oracle.ha_neighbor_origin(h0.s.expand_time, h0.s.steer_set, h0.s.gear_set)
-        n, cp, t0 = 0, 0, time.perf_counter()
-        while time.perf_counter() - t0 < 3.0 and n < len(hs):
-            h = hs[n]
-            cp += oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc,
-                                 pc)["pops"]
-            n += 1
-        dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": cp / dt, "unit": "node expansions/s", "cores": 1, "kind": "port",
-                               "sample": f"{n} scenarios ({cp} pops) in {dt:.1f} s, scalar C oracle"}
+
+        def work(i):
+            h = hs[i]
+            return oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc,
+                                  pc)["pops"]
+
+        T = cpu_threads()
+        cp, n, dt = timed_pool(work, 3.0, T, limit=len(hs))
+        out["cpu_baseline"] = {"value": cp / dt, "unit": "node expansions/s", "cores": T, "kind": "port",
+                               "sample": f"{n} scenarios ({cp} pops) in {dt:.1f} s on {T} threads, scalar C oracle"}
     return out
 
 
+def cpu_threads():
+    """Host threads for the CPU baselines: MPGPU_CPU_THREADS, else OMP_NUM_THREADS (16 on the GPU box,
+    this job's CPU share), else min(16, cpu_count)."""
+    v = os.environ.get("MPGPU_CPU_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(v)) if v else min(16, os.cpu_count() or 1)
+
+
+def timed_pool(work, budget_s, threads, limit=None):
+    """Run work(i) for i = 0, 1, ... (i < limit) on `threads` Python threads until budget_s has passed
+    and return (units summed, items, seconds).  The oracle's ctypes calls release the GIL, so the
+    threads run the scalar C restatement in parallel, one independent solve per call."""
+    import threading
+
+    lock = threading.Lock()
+    state = {"next": 0, "units": 0, "items": 0}
+    t0 = time.perf_counter()
+    stop = t0 + budget_s
+
+    def worker():
+        while time.perf_counter() < stop:
+            with lock:
+                i = state["next"]
+                if limit is not None and i >= limit:
+                    return
+                state["next"] = i + 1
+            u = work(i)
+            with lock:
+                state["units"] += u
+                state["items"] += 1
+
+    ths = [threading.Thread(target=worker) for _ in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    return state["units"], state["items"], time.perf_counter() - t0
+
+
 def cpu_baseline(budget_s):
-    """The oracle (scalar C port, 1 thread) on the same cfg2 workload, bounded to ~budget_s."""
+    """The oracle (scalar C port) on the same cfg2 workload, bounded to ~budget_s: one thread for a
+    third of the budget, then every host thread of this job's share (independent MPPIPlan solves
+    per thread, as the GPU runs independent scenes)."""
     import oracle
     from motionplanning_amd import configs
     from motionplanning_amd.abi import MP_NOISE_PHILOX
 
     c = configs.cfg2(noise_mode=MP_NOISE_PHILOX)
-    p = c["params"]
-    n, t0 = 0, time.perf_counter()
-    while True:
-        p.offset = n
+    p0 = c["params"]
+
+    def work(i):
+        p = type(p0).from_buffer_copy(p0)  # per-call params: the Philox counter word differs
+        p.offset = i
         oracle.mppi_plan(p, c["X0"], c["goal"], c["unom"], None, c["grid"], None)
-        n += 1
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": p.K * p.H * n / dt, "unit": "rollout-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} full cfg2 MPPIPlan solves (K=8192, H=50, grid, Philox noise) in {dt:.1f} s, "
-                      f"scalar C oracle, 1 thread on {os.cpu_count()}-CPU host"}
+        return p.K * p.H
+
+    u1, n1, t1 = timed_pool(work, budget_s / 3, 1)
+    T = cpu_threads()
+    uT, nT, tT = timed_pool(work, budget_s, T)
+    return {"value": uT / tT, "unit": "rollout-steps/s", "cores": T, "kind": "port",
+            "sample": f"{nT} full cfg2 MPPIPlan solves (K=8192, H=50, grid, Philox noise) in {tT:.1f} s on {T} "
+                      f"threads (one solve per thread at a time), scalar C oracle, {os.cpu_count()}-CPU host",
+            "single_thread": {"value": u1 / t1, "cores": 1, "sample": f"{n1} solves in {t1:.1f} s"}}
 
 
 if __name__ == "__main__":

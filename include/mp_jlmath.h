@@ -638,12 +638,12 @@ MPJ_FN double mpj_atan_tab(double x, const double* tab) {
   const double s1 = z * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT10, aT8), aT6), aT4), aT2), aT0);
   const double s2 = w * mpj_fma(w, mpj_fma(w, mpj_fma(w, mpj_fma(w, aT9, aT7), aT5), aT3), aT1);
   const double r = hi - ((ax * (s1 + s2) - lo) - ax);
-  const double rs = mpj_flip(r, hx & 0x80000000u);
   /* FDLIBM's |x| < 2^-27 case needs no select here: with id 0 (ax = a) the polynomial term is
    * below half an ulp of a, so r == a exactly and the flip returns x (±0 and subnormals
-   * included; tests/test_jlmath.py).  |x| >= 2^66 keeps its select (±Inf would give 0·Inf). */
+   * included; tests/test_jlmath.py).  |x| >= 2^66 keeps a select (±Inf would give 0·Inf), taken
+   * before the sign flip: FDLIBM's -atanhi[3] - atanlo[3] is exactly -(atanhi[3] + atanlo[3]). */
   const double big = 1.57079632679489655800e+00 + 6.12323399573676603587e-17;
-  return MPJ_SEL(ix >= 0x44100000u && x == x, MPJ_SEL(hx >> 31, -big, big), rs);
+  return mpj_flip(MPJ_SEL(ix >= 0x44100000u && x == x, big, r), hx & 0x80000000u);
 }
 
 /* mpj_atan2 with the branch-free atan core (bit-identical: mpj_atan_bl == mpj_atan). */
@@ -782,6 +782,58 @@ MPJ_FN double mpj_sin_bl(double x) {
   double s, c;
   mpj_sincos_bl(x, &s, &c);
   return s;
+}
+
+/* sin for |x| <= 3π/4 as straight-line code (the tyre model's sin(C·atan(…)), C = 1.3,
+ * vehicledynamics.jl:35-38, never leaves |x| < 1.3·π/2): below π/4 FDLIBM's sin_k0(x), above it
+ * the reduction by n = ±1 and ±cos_k(y0, y1) — mpj_sin's own operations on that range, without
+ * the sin_k / n = ±2..4 lanes of mpj_sincos_fast.  Larger |x|, NaN/Inf and the cwext points next
+ * to ±π/2 take mpj_sin (wave-uniform on the device). */
+MPJ_FN double mpj_sin_34(double x) {
+  const uint32_t xhp = mpj_hi(x) & 0x7fffffffu;
+  const double ax = mpj_fabs(x);
+  const int small = ax < MPJ_PIO4;
+  if (MPJ_ANY(xhp > 0x4002d97cu || (!small && (xhp & 0xfffffu) == 0x921fbu))) return mpj_sin(x);
+  double y0, y1;
+  mpj_cw2c(x, x > 0.0 ? 1.0 : -1.0, 0, &y0, &y1);
+  const double xa = MPJ_SEL(small, x, y0), ya = MPJ_SEL(small, 0.0, y1);
+  const double z = xa * xa, w = z * z;
+  const double r = mpj_fma(z, mpj_fma(z, MPJ_S4, MPJ_S3), MPJ_S2) + z * w * mpj_fma(z, MPJ_S6, MPJ_S5);
+  const double v = z * xa;
+  const double sk0 = xa + v * (MPJ_S1 + z * r); /* mpj_sin_k0(x) */
+  const double ck = mpj_cos_k(xa, ya);           /* n = 1: cos_k; n = -1 (& 3 = 3): -cos_k */
+  return MPJ_SEL(small, MPJ_SEL(ax < MPJ_SQRT_EPS, x, sk0), mpj_flip(ck, mpj_hi(x) & 0x80000000u));
+}
+
+/* log for the Box–Muller draws, FDLIBM e_log.c as one basic block: its four result forms are two
+ * (the k == 0 forms are the k != 0 ones with dk = 0: 0·ln2_hi - (a - f) == f - a and
+ * b ± 0·ln2_lo == b exactly, the result of a normal x != 1 being nonzero), selected by FDLIBM's
+ * i > 0 test.  Zero, negative, subnormal, Inf/NaN and the |f| < 2^-20 case take mpj_log
+ * (wave-uniform on the device). */
+MPJ_FN double mpj_log_bl(double x) {
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
+               Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
+               Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  const int32_t hx0 = (int32_t)mpj_hi(x);
+  const int32_t hm = hx0 & 0x000fffff;
+  if (MPJ_ANY(hx0 < 0x00100000 || hx0 >= 0x7ff00000 || (0x000fffff & (2 + hm)) < 3)) return mpj_log(x);
+  const int32_t i0 = (hm + 0x95f64) & 0x100000;
+  const int32_t k = (hx0 >> 20) - 1023 + (i0 >> 20);
+  const double f = mpj_from_words((uint32_t)(hm | (i0 ^ 0x3ff00000)), mpj_lo(x)) - 1.0;
+  const double s = f / (2.0 + f);
+  const double dk = (double)k;
+  const double z = s * s;
+  const double w = z * z;
+  const double t1 = w * mpj_fma(w, mpj_fma(w, Lg6, Lg4), Lg2);
+  const double t2 = z * mpj_fma(w, mpj_fma(w, mpj_fma(w, Lg7, Lg5), Lg3), Lg1);
+  const int32_t i = (hm - 0x6147a) | (0x6b851 - hm);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double rp = dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+  const double rn = dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
+  return MPJ_SEL(i > 0, rp, rn);
 }
 
 /* exp for 2^-28 <= |x| < 704 as one basic block (FDLIBM e_exp.c with every branch a select):

@@ -62,6 +62,15 @@ void* mp_ctx_stream(mp_ctx* ctx);
  * count since the last query, and resets them. */
 int mp_ctx_kernel_timing(mp_ctx* ctx, int enable);
 int mp_ctx_kernel_ms(mp_ctx* ctx, double* ms_sum, int32_t* count);
+/* Device workspaces.  A context caches its scratch buffers across calls (they only grow, with
+ * 25 % headroom).  mp_ctx_trim synchronises and frees every cached buffer larger than
+ * keep_bytes (0: all of them); later calls re-allocate what they need.
+ * mp_ctx_set_workspace_limit caps any single buffer (0: no cap).  Optional speed-up buffers
+ * (mp_ilqr_solve's all-trials-at-once line-search slots, which are also skipped when they
+ * would take more than half of the free device memory) fall back to a smaller layout with
+ * identical results; a call that cannot run within the cap returns MP_ERR_NOMEM. */
+int mp_ctx_trim(mp_ctx* ctx, size_t keep_bytes);
+int mp_ctx_set_workspace_limit(mp_ctx* ctx, size_t bytes);
 
 /* ---------------------------------------------------------------- MPPI */
 #define MP_NX 7 /* [x, y, v, r, psi, ux, sa]  vehicledynamics.jl:20-26 */
@@ -280,7 +289,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
  * 4 atan2(x, y), 5 asin, 6 acos, 7 exp, 8 log, 9 modpi, 10 sqrt; the branch-free
  * variants of the hot kernels: 11 modpi_bl, 12 atan_bl, 13 atan_tab, 14 sin (sincos_bl),
  * 15 cos (sincos_bl), 16 exp_bl, 17 tan_bl, 18 atan2_sel(x, y), 19 sin / 20 cos (sincos_wide),
- * 21 tan_wide — each must equal its exact routine bit for bit. */
+ * 21 tan_wide, 22 sin_34 (tyre sin, |x| <= 3π/4 fast path), 23 log_bl — each must equal its exact
+ * routine bit for bit. */
 int mp_math_eval(mp_ctx* ctx, int32_t fn, int64_t n, const double* x, const double* y, double* out);
 
 #ifdef __cplusplus

@@ -120,6 +120,8 @@ SIGNATURES = {
     "mp_ctx_stream": (_V, [_V]),
     "mp_ctx_kernel_timing": (ctypes.c_int, [_V, ctypes.c_int]),
     "mp_ctx_kernel_ms": (ctypes.c_int, [_V, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]),
+    "mp_ctx_trim": (ctypes.c_int, [_V, ctypes.c_size_t]),
+    "mp_ctx_set_workspace_limit": (ctypes.c_int, [_V, ctypes.c_size_t]),
     "mp_mppi_plan": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), _I] + [_V] * 16),
     "mp_mppi_plan_dev": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), _I] + [_V] * 16),
     "mp_rollout": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), _I, _I, _V, _V, _V, ctypes.c_int64]

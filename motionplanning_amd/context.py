@@ -27,6 +27,14 @@ class Context:
     def synchronize(self):
         self.check(self.lib.mp_ctx_synchronize(self.handle))
 
+    def trim(self, keep_bytes=0):
+        """Free cached device workspaces larger than keep_bytes (0: all) — mp_ctx_trim."""
+        self.check(self.lib.mp_ctx_trim(self.handle, int(keep_bytes)))
+
+    def set_workspace_limit(self, nbytes):
+        """Cap any single device workspace at nbytes (0: no cap) — mp_ctx_set_workspace_limit."""
+        self.check(self.lib.mp_ctx_set_workspace_limit(self.handle, int(nbytes)))
+
     @property
     def stream(self):
         return self.lib.mp_ctx_stream(self.handle)

@@ -35,6 +35,8 @@ __global__ void math_kernel(int fn, long long n, const double* x, const double* 
     case 19: { double s, c; int b = 0; mpj_sincos_wide(a, &s, &c, &b); r = b ? mpj_sin(a) : s; break; }
     case 20: { double s, c; int b = 0; mpj_sincos_wide(a, &s, &c, &b); r = b ? mpj_cos(a) : c; break; }
     case 21: { int b = 0; r = mpj_tan_wide(a, &b); r = b ? mpj_tan(a) : r; break; }
+    case 22: r = mpj_sin_34(a); break;
+    case 23: r = mpj_log_bl(a); break;
   }
   out[i] = r;
 }
@@ -42,7 +44,7 @@ __global__ void math_kernel(int fn, long long n, const double* x, const double* 
 
 extern "C" int mp_math_eval(mp_ctx* ctx, int32_t fn, int64_t n, const double* x, const double* y, double* out) {
   if (!ctx) return MP_ERR_INVALID;
-  MP_CHECK(ctx, fn >= 0 && fn <= 21 && n >= 0 && x && out && ((fn != 4 && fn != 18) || y), "bad mp_math_eval arguments");
+  MP_CHECK(ctx, fn >= 0 && fn <= 23 && n >= 0 && x && out && ((fn != 4 && fn != 18) || y), "bad mp_math_eval arguments");
   if (n == 0) return MP_OK;
   MP_HIP(ctx, hipSetDevice(ctx->device));
   int st = MP_OK;

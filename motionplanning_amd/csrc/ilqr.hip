@@ -1405,8 +1405,11 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   double* dk = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * 2 * (N - 1) * B);
   double* dK = (double*)mp_ws(ctx, WS_IO3, sizeof(double) * 8 * (N - 1) * B);
   // trial slots for the G-wide line search: G = 16 (1024 waves at B = 4096) while the slots stay
-  // within 1 GiB of HBM, else 4, else 1 (the sequential loop)
-  const int G = (size_t)16 * B * N * 48 <= ((size_t)1 << 30) ? 16 : (size_t)4 * B * N * 48 <= ((size_t)1 << 30) ? 4 : 1;
+  // within 1 GiB of HBM (and the context's workspace cap), else 4, else 1 (the sequential loop)
+  auto fits = [&](size_t g) {  // X slots 32 B, U slots 16 B per (trial, instance, knot)
+    return g * B * N * 48 <= ((size_t)1 << 30) && (!ctx->ws_limit || g * B * N * 32 <= ctx->ws_limit);
+  };
+  const int G = fits(16) ? 16 : fits(4) ? 4 : 1;
   double* dXn = (double*)mp_ws(ctx, WS_IO4, sizeof(double) * 4 * N * B * G);
   double* dUn = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 2 * N * B * G);
   double* dJ = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * B);
@@ -1417,17 +1420,24 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   int* dfl = dint + 2 * B;
   int* dn = dint + 3 * B;
   // trials G..ls_cap in one pass for the instances still searching after round 0 (G = 16 only),
-  // while their slots fit in 8 GiB; else the G-wide kernel runs its rounds to the end
+  // while their slots fit in 8 GiB, in half of the free device memory and in the context's
+  // workspace cap.  Otherwise -- or when allocating them fails -- the G-wide kernel runs its
+  // rounds to the end: the same accepted trials (tests/test_gpu_ilqr.py), more latency.
   const size_t T2 = G == 16 && D.ls_cap + 1 > G ? (size_t)(D.ls_cap + 1 - G) : 0;
-  const bool rest = T2 > 0 && T2 * B * N * 48 <= ((size_t)8 << 30);
+  bool rest = T2 > 0 && T2 * B * N * 48 <= ((size_t)8 << 30) &&
+              mp_ws_affordable(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2, 0.5) &&
+              mp_ws_affordable(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2, 0.25);
   double *dXs2 = nullptr, *dUs2 = nullptr, *dJt = nullptr;
   int* dpw = nullptr;  // pending[B], winm[B]
   if (rest) {
     dXs2 = (double*)mp_ws(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2);
-    dUs2 = (double*)mp_ws(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2);
-    dJt = (double*)mp_ws(ctx, WS_IO12, sizeof(double) * B * T2);
-    dpw = (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 2 * (size_t)B);
-    if (!dXs2 || !dUs2 || !dJt || !dpw) return MP_ERR_NOMEM;
+    dUs2 = dXs2 ? (double*)mp_ws(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2) : nullptr;
+    dJt = dUs2 ? (double*)mp_ws(ctx, WS_IO12, sizeof(double) * B * T2) : nullptr;
+    dpw = dJt ? (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 2 * (size_t)B) : nullptr;
+    if (!dXs2 || !dUs2 || !dJt || !dpw) {
+      rest = false;      // fall back to the multi-round 16-wide search
+      ctx->err.clear();  // (the failed allocation left a message; mp_ws already cleared the HIP error)
+    }
   }
   const dim3 g1((B + 63) / 64), b1(64);
   hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl);

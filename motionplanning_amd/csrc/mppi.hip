@@ -77,6 +77,7 @@ struct PlanArgs {
   int nb;
   int pstride;
   int lds_unom, lds_obs, lds_grid;  // offsets (in doubles) into dynamic LDS; lds_grid < 0: grid stays in HBM
+  int lds_cq;                       // control-cost rows [H][2] (ctrl_cost_row)
   int lds_ctrl, lds_part;           // control lists [RPB][2H+1] / staged partials (< 0: use HBM)
   unsigned long long* stamps;       // diagnostic build only (MPGPU_STAMPS=1): [grid][8] s_memrealtime
   int inline_noise;                 // 1: Philox draws inside the rollout loop (no noise_prep pass)
@@ -181,6 +182,8 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     const double* gu = A.unom + (size_t)H2 * s;
     if (tid == 0) mpj_atan_tab_init(atab);
     for (int i = tid; i < H2; i += NT) unom[i] = gu[i];
+    if (P.ctrl_cost)
+      for (int i = tid; i < H; i += NT) ctrl_cost_row(P, gu[2 * i], gu[2 * i + 1], dyn + A.lds_cq + 2 * i);
     if (A.obs) {
       const double* go = A.obs + (size_t)3 * P.n_obs * s;
       for (int i = tid; i < 3 * P.n_obs; i += NT) obs[i] = go[i];
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     };
     // inactive pairs (k >= K) recompute rollout K-1 and write identical values
     const TrajOut traj{A.coll_traj ? A.coll_traj + (size_t)s * (H + 1) * 7 * K + kk : nullptr, 7LL * K, (long long)K};
-    c = rollout_pair<LPR>(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas, atab);
+    c = rollout_pair<LPR>(P, X0, goal, obs, grid, unom, side, ctrl, store, traj, &feas, atab, dyn + A.lds_cq);
   }
   MP_STAMP(1);
   MP_STAMP_WAVE();
@@ -695,6 +698,8 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   int off = 2 * H + nb;
   A.lds_unom = off;
   off += 2 * H;
+  A.lds_cq = off;
+  off += 2 * H;
   A.lds_obs = off;
   off += 3 * D.n_obs;
   const size_t gbytes = (size_t)D.gnx * D.gny;
@@ -724,8 +729,8 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   }
   const size_t shmem = sizeof(double) * (size_t)off;
   MP_CHECK(ctx, shmem <= kMaxLds, "K/H/obstacles too large for one scene (dynamic LDS %zu B)", shmem);
-  static bool attr_set = false;
-  if (!attr_set) {
+  if (!ctx->mppi_lds_attr) {
+    MP_HIP(ctx, hipSetDevice(ctx->device));  // the attribute applies to the current device
     MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<256, 2>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
     MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<512, 2>,
@@ -738,7 +743,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
     MP_HIP(ctx, hipFuncSetAttribute((const void*)mppi_plan_kernel<128, 1>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds));
-    attr_set = true;
+    ctx->mppi_lds_attr = true;
   }
   // deferred final rollout: snapshot ring slot of this call, free once the final rollout of
   // the call MP_FIN_RING back (same slot) is done
@@ -789,11 +794,11 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     const int grid_lds = (size_t)R.stride * 8 <= 64 * 1024;
     const size_t fsh = sizeof(double) * (size_t)(grid_lds ? R.stride : R.grid);
     MP_CHECK(ctx, fsh <= kMaxLds, "final rollout snapshot too large for LDS (%zu B)", fsh);
-    static bool fattr = false;
-    if (!fattr) {
+    if (!ctx->fin_lds_attr) {
+      MP_HIP(ctx, hipSetDevice(ctx->device));
       MP_HIP(ctx, hipFuncSetAttribute((const void*)final_rollout_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kMaxLds));
-      fattr = true;
+      ctx->fin_lds_attr = true;
     }
     hipEvent_t plan_done = t_stop;
     if (!plan_done) {

@@ -71,7 +71,7 @@ __device__ __forceinline__ void dyn_pair_sc(const double* x, double sr, double a
   // front: (v + la*r) ... - sa;  rear: (v - lb*r) ... [(-lb)*r == -(lb*r) exactly]  (:32-33)
   const double alpha = mpj_atan_tab((v + pk.lr * r) / (ux + 0.01), atab) - (side ? 0.0 : sa);
   const double X1 = B * alpha;
-  const double FY = mu * FZ * 1.0 * mpj_sin_bl(C * mpj_atan_tab(X1 - E * (X1 - mpj_atan_tab(X1, atab)), atab));  // (:35-38)
+  const double FY = mu * FZ * 1.0 * mpj_sin_34(C * mpj_atan_tab(X1 - E * (X1 - mpj_atan_tab(X1, atab)), atab));  // (:35-38)
   const double FYo = pair_swap(FY);
   const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);  // (:40-42)
   d[0] = uxc * cp - v * sp;
@@ -109,8 +109,8 @@ __device__ __forceinline__ void dyn_lane(const double* x, double sr, double ax, 
   const double af = mpj_atan_tab((v + la * r) / (ux + 0.01), atab) - sa;
   const double ar = mpj_atan_tab((v + (-lb) * r) / (ux + 0.01), atab) - 0.0;
   const double Xf = B * af, Xr = B * ar;
-  const double FY1 = mu * FZf * 1.0 * mpj_sin_bl(C * mpj_atan_tab(Xf - E * (Xf - mpj_atan_tab(Xf, atab)), atab));
-  const double FY2 = mu * FZr * 1.0 * mpj_sin_bl(C * mpj_atan_tab(Xr - E * (Xr - mpj_atan_tab(Xr, atab)), atab));
+  const double FY1 = mu * FZf * 1.0 * mpj_sin_34(C * mpj_atan_tab(Xf - E * (Xf - mpj_atan_tab(Xf, atab)), atab));
+  const double FY2 = mu * FZr * 1.0 * mpj_sin_34(C * mpj_atan_tab(Xr - E * (Xr - mpj_atan_tab(Xr, atab)), atab));
   const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);
   double sp, cp;
   mpj_sincos_bl(psi, &sp, &cp);
@@ -184,6 +184,10 @@ __device__ __forceinline__ double bound_cost(const MppiDev& P, const double* x, 
 // ------------------------------------------------------------------ noise
 __device__ __forceinline__ void philox4x32(unsigned c0, unsigned c1, unsigned c2, unsigned c3, unsigned k0,
                                            unsigned k1, unsigned* o) {
+  // The key schedule is wave-uniform: an opaque register copy makes the scalar unit recompute
+  // the 20 round keys per call (s_add), instead of the compiler hoisting them out of the rollout
+  // loop, spilling them to VGPR lanes and restoring them with v_readlane (VALU work) every call.
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int i = 0; i < 10; i++) {
     const unsigned long long p0 = (unsigned long long)0xD2511F53u * c0;
@@ -214,7 +218,7 @@ __device__ __forceinline__ void philox_normal2(const MppiDev& P, unsigned scene,
   const unsigned long long b2 = ((unsigned long long)(o[2] >> 5) << 26) | (unsigned long long)(o[3] >> 6);
   const double u1 = ((double)b1 + 0.5) * 1.1102230246251565e-16;
   const double u2 = ((double)b2 + 0.5) * 1.1102230246251565e-16;
-  const double rr = mpj_sqrt(-2.0 * mpj_log(u1));
+  const double rr = mpj_sqrt(-2.0 * mpj_log_bl(u1));
   double sn, cs;
   mpj_sincos_bl(MPJ_TWO_PI * u2, &sn, &cs);
   z[0] = rr * cs;
@@ -268,15 +272,27 @@ __device__ __forceinline__ void store_state(const TrajOut& T, int j, const doubl
   }
 }
 
+// The control cost λ·u_nomᵀ·inv(Σ)·(u − u_nom) of step j (MPPIUtils.jl:45, Julia's n-ary `*` as a
+// left fold): its row vector t = (λ·u_nom)ᵀ·inv(Σ) depends only on the scene's nominal control,
+// so the plan kernel evaluates it once per (scene, step) into LDS (same operations, same bits)
+// instead of once per rollout-step.
+__device__ __forceinline__ void ctrl_cost_row(const MppiDev& P, double un0, double un1, double* t) {
+  const double a0 = P.lambda * un0, a1 = P.lambda * un1;
+  t[0] = a0 * P.Si[0] + a1 * P.Si[2];
+  t[1] = a0 * P.Si[1] + a1 * P.Si[3];
+}
+
 // --------------------------------------------------------------- rollout
 // TrajectoryRollout for the lane pair (MPPIUtils.jl:31-57).  `ctrl(j, u)` yields the
 // control of step j.  traj.p (optional) gets the H+1 states (store_state).
+// cq: the control-cost rows [H][2] (ctrl_cost_row), or nullptr to evaluate them per step.
 // Returns cost_total; *feas = constraint.
 template <int LPR = 2, class CtrlFn, class StoreFn>
 __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X0, const double* goal,
                                                const double* obs, const unsigned char* grid,
                                                const double* unom, int side, CtrlFn ctrl, StoreFn store,
-                                               const TrajOut& traj, int* feas, const double* atab) {
+                                               const TrajOut& traj, int* feas, const double* atab,
+                                               const double* cq = nullptr) {
   double x[7];
 #pragma unroll
   for (int i = 0; i < 7; i++) x[i] = X0[i];
@@ -319,10 +335,15 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
     double cj = pc + cb + cc;
     if (P.ctrl_cost) {
       const double un0 = unom[2 * j], un1 = unom[2 * j + 1];
-      const double a0 = P.lambda * un0, a1 = P.lambda * un1;
-      const double t0 = a0 * P.Si[0] + a1 * P.Si[2], t1 = a0 * P.Si[1] + a1 * P.Si[3];
+      double t[2];
+      if (cq) {
+        t[0] = cq[2 * j];
+        t[1] = cq[2 * j + 1];
+      } else {
+        ctrl_cost_row(P, un0, un1, t);
+      }
       const double d0 = u[0] - un0, d1 = u[1] - un1;
-      cj = cj + (t0 * d0 + t1 * d1);
+      cj = cj + (t[0] * d0 + t[1] * d1);
     }
     sum = sum + cj;
     ok_all &= okc & okb;

@@ -25,6 +25,11 @@ void* mp_ws(mp_ctx* ctx, int slot, size_t bytes) {
   }
   if (bytes == 0) bytes = 16;
   if (ctx->ws_size[slot] >= bytes) return ctx->ws_ptr[slot];
+  if (ctx->ws_limit && bytes > ctx->ws_limit) {
+    mp_fail(ctx, MP_ERR_NOMEM, "workspace slot %d needs %zu B, above the context limit of %zu B", slot, bytes,
+            ctx->ws_limit);
+    return nullptr;
+  }
   if (ctx->ws_ptr[slot]) {
     mp_sync_all(ctx);
     hipFree(ctx->ws_ptr[slot]);
@@ -32,14 +37,38 @@ void* mp_ws(mp_ctx* ctx, int slot, size_t bytes) {
     ctx->ws_size[slot] = 0;
   }
   size_t cap = bytes + bytes / 4;  // grow with headroom
+  if (ctx->ws_limit && cap > ctx->ws_limit) cap = ctx->ws_limit;
   void* p = nullptr;
   if (hipMalloc(&p, cap) != hipSuccess) {
-    mp_fail(ctx, MP_ERR_NOMEM, "hipMalloc(%zu) failed for workspace slot %d", cap, slot);
-    return nullptr;
+    // an out-of-memory hipMalloc is not sticky, but it stays the thread's last error: clear it so
+    // the next launch check does not report it; then try without the headroom
+    (void)hipGetLastError();
+    p = nullptr;
+    if (cap == bytes || hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      mp_fail(ctx, MP_ERR_NOMEM, "hipMalloc(%zu) failed for workspace slot %d", bytes, slot);
+      return nullptr;
+    }
+    cap = bytes;
   }
   ctx->ws_ptr[slot] = p;
   ctx->ws_size[slot] = cap;
   return p;
+}
+
+size_t mp_ws_size(mp_ctx* ctx, int slot) {
+  return slot >= 0 && slot < (int)ctx->ws_size.size() ? ctx->ws_size[slot] : 0;
+}
+
+bool mp_ws_affordable(mp_ctx* ctx, int slot, size_t bytes, double frac) {
+  if (mp_ws_size(ctx, slot) >= bytes) return true;
+  if (ctx->ws_limit && bytes > ctx->ws_limit) return false;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return (double)(bytes - mp_ws_size(ctx, slot)) <= frac * (double)fr;
 }
 
 int mp_ticket_reserve(mp_ctx* ctx, int n) {
@@ -222,5 +251,24 @@ int mp_ctx_join(mp_ctx* ctx) {
 }
 
 void* mp_ctx_stream(mp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int mp_ctx_trim(mp_ctx* ctx, size_t keep_bytes) {
+  if (!ctx) return MP_ERR_INVALID;
+  MP_HIP(ctx, hipSetDevice(ctx->device));
+  mp_sync_all(ctx);  // in-flight work (incl. the side stream's final rollouts) may still read them
+  for (size_t i = 0; i < ctx->ws_ptr.size(); i++)
+    if (ctx->ws_ptr[i] && (keep_bytes == 0 || ctx->ws_size[i] > keep_bytes)) {
+      MP_HIP(ctx, hipFree(ctx->ws_ptr[i]));
+      ctx->ws_ptr[i] = nullptr;
+      ctx->ws_size[i] = 0;
+    }
+  return MP_OK;
+}
+
+int mp_ctx_set_workspace_limit(mp_ctx* ctx, size_t bytes) {
+  if (!ctx) return MP_ERR_INVALID;
+  ctx->ws_limit = bytes;
+  return MP_OK;
+}
 
 }  // extern "C"

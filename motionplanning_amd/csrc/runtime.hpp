@@ -42,6 +42,11 @@ struct mp_ctx {
   hipStream_t side = nullptr;
   hipEvent_t ev_plan[MP_FIN_RING] = {}, ev_fin[MP_FIN_RING] = {}, ev_join = nullptr;
   int fin_par = 0;
+  // cap on any one workspace slot (mp_ctx_set_workspace_limit), 0 = none
+  size_t ws_limit = 0;
+  // kernel attributes (150 KiB dynamic LDS) are per device: set once per context, on its device
+  // (a context is used by one thread at a time, so the flags need no lock)
+  bool mppi_lds_attr = false, fin_lds_attr = false;
 };
 
 // Create the side stream and its events on first use.
@@ -92,6 +97,11 @@ enum {
 
 int mp_fail(mp_ctx* ctx, int code, const char* fmt, ...);
 void* mp_ws(mp_ctx* ctx, int slot, size_t bytes);  // nullptr on failure (error set)
+// bytes currently held by a workspace slot (0 if none)
+size_t mp_ws_size(mp_ctx* ctx, int slot);
+// whether a slot of `bytes` may be allocated now: within the context limit and, if the slot must
+// grow, within `frac` of the device's free memory (optional speed-up buffers only)
+bool mp_ws_affordable(mp_ctx* ctx, int slot, size_t bytes, double frac);
 int mp_ticket_reserve(mp_ctx* ctx, int n);
 void* mp_pinned(mp_ctx* ctx, size_t bytes);
 

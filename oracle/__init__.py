@@ -32,7 +32,7 @@ def lib():
         if not os.path.exists(LIB):
             build()
         L = ctypes.CDLL(LIB)
-        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "atan_tab", "modpi_bl", "sin_bl", "cos_bl", "exp_bl", "tan_bl", "sin_wide", "cos_wide", "tan_wide"]:
+        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "atan_tab", "modpi_bl", "sin_bl", "cos_bl", "exp_bl", "tan_bl", "sin_wide", "cos_wide", "tan_wide", "sin_34", "log_bl"]:
             f = getattr(L, "or_m_" + n)
             f.restype = _D
             f.argtypes = [_D]

@@ -360,4 +360,6 @@ double or_m_atan_tab(double x) {
   return mpj_atan_tab(x, tab);
 }
 double or_m_sin_bl(double x) { return mpj_sin_bl(x); }
+double or_m_sin_34(double x) { return mpj_sin_34(x); }
+double or_m_log_bl(double x) { return mpj_log_bl(x); }
 double or_m_cos_bl(double x) { double s, c; mpj_sincos_bl(x, &s, &c); return c; }

@@ -53,6 +53,42 @@ def test_solve_bitexact(ctx, variant, N, max_iter):
         assert 10080 < J[0] < 10100 and it[0] == 13
 
 
+def test_solve_under_workspace_limit():
+    """mp_ilqr_solve keeps its results when its optional line-search slots cannot be allocated: a
+    context capped below the all-trials-at-once slots falls back to the multi-round 16-wide search,
+    a tighter cap to the 4-wide one; a cap below the base buffers is MP_ERR_NOMEM, and the context
+    works again after mp_ctx_trim + lifting the cap (no hard failure where the old
+    search fit)."""
+    from motionplanning_amd.abi import MP_ERR_NOMEM, MPGPUError
+    from motionplanning_amd.context import Context
+
+    p = ilqr.params(N=20, max_iter=60)
+    x0, U0 = _instances(24, 20, seed=7)  # includes instances that stall (max_ls trials)
+    c = Context(0)
+    try:
+        X0, _ = ilqr.ilqr_rollout(p, x0, U0, ctx=c)
+        ref = ilqr.ilqr_solve(p, X0, U0, ctx=c)  # no cap: rest slots (2.8 MB) in use
+        # 1 MB: the 16-wide slots (245 KB) fit, the rest slots (2.8 MB) do not; 230 KB: the
+        # 4-wide slots (61 KB) and the derivative records (212 KB) only
+        for cap in (1 << 20, 230 << 10):
+            c.trim()
+            c.set_workspace_limit(cap)
+            got = ilqr.ilqr_solve(p, X0, U0, ctx=c)
+            for a, b in zip(got[:4], ref[:4]):
+                assert np.array_equal(a, b), cap
+        c.trim()  # the cap applies when a workspace grows: cached buffers are kept until trimmed
+        c.set_workspace_limit(1024)
+        with pytest.raises(MPGPUError) as e:
+            ilqr.ilqr_solve(p, X0, U0, ctx=c)
+        assert e.value.status == MP_ERR_NOMEM
+        c.set_workspace_limit(0)
+        c.trim()
+        got = ilqr.ilqr_solve(p, X0, U0, ctx=c)
+        assert np.array_equal(got[2], ref[2]) and np.array_equal(got[3], ref[3])
+    finally:
+        c.close()
+
+
 def test_cfg3_full_size_one_pass(ctx):
     """BASELINE configs[2]: H=100 knots x 4096 initial states, one backward + one forward trial;
     16 instances spot-checked bit-exact, all finite."""

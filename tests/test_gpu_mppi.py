@@ -186,15 +186,15 @@ def test_jlmath_bitexact(ctx):
     ranges = {0: (-30, 30), 1: (-30, 30), 2: (-1.5, 1.5), 3: (-60, 60), 4: (-5, 5), 5: (-1, 1), 6: (-1, 1),
               7: (-700, 700), 8: (1e-300, 1e4), 9: (-40, 40), 10: (0, 1e6), 11: (-15, 15), 12: (-60, 60),
               13: (-60, 60), 14: (-10, 10), 15: (-10, 10), 16: (-720, 720), 17: (-1.0, 1.0), 18: (-5, 5),
-              19: (-1e6, 1e6), 20: (-12, 12), 21: (-12, 12)}
+              19: (-1e6, 1e6), 20: (-12, 12), 21: (-12, 12), 22: (-2.3, 2.3), 23: (1e-17, 1.0)}
     names = {0: "sin", 1: "cos", 2: "tan", 3: "atan", 4: "atan2", 5: "asin", 6: "acos", 7: "exp", 8: "log",
              9: "modpi", 11: "modpi", 12: "atan", 13: "atan", 14: "sin", 15: "cos", 16: "exp", 17: "tan",
-             18: "atan2", 19: "sin", 20: "cos", 21: "tan"}
+             18: "atan2", 19: "sin", 20: "cos", 21: "tan", 22: "sin", 23: "log"}
     edges = np.array([0.0, -0.0, 1e-300, -1e-300, 0.4375, 0.6875, 1.1875, 2.4375, np.pi / 4, np.pi / 2, np.pi,
                       2 * np.pi, 3 * np.pi / 4, 4 * np.pi, -4 * np.pi, 1e5, -1e5] +  # |x| < 2^20 pi/2 (Cody-Waite domain)
                      [np.nextafter(k * np.pi / 2, d) for k in range(-6, 7) for d in (-np.inf, np.inf)])
     for fn, (lo, hi) in ranges.items():
-        x = np.r_[r.uniform(lo, hi, 20000), edges if fn in (11, 12, 13, 14, 15, 16, 17, 19, 20, 21) else [],
+        x = np.r_[r.uniform(lo, hi, 20000), edges if fn in (11, 12, 13, 14, 15, 16, 17, 19, 20, 21, 22) else [],
                   EXP_EDGES if fn == 16 else [], TAN_EDGES if fn in (17, 21) else []]
         y = r.uniform(-5, 5, len(x))
         if fn == 18:

@@ -71,6 +71,28 @@ def test_branchless_variants_bitidentical():
                 assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0], (fb, x)
 
 
+def test_tyre_sin_and_log_variants_bitidentical():
+    """mpj_sin_34 (the tyre model's sin, n = 0 / ±1 only) == mpj_sin, mpj_log_bl (Box–Muller log,
+    two selected result forms) == mpj_log — incl. the cwext points next to ±π/2, the 3π/4 edge,
+    arguments outside the fast ranges, and u in (0, 1) as the Philox draws produce them."""
+    r = np.random.default_rng(21)
+    near = np.concatenate([k * np.pi / 2 + r.uniform(-3e-7, 3e-7, 400) for k in (-1, 1)])
+    xs = np.concatenate([r.uniform(-2.1, 2.1, 40000), r.uniform(-3, 3, 5000), near, r.uniform(-1e-7, 1e-7, 500),
+                         [np.nextafter(k * np.pi / 4, d) for k in range(-4, 5) for d in (-np.inf, np.inf)],
+                         np.array([0.0, -0.0, 2.356194490192345, -2.356194490192345, 2.3561944901923453, 1e-300,
+                                   1.5707963267948966, -1.5707963267948966, 7.0, -9.5, 1e6, np.inf, -np.inf, np.nan])])
+    for x in xs:
+        a, b = oracle.m("sin_34", float(x)), oracle.m("sin", float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), x
+    us = np.concatenate([(r.integers(0, 2 ** 53, 30000) + 0.5) * 2.0 ** -53, r.uniform(0, 1, 5000),
+                         np.exp(r.uniform(-700, 700, 5000)),
+                         np.array([1.0, 0.5, 2.0, 1.0 + 2.0 ** -52, 1.0 - 2.0 ** -53, 0.7071067811865476, 1.5, 0.0,
+                                   -1.0, 5e-324, 2.2250738585072014e-308, 1e300, np.inf, np.nan])])
+    for x in us:
+        a, b = oracle.m("log_bl", float(x)), oracle.m("log", float(x))
+        assert np.array([a]).view(np.int64)[0] == np.array([b]).view(np.int64)[0] or (a != a and b != b), x
+
+
 def test_modpi_branchless_bitidentical():
     """mpj_modpi_bl (device fast path, no fmod loop) == mpj_modpi (Julia modπ)."""
     r = np.random.default_rng(5)
