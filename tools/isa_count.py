@@ -70,13 +70,17 @@ def main():
         body = lines[s0:e0]
         heads = [i for i, l in enumerate(body) if "Loop Header: Depth=1" in l and l.startswith(".LBB")]
         for h in heads:
-            lab = body[h].split(":")[0]
-            back = [j for j, l in enumerate(body) if re.search(r"s_(cbranch_\w+|branch)\s+" + re.escape(lab) + r"$", l.strip())]
-            if not back:
-                continue
-            seg = body[h:max(back) + 1]
-            ins = [l.strip().split()[0] for l in seg if l.strip() and not l.strip().startswith((";", ".")) and
-                   not l.startswith(".")]
+            lab = body[h].split(":")[0]  # .LBBk_n
+            tag = lab[2:]  # BBk_n as in the "in Loop: Header=BBk_n" / "Parent Loop BBk_n" block notes
+            # every basic block of the loop nest: the header and each block the assembler notes as in it
+            ins, inside = [], False
+            for l in body:
+                if l.startswith(".LBB") or l.startswith("; %bb."):
+                    inside = l.startswith(lab + ":") or ("Header=" + tag + " ") in l or ("Parent Loop " + tag + " ") in l
+                    continue
+                t = l.strip()
+                if inside and t and not t.startswith((";", ".")):
+                    ins.append(t.split()[0])
             if best is None or len(ins) > len(best[1]):
                 best = (lines[s0].split(":")[0], ins)
     name, ins = best
