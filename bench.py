@@ -209,6 +209,7 @@ def main():
     if not a.no_extras:
         out["ilqr"] = bench_ilqr(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
         out["hybrid_astar"] = bench_hastar(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
+        out["closed_loop"] = bench_closed_loop(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     if rank == 0:
@@ -342,6 +343,74 @@ def bench_hastar(ctx, world, rank, cpu=False):
         cp, n, dt = timed_pool(work, 3.0, T, limit=len(hs))
         out["cpu_baseline"] = {"value": cp / dt, "unit": "node expansions/s", "cores": T, "kind": "port",
                                "sample": f"{n} scenarios ({cp} pops) in {dt:.1f} s on {T} threads, scalar C oracle"}
+    return out
+
+
+def bench_closed_loop(ctx, world, rank, cpu=False, S=8, sim_s=2.0):
+    """configs[4]-style multi-ego closed loop (OptimalControl/MPPI/main.jl:55-83 per scene): S scenes per
+    GPU, each replanning configs[1] (K=8192, H=50, grid, device Philox) every 100 plant steps of the
+    1 kHz Euler plant, for sim_s seconds of simulated time (goals out of reach: no early stop), all on
+    the device (mp_mppi_closed_loop: plan kernel + plant kernel per replan, the final rollouts on the
+    side stream beside the plant).  Plus the reference's own run (MPPI/main.jl exactly: one scene,
+    K=1500, N=20, three circles, up to 15 s) timed end to end against the oracle's."""
+    from motionplanning_amd import configs
+    from motionplanning_amd.mppi import mppi_closed_loop_batch
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    c = configs.cfg2()
+    p = c["params"]
+    p.scene_base = rank * S
+    K, H = p.K, p.H
+    upd, hold = configs.mppi_hold_index(H * p.dt, H)
+    steps = int(round(sim_s / configs.PLANT_DT_REF))
+    X0 = np.tile(c["X0"], (S, 1))
+    X0[:, 1] = np.linspace(-0.5, 0.5, S) if S > 1 else 0.0
+    goal = np.tile([1e4, 0.0], (S, 1))
+    grid = np.tile(c["grid"], (S, 1, 1))
+    U0 = np.zeros((S, H, 2))
+
+    def once(seed):
+        p.seed = seed
+        return mppi_closed_loop_batch(p, X0, goal, U0, hold, upd, steps, configs.PLANT_DT_REF, 6.0, None, grid,
+                                      None, logs=False, ctx=ctx)
+
+    once(1)  # warm-up: workspaces
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g = once(2)
+    el = _sync_max(time.perf_counter() - t0, world, dev)
+    R = int(g["n_replans"].max())
+    out = {"metric": "MPPI closed loop (MPPI/main.jl:55-83), S scenes x configs[1] replanned every 100 plant steps",
+           "value": world * S * K * H * R / el, "unit": "rollout-steps/s (incl. plant)", "scenes_per_gpu": S,
+           "replans": R, "plant_steps": steps, "ms_per_replan": el / R * 1e3, "ms_total": el * 1e3,
+           "scaling": "weak", "dtype": "f64", "valid": bool((g["n_rows"] == steps + 1).all() and not g["nan"])}
+    # the reference's run, whole
+    pr = configs.mppi_params(K=1500, H=20, T=3.0, n_obs=3, noise_mode=1, seed=7)
+    u2, h2 = configs.mppi_hold_index(3.0, 20)
+    ms = int(np.floor(configs.SIM_TIME_REF / configs.PLANT_DT_REF))
+    obs = np.array(configs.OBSTACLES_REF)[None]
+    args = (np.array(configs.X0_REF)[None], np.array(configs.GOAL_REF)[None], np.zeros((1, 20, 2)), h2, u2, ms,
+            configs.PLANT_DT_REF, configs.GOAL_RADIUS_MPPI, obs)
+    mppi_closed_loop_batch(pr, *args, logs=False, ctx=ctx)
+    t0 = time.perf_counter()
+    gr = mppi_closed_loop_batch(pr, *args, logs=False, ctx=ctx)
+    e2 = time.perf_counter() - t0
+    out["reference_run"] = {"workload": "MPPI/main.jl: 1 scene, K=1500, N=20, 3 circles, 100 plant steps per "
+                                        "replan, until within 6 m of the goal or 15 s",
+                            "ms_total": e2 * 1e3, "replans": int(gr["n_replans"][0]),
+                            "ms_per_replan": e2 / max(1, int(gr["n_replans"][0])) * 1e3,
+                            "plant_rows": int(gr["n_rows"][0])}
+    if cpu:
+        import oracle
+
+        t0 = time.perf_counter()
+        o = oracle.mppi_closed_loop(pr, args[0][0], args[1][0], args[2][0], h2, u2, ms, configs.PLANT_DT_REF,
+                                    configs.GOAL_RADIUS_MPPI, obstacles=obs[0])
+        e3 = time.perf_counter() - t0
+        out["reference_run"]["cpu_baseline"] = {
+            "ms_total": e3 * 1e3, "replans": o["n_replans"], "cores": 1, "kind": "port",
+            "sample": "the same whole run (same Philox seed) on the scalar C oracle, 1 thread"}
     return out
 
 

@@ -179,6 +179,48 @@ int mp_rollout(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, int32_t K, const
 int mp_vehicle_euler(mp_ctx* ctx, int32_t n, double* states, const double* ctrl, double dt,
                      int32_t nsteps, double* his);
 
+/* Closed-loop driver settings (OptimalControl/MPPI/main.jl:14-19,55-83). */
+typedef struct mp_mppi_loop_params {
+  int32_t update_steps; /* plant steps per replan: update_idx = Int32(floor(update_time/δt)) (main.jl:19) */
+  int32_t max_steps;    /* plant steps of the run: Int32(floor(15/δt)) (main.jl:55)                     */
+  double plant_dt;      /* δt (main.jl:18)                                                           */
+  double goal_radius;   /* stop after the plant step that ends within this distance of goal (main.jl:80: 6) */
+  int32_t poll_every;   /* replans enqueued between host checks of the live-scene flags (0: 8)        */
+  int32_t reserved;
+} mp_mppi_loop_params;
+
+/*
+ * mp_mppi_closed_loop — the MPPI closed loop of OptimalControl/MPPI/main.jl:55-83 for S independent
+ * scenes (egos) in lockstep, entirely on the device.  Every update_steps plant steps (and at
+ * step 1): ShiftInitialCondition(mppi, states); defineMPPINominalControl!(mppi, NominalControls);
+ * MPPIPlan(mppi); NominalControls = mppi.r.Control.  Each plant step applies
+ * controls[i] = NominalControls[hold_idx[i] + 1, :] (0-based row hold_idx[i] of U; the caller's
+ * interpolate(time_serial, ·, Gridded(Constant{Previous}()))(fined_time_serial), main.jl:64-66),
+ * i = (time_idx − 1) mod update_steps, and states .+= VehicleDynamics(states, u)·δt (main.jl:74-75).
+ * A scene stops after the step whose (x, y) is within goal_radius of its goal (main.jl:77-79);
+ * the others go on.  Replan r of every scene uses Philox counter word p->offset + r (MP_NOISE_PHILOX)
+ * or the caller's z (MP_NOISE_EXTERNAL).  The final rollout of each plan runs on the side stream
+ * (p->final_stream is ignored), beside the plant.
+ *
+ * in : X0[S][7], goal[S][2], U_nom0[S][H][2] (NominalControls before the first plan),
+ *      obstacles[S][n_obs][3], grid[S][ny][nx] as mp_mppi_plan,
+ *      hold_idx[update_steps] (0-based rows of U, each in [0, H)),
+ *      noise[R][S][K][H][2] (MP_NOISE_EXTERNAL; R = ceil(max_steps / update_steps)) or NULL.
+ * out: his[S][max_steps+1][8]  states_his' rows [time_idx·δt, states...]; row 0 = [0, X0]
+ *      n_rows[S]               rows written (time steps run + 1)
+ *      n_replans[S]            MPPIPlan calls made for the scene
+ * optional (NULL to skip), per replan r < n_replans[s]:
+ *      U_log[S][R][H][2] (mppi.r.Control), traj_log[S][R][H+1][7] (mppi.r.Traj),
+ *      cost_log[S][R] (mppi.r.cost), feas_log[S][R] (mppi.r.Feasibility),
+ *      rc_log[S][R] (mppi.r.RolloutCount).
+ * Returns MP_ERR_NUMERIC (after writing outputs) if any rollout cost was NaN.
+ */
+int mp_mppi_closed_loop(mp_ctx* ctx, const mp_mppi_params* p, const mp_mppi_loop_params* lp, int32_t S,
+                        const double* X0, const double* goal, const double* U_nom0, const double* obstacles,
+                        const uint8_t* grid, const int32_t* hold_idx, const double* noise, double* his,
+                        int32_t* n_rows, int32_t* n_replans, double* U_log, double* traj_log, double* cost_log,
+                        int32_t* feas_log, int32_t* rc_log);
+
 /* ---------------------------------------------------------------- iLQR */
 #define MP_ILQR_NX 4 /* [x, y, ux, ψ]  OptimalControl/ILQR/Dynamics.jl:4-7 */
 #define MP_ILQR_NU 2 /* [ax, δ]                                          */

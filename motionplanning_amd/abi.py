@@ -74,6 +74,19 @@ class MPPIParams(ctypes.Structure):
     ]
 
 
+class MPPILoopParams(ctypes.Structure):
+    """mp_mppi_loop_params (include/mpgpu.h) — the closed-loop settings of MPPI/main.jl:14-19,55,80."""
+
+    _fields_ = [
+        ("update_steps", ctypes.c_int32),
+        ("max_steps", ctypes.c_int32),
+        ("plant_dt", ctypes.c_double),
+        ("goal_radius", ctypes.c_double),
+        ("poll_every", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
 class ILQRParams(ctypes.Structure):
     """mp_ilqr_params (include/mpgpu.h) — OptimalControl/ILQR/ILQR.jl:12-18 settings."""
 
@@ -127,6 +140,8 @@ SIGNATURES = {
     "mp_rollout": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), _I, _I, _V, _V, _V, ctypes.c_int64]
                    + [_V] * 7),
     "mp_vehicle_euler": (ctypes.c_int, [_V, _I, _V, _V, ctypes.c_double, _I, _V]),
+    "mp_mppi_closed_loop": (ctypes.c_int, [_V, ctypes.POINTER(MPPIParams), ctypes.POINTER(MPPILoopParams), _I]
+                            + [_V] * 15),
     "mp_ilqr_rollout": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
     "mp_ilqr_backward": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
     "mp_ilqr_forward": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I] + [_V] * 8),

@@ -43,6 +43,38 @@ def julia_linrange(a, b, n):
     return out
 
 
+# MPPI closed loop, OptimalControl/MPPI/main.jl:17-19,55,77
+UPDATE_TIME_REF = 0.1
+PLANT_DT_REF = 1e-3
+SIM_TIME_REF = 15.0
+GOAL_RADIUS_MPPI = 6.0
+
+
+def julia_range(a, b, n):
+    """collect(range(a, b, length=n)) for Float64 endpoints: Julia's StepRangeLen evaluates each
+    element in TwicePrecision, i.e. the correctly rounded a + (i-1)(b-a)/(n-1) (exact rationals here)."""
+    from fractions import Fraction
+
+    if n == 1:
+        return np.array([float(a)])
+    fa, fb = Fraction(float(a)), Fraction(float(b))
+    return np.array([float(fa + (fb - fa) * i / (n - 1)) for i in range(n)])
+
+
+def mppi_hold_index(T, N, update_time=UPDATE_TIME_REF, plant_dt=PLANT_DT_REF):
+    """The zero-order hold of MPPI/main.jl:51-52,64-66: update_idx = Int32(floor(update_time/δt)) plant
+    steps per replan, and step i of a period applies row j of NominalControls where
+    interpolate((time_serial,), ·, Gridded(Constant{Previous}())) picks the last knot
+    time_serial[j] <= fined_time_serial[i].  Returns (update_idx, 0-based rows [update_idx])."""
+    update_idx = int(math.floor(update_time / plant_dt))
+    ts = julia_range(0.0, T, N)
+    fs = julia_range(0.0, update_time, update_idx)
+    hold = np.array([int(np.searchsorted(ts, t, side="right")) - 1 for t in fs], np.int32)
+    if hold.min() < 0:
+        raise ValueError("fined_time_serial starts before time_serial")
+    return update_idx, hold
+
+
 def dwa_control_samples(CL=CL_DWA, CU=CU_DWA, counts=DWA_SAMPLES):
     """defineDWAcontrols! (DynamicWindow/src/setup.jl:59-94): sr-major, ax-minor grid."""
     v1 = julia_linrange(CL[0], CU[0], counts[0])

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 using namespace mpk;
@@ -83,6 +84,7 @@ struct PlanArgs {
   int inline_noise;                 // 1: Philox draws inside the rollout loop (no noise_prep pass)
   double* fin;                      // deferred final rollout: per-scene input snapshot (FinRec), or null
   int fin_stride;                   // doubles per scene record
+  const int* live;                  // closed loop: scenes with live[s] == 0 are skipped (null: all run)
 };
 
 // Snapshot record of one scene for the deferred final rollout (final_stream = 1), in doubles:
@@ -167,6 +169,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   const int k = b * RPB + pair;
   const bool active = k < K;
   const int kk = active ? k : K - 1;
+  if (A.live && A.live[s] == 0) return;  // closed loop: this scene has reached its goal (block-uniform)
   MP_STAMP(0);
   __builtin_amdgcn_s_setprio(3);
 
@@ -478,10 +481,11 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
 // rollouts already occupy the rest of the GPU.
 __global__ __launch_bounds__(64) void final_rollout_kernel(MppiDev P, const double* fin, int fin_stride,
                                                            int grid_lds, double* traj_out, double* cost_out,
-                                                           int* feas_out, int* flags) {
+                                                           int* feas_out, int* flags, const int* live) {
   extern __shared__ double fsh[];
   __shared__ double atab[20];
   const int s = blockIdx.x, tid = threadIdx.x, side = tid & 1, H = P.H;
+  if (live && live[s] == 0) return;  // closed loop: the plan kernel skipped this scene (no snapshot)
   const FinRec R(H, P.n_obs, P.gnx * P.gny);
   const double* rec = fin + (size_t)s * fin_stride;
   const int nw = grid_lds ? R.stride : R.grid;  // the grid stays in the record when it does not fit
@@ -587,6 +591,75 @@ __global__ __launch_bounds__(64) void euler_kernel(int n, double* states, const 
     for (int i = 0; i < 7; i++) states[7 * v + i] = x[i];
 }
 
+
+// ------------------------------------------------------- closed loop (plant)
+// One replan period of the MPPI closed loop (MPPI/main.jl:55-83) for every scene: the plant
+// `states .+= VehicleDynamics(states, u)·δt` for time_idx = step0+1 .. step0+nsub with the
+// zero-order-held control row hold[i] of this replan's MPPICtrl, one history row per step and
+// the goal check after it.  One lane pair per scene (dyn_pair); every lane runs the same trip
+// count (no divergent wave ops in the FDLIBM cores), a finished scene's lanes just stop writing.
+// rows: [S][max_steps+1][8] = [time_idx·δt, x...]; st[0..S) n_rows, st[S..2S) live,
+// st[2S..3S) n_replans.
+__global__ __launch_bounds__(64) void loop_plant_kernel(int S, int H, double* states, const double* U,
+                                                        const int* hold, int nsub, double dt, const double* goal,
+                                                        double r2, int step0, int max_steps, double* rows, int* st,
+                                                        int r) {
+  const int tid = blockIdx.x * 64 + threadIdx.x;
+  const int v = tid >> 1, side = tid & 1;
+  const int vv = v < S ? v : S - 1;
+  __shared__ double atab[20];
+  if (threadIdx.x == 0) mpj_atan_tab_init(atab);
+  __syncthreads();
+  int* n_rows = st;
+  int* live = st + S;
+  int* n_replans = st + 2 * S;
+  int act = v < S && live[vv];
+  const int act0 = act;
+  if (act && side == 0) n_replans[vv] = r + 1;
+  double x[7], d[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) x[i] = states[7 * vv + i];
+  const double g0 = goal[2 * vv], g1 = goal[2 * vv + 1];
+  double* row = rows + (size_t)vv * (max_steps + 1) * 8;
+  if (step0 == 0 && act && side == 0) {
+    row[0] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) row[1 + i] = x[i];
+  }
+  const double* u = U + (size_t)vv * H * 2;
+  int last = step0;
+  for (int i = 0; i < nsub; i++) {
+    const int t = step0 + i + 1;
+    if (t > max_steps) break;  // uniform: the run's time_idx range ends (main.jl:55)
+    const int h = hold[i];
+    dyn_pair(x, u[2 * h], u[2 * h + 1], d, side, atab);
+#pragma unroll
+    for (int k = 0; k < 7; k++) x[k] = x[k] + d[k] * dt;
+    if (act) {
+      last = t;
+      if (side == 0) {
+        double* q = row + (size_t)t * 8;
+        q[0] = (double)t * dt;
+#pragma unroll
+        for (int k = 0; k < 7; k++) q[1 + k] = x[k];
+      }
+      const double ex = x[0] - g0, ey = x[1] - g1;
+      if (ex * ex + ey * ey <= r2) {  // main.jl:77-79: break after this step's row
+        if (side == 0) live[vv] = 0;
+        act = 0;
+      }
+    }
+  }
+  if (act0 && side == 0) {
+    n_rows[vv] = last + 1;
+    if (act) {  // still running after the period: carry the state into the next replan
+#pragma unroll
+      for (int k = 0; k < 7; k++) states[7 * vv + k] = x[k];
+      if (last >= max_steps) live[vv] = 0;
+    }
+  }
+}
+
 // ----------------------------------------------------------------- host
 static void inv2(const double* A, double* Ai) {
   const double a = A[0], b = A[1], c = A[2], d = A[3];
@@ -661,7 +734,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
                        const double* U_nom, const double* obstacles, const uint8_t* grid, const double* noise,
                        double* U_out, double* traj_out, double* cost_out, int32_t* feasible_out,
                        int32_t* rc_out, int32_t* fc_out, double* coll_traj, double* coll_ctrl,
-                       double* coll_cost, uint8_t* coll_feas, int final_stream) {
+                       double* coll_cost, uint8_t* coll_feas, int final_stream, const int* live = nullptr) {
   const int K = D.K, H = D.H;
   // 8-wave blocks once the launch fills every CU with one (the dispatcher then places
   // exactly two waves per SIMD; with 4-wave blocks, two per CU, it can stack 3 + 1 and
@@ -685,6 +758,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   const int nb = (K + RPBh - 1) / RPBh;
   const int pstride = 4 + 2 * H;
   PlanArgs A;
+  A.live = live;
   A.X0 = X0; A.goal = goal; A.unom = U_nom; A.obs = D.n_obs > 0 ? obstacles : nullptr;
   A.grid = D.gnx > 0 ? grid : nullptr;
   static const bool noise_pass = getenv("MPGPU_NOISE_PASS") != nullptr;
@@ -812,7 +886,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     }
     MP_HIP(ctx, hipStreamWaitEvent(ctx->side, plan_done, 0));
     hipLaunchKernelGGL(final_rollout_kernel, dim3(S), dim3(64), fsh, ctx->side, D, A.fin, A.fin_stride, grid_lds,
-                       traj_out, cost_out, feasible_out, ctx->flags);
+                       traj_out, cost_out, feasible_out, ctx->flags, live);
     MP_HIP(ctx, hipGetLastError());
     MP_HIP(ctx, hipEventRecord(ctx->ev_fin[par], ctx->side));
   }
@@ -970,6 +1044,143 @@ int mp_mppi_plan(mp_ctx* ctx, const mp_mppi_params* p, int32_t S, const double* 
   if ((st = mp_download(ctx, &flag, ctx->flags, 1))) return st;
   MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (flag & 1) return mp_fail(ctx, MP_ERR_NUMERIC, "NaN rollout cost (Julia would have produced NaN weights)");
+  return MP_OK;
+}
+
+int mp_mppi_closed_loop(mp_ctx* ctx, const mp_mppi_params* p, const mp_mppi_loop_params* lp, int32_t S,
+                        const double* X0, const double* goal, const double* U_nom0, const double* obstacles,
+                        const uint8_t* grid, const int32_t* hold_idx, const double* noise, double* his,
+                        int32_t* n_rows, int32_t* n_replans, double* U_log, double* traj_log, double* cost_log,
+                        int32_t* feas_log, int32_t* rc_log) {
+  if (!ctx) return MP_ERR_INVALID;
+  MppiDev D;
+  int st = make_dev_params(ctx, p, p ? p->K : 0, &D);
+  if (st) return st;
+  MP_CHECK(ctx, lp != nullptr, "loop params is NULL");
+  MP_CHECK(ctx, S >= 1, "S (%d) must be >= 1", S);
+  MP_CHECK(ctx, lp->update_steps >= 1, "update_steps (%d) must be >= 1", lp->update_steps);
+  MP_CHECK(ctx, lp->max_steps >= 0, "max_steps (%d) must be >= 0", lp->max_steps);
+  MP_CHECK(ctx, lp->plant_dt > 0.0, "plant_dt (%g) must be > 0", lp->plant_dt);
+  MP_CHECK(ctx, X0 && goal && U_nom0 && hold_idx && his && n_rows && n_replans, "required pointer is NULL");
+  MP_CHECK(ctx, p->noise_mode != MP_NOISE_EXTERNAL || noise, "noise is NULL in MP_NOISE_EXTERNAL mode");
+  MP_CHECK(ctx, p->n_obs == 0 || obstacles, "obstacles NULL with n_obs > 0");
+  MP_CHECK(ctx, p->grid_nx == 0 || grid, "grid NULL with grid_nx > 0");
+  for (int i = 0; i < lp->update_steps; i++)
+    MP_CHECK(ctx, hold_idx[i] >= 0 && hold_idx[i] < p->H, "hold_idx[%d] = %d outside [0, H=%d)", i, hold_idx[i],
+             p->H);
+  MP_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t K = p->K, H = p->H, SS = S, nsub = lp->update_steps, M = lp->max_steps;
+  const int R = (int)((M + nsub - 1) / nsub);  // replans needed to cover the run
+  const size_t RR = R > 0 ? (size_t)R : 1;
+  st = MP_OK;
+  // device state: the plant states (= the next plan's X0), logs replan-major [R][S]...
+  double* dstate = (double*)mp_upload(ctx, WS_IO0, X0, 7 * SS, &st);
+  const double* dgoal = mp_upload(ctx, WS_IO1, goal, 2 * SS, &st);
+  const double* dU0 = mp_upload(ctx, WS_IO2, U_nom0, 2 * H * SS, &st);
+  const double* dobs = mp_upload(ctx, WS_IO3, p->n_obs ? obstacles : nullptr, 3 * (size_t)p->n_obs * SS, &st);
+  const uint8_t* dgrid = mp_upload(ctx, WS_IO4, p->grid_nx ? grid : nullptr, (size_t)p->grid_nx * p->grid_ny * SS, &st);
+  const double* dnoise =
+      mp_upload(ctx, WS_IO5, p->noise_mode == MP_NOISE_EXTERNAL ? noise : nullptr, RR * SS * K * H * 2, &st);
+  const int32_t* dhold = mp_upload(ctx, WS_IO15, hold_idx, nsub, &st);
+  double* dU = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * RR * SS * H * 2);
+  const size_t traj_n = (traj_log ? RR : 1) * SS * (H + 1) * 7;  // without a log: one scratch set
+  double* dtraj = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * traj_n);
+  double* dcost = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * RR * SS);
+  int32_t* dfeas = (int32_t*)mp_ws(ctx, WS_IO9, sizeof(int32_t) * RR * SS);
+  int32_t* drc = (int32_t*)mp_ws(ctx, WS_IO10, sizeof(int32_t) * RR * SS);
+  int32_t* dfc = (int32_t*)mp_ws(ctx, WS_IO11, sizeof(int32_t) * RR * SS);
+  double* drows = (double*)mp_ws(ctx, WS_IO12, sizeof(double) * SS * (M + 1) * 8);
+  int32_t* dst = (int32_t*)mp_ws(ctx, WS_IO13, sizeof(int32_t) * 3 * SS);  // n_rows | live | n_replans
+  int32_t* pin = (int32_t*)mp_pinned(ctx, sizeof(int32_t) * 2 * SS);
+  if (st || !dU || !dtraj || !dcost || !dfeas || !drc || !dfc || !drows || !dst) return st ? st : MP_ERR_NOMEM;
+  MP_CHECK(ctx, pin != nullptr, "pinned host buffer allocation failed");
+  MP_HIP(ctx, hipMemsetAsync(drows, 0, sizeof(double) * SS * (M + 1) * 8, ctx->stream));
+  {  // n_rows = 1, live = 1, n_replans = 0
+    std::vector<int32_t> init(3 * SS, 0);
+    for (size_t i = 0; i < SS; i++) init[i] = 1, init[SS + i] = M > 0 ? 1 : 0;
+    MP_HIP(ctx, hipMemcpyAsync(dst, init.data(), init.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (M == 0) {  // no plant step: the history is the start row only
+      std::vector<double> r0(SS * 8);
+      for (size_t s = 0; s < SS; s++) {
+        r0[8 * s] = 0.0;
+        for (int i = 0; i < 7; i++) r0[8 * s + 1 + i] = X0[7 * s + i];
+      }
+      MP_HIP(ctx, hipMemcpy2DAsync(drows, (M + 1) * 8 * sizeof(double), r0.data(), 8 * sizeof(double),
+                                   8 * sizeof(double), SS, hipMemcpyHostToDevice, ctx->stream));
+    }
+    MP_HIP(ctx, hipStreamSynchronize(ctx->stream));  // `init` leaves scope
+  }
+  MP_HIP(ctx, hipMemsetAsync(ctx->flags, 0, sizeof(int), ctx->stream));
+  int32_t* live = dst + SS;
+  const int poll = lp->poll_every > 0 ? lp->poll_every : 8;
+  const double r2 = lp->goal_radius * lp->goal_radius;
+  int pending = -1;  // pinned half holding the last poll's live flags (its copy is in flight)
+  hipEvent_t ev_poll[2];
+  MP_HIP(ctx, hipEventCreateWithFlags(&ev_poll[0], hipEventDisableTiming));
+  MP_HIP(ctx, hipEventCreateWithFlags(&ev_poll[1], hipEventDisableTiming));
+  int rc = MP_OK;
+  for (int r = 0; r < R; r++) {
+    MppiDev Dr = D;
+    Dr.offset = p->offset + (unsigned long long)r;  // a fresh Philox counter word per replan
+    const double* un = r == 0 ? dU0 : dU + (size_t)(r - 1) * SS * H * 2;  // NominalControls = r.Control
+    double* tr = dtraj + (traj_log ? (size_t)r * SS * (H + 1) * 7 : 0);
+    rc = plan_launch(ctx, Dr, S, dstate, dgoal, un, dobs, dgrid, dnoise ? dnoise + (size_t)r * SS * K * H * 2 : nullptr,
+                     dU + (size_t)r * SS * H * 2, tr, dcost + (size_t)r * SS, dfeas + (size_t)r * SS,
+                     drc + (size_t)r * SS, dfc + (size_t)r * SS, nullptr, nullptr, nullptr, nullptr, 1, live);
+    if (rc) break;
+    hipLaunchKernelGGL(loop_plant_kernel, dim3((unsigned)((2 * SS + 63) / 64)), dim3(64), 0, ctx->stream, S, (int)H,
+                       dstate, (const double*)(dU + (size_t)r * SS * H * 2), dhold, (int)nsub, lp->plant_dt, dgoal, r2,
+                       (int)(r * nsub), (int)M, drows, dst, r);
+    if (hipGetLastError() != hipSuccess) { rc = mp_fail(ctx, MP_ERR_HIP, "loop_plant_kernel launch failed"); break; }
+    if ((r + 1) % poll == 0 && r + 1 < R) {
+      // the previous poll's flags (one period behind, so the GPU stays fed while the host looks)
+      bool done = false;
+      if (pending >= 0) {
+        if (hipEventSynchronize(ev_poll[pending]) != hipSuccess) { rc = mp_fail(ctx, MP_ERR_HIP, "poll failed"); break; }
+        done = true;
+        for (size_t s = 0; s < SS; s++) done = done && pin[pending * SS + s] == 0;
+      }
+      if (done) break;
+      const int h = pending < 0 ? 0 : 1 - pending;
+      if (hipMemcpyAsync(pin + h * SS, live, sizeof(int32_t) * SS, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+          hipEventRecord(ev_poll[h], ctx->stream) != hipSuccess) {
+        rc = mp_fail(ctx, MP_ERR_HIP, "poll copy failed");
+        break;
+      }
+      pending = h;
+    }
+  }
+  if (!rc) rc = mp_ctx_join(ctx);  // the logged final rollouts come from the side stream
+  mp_sync_all(ctx);
+  hipEventDestroy(ev_poll[0]);
+  hipEventDestroy(ev_poll[1]);
+  if (rc) return rc;
+  // results: [S]-major host layouts
+  std::vector<int32_t> hst(3 * SS);
+  int flag = 0;
+  MP_HIP(ctx, hipMemcpy(hst.data(), dst, hst.size() * 4, hipMemcpyDeviceToHost));
+  MP_HIP(ctx, hipMemcpy(his, drows, sizeof(double) * SS * (M + 1) * 8, hipMemcpyDeviceToHost));
+  MP_HIP(ctx, hipMemcpy(&flag, ctx->flags, sizeof(int), hipMemcpyDeviceToHost));
+  for (size_t s = 0; s < SS; s++) {
+    n_rows[s] = hst[s];
+    n_replans[s] = hst[2 * SS + s];
+  }
+  auto gather = [&](auto* host, const auto* dev, size_t per) -> int {  // [R][S][per] -> [S][R][per]
+    if (!host || R == 0) return MP_OK;
+    using T = std::remove_cv_t<std::remove_pointer_t<decltype(dev)>>;
+    std::vector<T> tmp((size_t)R * SS * per);
+    MP_HIP(ctx, hipMemcpy(tmp.data(), dev, tmp.size() * sizeof(T), hipMemcpyDeviceToHost));
+    for (size_t s = 0; s < SS; s++)
+      for (int r = 0; r < R; r++)
+        for (size_t i = 0; i < per; i++) host[((size_t)s * R + r) * per + i] = tmp[((size_t)r * SS + s) * per + i];
+    return MP_OK;
+  };
+  if ((st = gather(U_log, dU, H * 2))) return st;
+  if ((st = gather(traj_log, dtraj, (H + 1) * 7))) return st;
+  if ((st = gather(cost_log, dcost, 1))) return st;
+  if ((st = gather(feas_log, dfeas, 1))) return st;
+  if ((st = gather(rc_log, drc, 1))) return st;
+  if (flag & 1) return mp_fail(ctx, MP_ERR_NUMERIC, "NaN rollout cost in the closed loop");
   return MP_OK;
 }
 

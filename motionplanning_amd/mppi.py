@@ -7,13 +7,14 @@ cost → weights → weighted control → final rollout) runs in one HIP launch 
 ``defineMPPINominalControl!`` are spelled with a trailing underscore.
 """
 import ctypes
+import math
 import time
 from dataclasses import dataclass, field
 
 import numpy as np
 
 from . import configs
-from .abi import MP_NOISE_EXTERNAL, MP_NOISE_PHILOX, MP_ERR_NUMERIC, MPPIParams, f64, ptr
+from .abi import MP_NOISE_EXTERNAL, MP_NOISE_PHILOX, MP_ERR_NUMERIC, MPPILoopParams, MPPIParams, f64, ptr
 from .context import default_context
 
 
@@ -75,6 +76,7 @@ class MPPIResult:
     time: float = 0.0
     FeasibleTrajCount: int = 0
     RolloutCount: int = 0
+    log: dict = None  # build extension: per-replan results of MPPIClosedLoop
 
 
 @dataclass
@@ -227,6 +229,82 @@ def MPPIPlan(mppi, noise=None, collect=True, ctx=None):
     r.FeasibleTrajCount = int(out["feasible_count"][0])
     r.time = time.time() - t1
     return None
+
+
+def mppi_closed_loop_batch(p: MPPIParams, X0, goal, U_nom0, hold, update_steps, max_steps, plant_dt, goal_radius,
+                           obstacles=None, grid=None, noise=None, logs=True, poll_every=0, ctx=None):
+    """S closed loops of MPPI/main.jl:55-83 in lockstep on the device (mp_mppi_closed_loop).
+    Shapes: X0 (S,7), goal (S,2), U_nom0 (S,H,2), hold (update_steps,) 0-based rows, noise (R,S,K,H,2)
+    or None (Philox, counter word p.offset + replan).  Returns his (S, max_steps+1, 8) with n_rows[s]
+    valid rows, n_replans (S,), and per-replan logs U (S,R,H,2), traj (S,R,H+1,7), cost, feasible,
+    rollout_count (S,R) valid for r < n_replans[s]."""
+    ctx = ctx or default_context()
+    X0 = f64(X0).reshape(-1, 7)
+    S, K, H = X0.shape[0], p.K, p.H
+    R = -(-int(max_steps) // int(update_steps))
+    goal = f64(goal, (S, 2))
+    U_nom0 = f64(U_nom0, (S, H, 2))
+    hold = np.ascontiguousarray(hold, np.int32).reshape(int(update_steps))
+    obstacles = None if obstacles is None or p.n_obs == 0 else f64(obstacles, (S, p.n_obs, 3))
+    grid = None if grid is None or p.grid_nx == 0 else np.ascontiguousarray(grid, np.uint8).reshape(
+        S, p.grid_ny, p.grid_nx)
+    if noise is not None:
+        noise = f64(noise, (R, S, K, H, 2))
+        p.noise_mode = MP_NOISE_EXTERNAL
+    else:
+        p.noise_mode = MP_NOISE_PHILOX
+    lp = MPPILoopParams(update_steps=int(update_steps), max_steps=int(max_steps), plant_dt=float(plant_dt),
+                        goal_radius=float(goal_radius), poll_every=int(poll_every))
+    out = dict(his=np.zeros((S, max_steps + 1, 8)), n_rows=np.zeros(S, np.int32), n_replans=np.zeros(S, np.int32))
+    Rl = max(R, 1)
+    lg = {}
+    if logs:
+        lg = dict(U=np.zeros((S, Rl, H, 2)), traj=np.zeros((S, Rl, H + 1, 7)), cost=np.zeros((S, Rl)),
+                  feasible=np.zeros((S, Rl), np.int32), rollout_count=np.zeros((S, Rl), np.int32))
+    st = ctx.lib.mp_mppi_closed_loop(ctx.handle, ctypes.byref(p), ctypes.byref(lp), S, ptr(X0), ptr(goal),
+                                     ptr(U_nom0), ptr(obstacles), ptr(grid), ptr(hold), ptr(noise), ptr(out["his"]),
+                                     ptr(out["n_rows"]), ptr(out["n_replans"]), ptr(lg.get("U")), ptr(lg.get("traj")),
+                                     ptr(lg.get("cost")), ptr(lg.get("feasible")), ptr(lg.get("rollout_count")))
+    out["nan"] = st == MP_ERR_NUMERIC
+    if st != MP_ERR_NUMERIC:
+        ctx.check(st)
+    out.update(lg)
+    return out
+
+
+def MPPIClosedLoop(mppi, update_time=configs.UPDATE_TIME_REF, δt=configs.PLANT_DT_REF, sim_time=configs.SIM_TIME_REF,
+                   goal_radius=configs.GOAL_RADIUS_MPPI, noise=None, ctx=None):
+    """The driver loop of OptimalControl/MPPI/main.jl:49-83 for the searcher's scene: replan every
+    update_idx plant steps from the current state with NominalControls = the previous r.Control,
+    hold the interpolated control, step the 1 kHz Euler plant, stop within goal_radius of the goal.
+    Returns states_his as rows [t, states...] (the transpose of the reference's 8×n matrix, i.e.
+    the MPPITrajectory.csv layout); mppi.r holds the last plan and mppi.r.log the per-replan
+    (Control, Traj, cost, Feasibility, RolloutCount)."""
+    s = mppi.s
+    t1 = time.time()
+    update_idx, hold = configs.mppi_hold_index(s.T, s.N, update_time, δt)
+    max_steps = int(math.floor(sim_time / δt))
+    p = params_of(mppi, MP_NOISE_EXTERNAL if noise is not None else MP_NOISE_PHILOX)
+    obst = np.asarray(s.obstacle_list, np.float64).reshape(1, -1, 3) if s.obstacle_list else None
+    grid = s.grid[None] if s.grid is not None else None
+    z = None if noise is None else np.asarray(noise, np.float64)[:, None]
+    out = mppi_closed_loop_batch(p, s.X0[None], s.goal[None], s.NominalControl[None], hold, update_idx, max_steps,
+                                 δt, goal_radius, obst, grid, z, ctx=ctx)
+    n, R = int(out["n_rows"][0]), int(out["n_replans"][0])
+    s.solve_counter += R
+    r = mppi.r
+    if R:
+        r.Traj = out["traj"][0, R - 1]
+        r.Control = out["U"][0, R - 1]
+        r.Feasibility = "Feasible" if out["feasible"][0, R - 1] else "InFeasible"
+        r.cost = float(out["cost"][0, R - 1])
+        r.RolloutCount = int(out["rollout_count"][0, R - 1])
+        s.X0 = out["his"][0, (R - 1) * update_idx, 1:].copy()
+        s.NominalControl = out["U"][0, R - 1].copy()
+    r.log = dict(Control=out["U"][0, :R], Traj=out["traj"][0, :R], cost=out["cost"][0, :R],
+                 Feasibility=out["feasible"][0, :R], RolloutCount=out["rollout_count"][0, :R])
+    r.time = time.time() - t1
+    return out["his"][0, :n]
 
 
 def TrajectoryRollout(mppi, ctrl_list, ctx=None):

@@ -51,6 +51,9 @@ def lib():
         L.or_mppi_plan.argtypes = [ctypes.POINTER(MPPIParams), ctypes.c_int] + [_V] * 16
         L.or_dwa_plan.restype = ctypes.c_int
         L.or_dwa_plan.argtypes = [ctypes.POINTER(MPPIParams), _V, _V, ctypes.c_int, _V, _V, _V, _V]
+        L.or_mppi_closed_loop.restype = ctypes.c_int
+        L.or_mppi_closed_loop.argtypes = [ctypes.POINTER(MPPIParams), ctypes.c_int, ctypes.c_int, ctypes.c_int, _D,
+                                          _D] + [_V] * 15
         L.or_vehicle_euler.restype = None
         L.or_vehicle_euler.argtypes = [_V, _V, _D, ctypes.c_int, _V]
         L.or_philox_normal2.restype = None
@@ -146,6 +149,35 @@ def vehicle_euler(states, ctrl, dt, nsteps, his=True):
     h = np.zeros((nsteps, 7)) if his else None
     lib().or_vehicle_euler(ptr(s), ptr(c), dt, nsteps, ptr(h))
     return s, h
+
+
+def mppi_closed_loop(p, X0, goal, unom0, hold, update_steps, max_steps, plant_dt, goal_radius, obstacles=None,
+                     grid=None, noise=None, scene=0):
+    """The MPPI closed loop of MPPI/main.jl:55-83 for one scene (or_mppi_closed_loop).
+    noise: (R, K, H, 2) standard normals per replan, or None for the Philox stream."""
+    K, H = p.K, p.H
+    R = -(-max_steps // update_steps)
+    X0 = np.ascontiguousarray(X0, np.float64)
+    goal = np.ascontiguousarray(goal, np.float64)
+    unom0 = np.ascontiguousarray(unom0, np.float64).reshape(H, 2)
+    hold = np.ascontiguousarray(hold, np.int32)
+    obstacles = None if obstacles is None else np.ascontiguousarray(obstacles, np.float64)
+    grid = None if grid is None else np.ascontiguousarray(grid, np.uint8)
+    noise = None if noise is None else np.ascontiguousarray(noise, np.float64).reshape(R, K, H, 2)
+    his = np.zeros((max_steps + 1, 8))
+    Rl = max(R, 1)
+    out = dict(U=np.zeros((Rl, H, 2)), traj=np.zeros((Rl, H + 1, 7)), cost=np.zeros(Rl),
+               feasible=np.zeros(Rl, np.int32), rollout_count=np.zeros(Rl, np.int32))
+    nr, npl = ctypes.c_int(), ctypes.c_int()
+    nan = lib().or_mppi_closed_loop(ctypes.byref(p), scene, update_steps, max_steps, plant_dt, goal_radius,
+                                    ptr(hold), ptr(X0), ptr(goal), ptr(unom0), ptr(obstacles), ptr(grid), ptr(noise),
+                                    ptr(his), ctypes.addressof(nr), ctypes.addressof(npl), ptr(out["U"]),
+                                    ptr(out["traj"]), ptr(out["cost"]), ptr(out["feasible"]),
+                                    ptr(out["rollout_count"]))
+    n = npl.value
+    out = {k: v[:n] for k, v in out.items()}
+    out.update(his=his[:nr.value], n_rows=nr.value, n_replans=n, nan=bool(nan))
+    return out
 
 
 def philox_normal2(seed, offset, scene, k, h):

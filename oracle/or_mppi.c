@@ -333,6 +333,70 @@ void or_vehicle_euler(double* states, const double* ctrl, double dt, int nsteps,
   }
 }
 
+/*
+ * The MPPI closed loop, OptimalControl/MPPI/main.jl:55-83, one scene.  Replan when
+ * mod(time_idx - 1, update_idx) + 1 == 1 (:58): ShiftInitialCondition + NominalControl +
+ * MPPIPlan (:59-61), NominalControls = r.Control (:62); the held control of plant step i of the
+ * period is row hold[i] of it (the Constant{Previous} interpolation, :64-66); the plant
+ * states .+= VehicleDynamics(states, u)*δt (:74-75); row [time_idx*δt; states] (:76); stop when
+ * within the goal radius (:77-79).  noise: [R][K][H][2] for this scene or NULL (Philox with
+ * counter word p->offset + replan).  Outputs as mp_mppi_closed_loop for one scene; logs are
+ * [R][...].  Returns 1 if any plan met a NaN cost.
+ */
+int or_mppi_closed_loop(const mp_mppi_params* p, int scene, int update_steps, int max_steps, double dt,
+                        double goal_radius, const int* hold, const double* X0, const double* goal,
+                        const double* unom0, const double* obs, const uint8_t* grid, const double* noise,
+                        double* his, int* n_rows, int* n_replans, double* U_log, double* traj_log,
+                        double* cost_log, int* feas_log, int* rc_log) {
+  const int H = p->H, K = p->K;
+  const int R = (max_steps + update_steps - 1) / update_steps;
+  const double r2 = goal_radius * goal_radius;
+  mp_mppi_params q = *p;
+  double states[7], ds[7];
+  double* nominal = (double*)malloc(sizeof(double) * 2 * H);
+  double* U = (double*)malloc(sizeof(double) * 2 * H);
+  double* traj = (double*)malloc(sizeof(double) * 7 * (H + 1));
+  memcpy(nominal, unom0, sizeof(double) * 2 * H);
+  memcpy(states, X0, sizeof(states));
+  his[0] = 0.0;
+  memcpy(his + 1, X0, sizeof(double) * 7);
+  int rows = 1, plans = 0, nan_seen = 0;
+  for (int t = 1; t <= max_steps; t++) {
+    const int i = (t - 1) % update_steps;
+    if (i == 0) {
+      const int r = plans++;
+      double cost;
+      int feas, rc, fc;
+      q.offset = p->offset + (uint64_t)r;
+      nan_seen |= or_mppi_plan(&q, scene, states, goal, nominal, obs, grid,
+                               noise ? noise + (size_t)r * K * H * 2 : NULL, U, traj, &cost, &feas, &rc, &fc,
+                               NULL, NULL, NULL, NULL);
+      memcpy(nominal, U, sizeof(double) * 2 * H);
+      if (U_log) memcpy(U_log + (size_t)r * 2 * H, U, sizeof(double) * 2 * H);
+      if (traj_log) memcpy(traj_log + (size_t)r * 7 * (H + 1), traj, sizeof(double) * 7 * (H + 1));
+      if (cost_log) cost_log[r] = cost;
+      if (feas_log) feas_log[r] = feas;
+      if (rc_log) rc_log[r] = rc;
+    }
+    const double* u = nominal + 2 * hold[i];
+    or_vehicle_dynamics(states, u, ds);
+    for (int k = 0; k < 7; k++) states[k] = states[k] + ds[k] * dt;
+    double* row = his + (size_t)t * 8;
+    row[0] = (double)t * dt;
+    memcpy(row + 1, states, sizeof(double) * 7);
+    rows = t + 1;
+    const double ex = states[0] - goal[0], ey = states[1] - goal[1];
+    if (ex * ex + ey * ey <= r2) break;
+  }
+  (void)R;
+  *n_rows = rows;
+  *n_replans = plans;
+  free(nominal);
+  free(U);
+  free(traj);
+  return nan_seen;
+}
+
 /* Scalar math entry points for tests/test_jlmath.py. */
 double or_m_sin(double x) { return mpj_sin(x); }
 double or_m_cos(double x) { return mpj_cos(x); }

@@ -1,0 +1,118 @@
+"""GPU parity: the MPPI closed loop (mp_mppi_closed_loop, OptimalControl/MPPI/main.jl:55-83).
+
+Checked per replan, so the comparison does not accumulate drift:
+  * plant rows (1 kHz Euler of VehicleDynamics with the held control): BIT-EXACT vs the oracle's
+    or_vehicle_euler started from the device's own row at the replan;
+  * each replan's MPPIPlan vs the oracle's from the device's X0 and nominal control:
+    RolloutCount exact, MPPICtrl rtol 1e-9 / atol 1e-12, final-rollout cost rtol 1e-9 and
+    Feasibility exact (same tolerances as tests/test_gpu_mppi.py);
+  * end to end vs the oracle's own closed loop: same number of rows and replans, states within
+    1e-6 (the MPPICtrl rounding differences, ~1e-15, pass through up to 15 replans of feedback).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from motionplanning_amd import configs
+from motionplanning_amd.mppi import mppi_closed_loop_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _scenes(S, seed=5):
+    r = np.random.default_rng(seed)
+    X0 = np.tile(np.array(configs.X0_REF), (S, 1))
+    X0[:, 1] = r.uniform(-1, 1, S)
+    X0[:, 5] = r.uniform(5, 8, S)
+    goal = np.c_[r.uniform(6, 12, S), r.uniform(-1, 1, S)]
+    obs = np.stack([np.array(configs.OBSTACLES_REF) - [40.0 - 4 * s, 0, 0] for s in range(S)])
+    return X0, goal, obs
+
+
+def _run(S=3, K=128, H=20, upd=100, max_steps=1450, poll=0, radius=3.0, seed=5):
+    p = configs.mppi_params(K=K, H=H, T=3.0, n_obs=3)
+    X0, goal, obs = _scenes(S, seed)
+    hold = np.zeros(upd, np.int32)
+    hold[upd // 2:] = 1  # a two-row hold exercises the interpolation table
+    R = -(-max_steps // upd)
+    z = np.random.default_rng(seed + 1).standard_normal((R, S, K, H, 2))
+    U0 = np.zeros((S, H, 2))
+    U0[:, :, 1] = 0.3
+    g = mppi_closed_loop_batch(p, X0, goal, U0, hold, upd, max_steps, 1e-3, radius, obs, None, z, poll_every=poll)
+    return p, X0, goal, obs, hold, z, U0, g
+
+
+def test_closed_loop_per_replan_parity(ctx):
+    S, upd = 3, 100
+    p, X0, goal, obs, hold, z, U0, g = _run(S=S, upd=upd)
+    assert not g["nan"]
+    for s in range(S):
+        n, R = int(g["n_rows"][s]), int(g["n_replans"][s])
+        his = g["his"][s]
+        assert R == -(-(n - 1) // upd)
+        np.testing.assert_array_equal(his[0], np.r_[0.0, X0[s]])
+        for r in range(R):
+            x0 = his[r * upd, 1:]
+            un = U0[s] if r == 0 else g["U"][s, r - 1]
+            ref = oracle.mppi_plan(p, x0, goal[s], un, obs[s], None, z[r, s])
+            np.testing.assert_allclose(g["U"][s, r], ref["U"], rtol=1e-9, atol=1e-12)
+            assert int(g["rollout_count"][s, r]) == ref["rollout_count"]
+            np.testing.assert_allclose(g["cost"][s, r], ref["cost"], rtol=1e-9)
+            assert bool(g["feasible"][s, r]) == ref["feasible"]
+            np.testing.assert_allclose(g["traj"][s, r], ref["traj"], rtol=1e-9, atol=1e-9)
+            # the plant over this period, bit for bit, from the device's own row and control
+            state = x0.copy()
+            t0 = r * upd
+            for i in range(min(upd, n - 1 - t0)):
+                state, _ = oracle.vehicle_euler(state, g["U"][s, r, hold[i]], 1e-3, 1, his=False)
+                row = his[t0 + i + 1]
+                assert row[0] == (t0 + i + 1) * 1e-3
+                assert np.array_equal(row[1:], state), (s, r, i)
+        if n - 1 < 1450:  # stopped at the goal: the last row is inside the radius, the one before is not
+            d2 = lambda q: (q[1] - goal[s, 0]) ** 2 + (q[2] - goal[s, 1]) ** 2
+            assert d2(his[n - 1]) <= 9.0 and d2(his[n - 2]) > 9.0
+
+
+def test_closed_loop_matches_oracle_loop(ctx):
+    S, upd, max_steps = 3, 100, 1450
+    p, X0, goal, obs, hold, z, U0, g = _run(S=S, upd=upd, max_steps=max_steps)
+    stops = []
+    for s in range(S):
+        ref = oracle.mppi_closed_loop(p, X0[s], goal[s], U0[s], hold, upd, max_steps, 1e-3, 3.0, obstacles=obs[s],
+                                      noise=z[:, s])
+        n = int(g["n_rows"][s])
+        assert n == ref["n_rows"] and int(g["n_replans"][s]) == ref["n_replans"]
+        np.testing.assert_allclose(g["his"][s, :n], ref["his"], rtol=0, atol=1e-6)
+        np.testing.assert_array_equal(g["rollout_count"][s, :ref["n_replans"]], ref["rollout_count"])
+        stops.append(n)
+    assert len(set(stops)) > 1, "scenes should finish at different steps (lockstep with early exits)"
+
+
+def test_closed_loop_poll_and_partial_period(ctx):
+    """A run length that ends mid-period (1000 steps, 70 per replan: the 15th replan drives 20 steps),
+    and host polling after every replan (poll_every = 1: the loop stops enqueueing once every scene
+    is done) giving the same rows as the default polling."""
+    a = _run(S=2, upd=70, max_steps=1000, poll=1, radius=0.0)[-1]
+    np.testing.assert_array_equal(a["n_rows"], [1001, 1001])
+    np.testing.assert_array_equal(a["n_replans"], [15, 15])
+    b = _run(S=2, upd=70, max_steps=4000, poll=1, radius=3.0)[-1]
+    c = _run(S=2, upd=70, max_steps=4000, poll=0, radius=3.0)[-1]
+    assert int(b["n_rows"].max()) < 4001, "every scene should reach its goal early"
+    for k in ("n_rows", "n_replans"):
+        np.testing.assert_array_equal(b[k], c[k])
+    np.testing.assert_array_equal(b["his"], c["his"])
+
+
+def test_closed_loop_philox_reference_settings(ctx):
+    """MPPI/main.jl settings (K=1500, N=20, update every 100 steps) with device noise: the GPU loop
+    equals the oracle's Philox loop for the first 0.5 s (5 replans) to 1e-9."""
+    p = configs.mppi_params(K=1500, H=20, T=3.0, n_obs=3, seed=7)
+    upd, hold = configs.mppi_hold_index(3.0, 20)
+    X0, goal = np.array(configs.X0_REF), np.array(configs.GOAL_REF)
+    obs = np.array(configs.OBSTACLES_REF)
+    g = mppi_closed_loop_batch(p, X0[None], goal[None], np.zeros((1, 20, 2)), hold, upd, 500, 1e-3, 6.0,
+                               obs[None])
+    ref = oracle.mppi_closed_loop(p, X0, goal, np.zeros((20, 2)), hold, upd, 500, 1e-3, 6.0, obstacles=obs)
+    assert int(g["n_rows"][0]) == 501 and int(g["n_replans"][0]) == 5
+    np.testing.assert_allclose(g["his"][0], ref["his"], rtol=0, atol=1e-9)
+    np.testing.assert_array_equal(g["rollout_count"][0], ref["rollout_count"])
