@@ -36,3 +36,5 @@ for B in (1, 16, 256):
                                                    ptr(ok), ptr(path), ptr(ln)))
             ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
         print(f"B={B:4d} {what:6s} kernel {ms.value * 1e3:9.1f} us", flush=True)
+    print(f"B={B:4d} free neighbours {fr.mean():.3f} of 62 per node; groups with any free "
+          f"{np.mean([fr[b, g * 16:(g + 1) * 16].any() for b in range(B) for g in range(4)]):.3f}", flush=True)
