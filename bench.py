@@ -199,6 +199,13 @@ def main():
                 "insts_per_launch": tr["valu_insts"], "achieved": rate, "peak": peak, "unit": "wave-insts/s",
                 "frac": rate / peak, "source": tr["source"] + " SQ_INSTS_VALU",
             }
+            if tr.get("valu_active") and tr.get("wave_cycles") and tr.get("waves"):
+                # measured, clock-independent: the share of each SIMD's time its waves spend issuing VALU
+                # instructions = (VALU-issue quad-cycles / wave quad-cycles) x waves per SIMD
+                out["roofline"]["valu"]["simd_busy"] = (tr["valu_active"] / tr["wave_cycles"]
+                                                        * tr["waves"] / VALU_SIMDS)
+                out["roofline"]["valu"]["simd_busy_source"] = (tr["source"] + " SQ_ACTIVE_INST_VALU / "
+                                                               "SQ_WAVE_CYCLES x SQ_WAVES / 1024 SIMDs")
     if not a.no_single and S != 1:
         e1, k1, ok1, _, _, _ = run(a, 1, ctx, dev, world, rank, a.steps, a.warmup, 12)
         out["single_scene"] = {
@@ -230,7 +237,8 @@ def load_traffic(path, S, K, H):
     if "traffic_bytes" not in e or d.get("config") != {"S": S, "K": K, "H": H}:
         return None
     return {"traffic_bytes": e["traffic_bytes"], "valu_insts": e.get("SQ_INSTS_VALU"),
-            "source": os.path.relpath(path, ROOT)}
+            "valu_active": e.get("SQ_ACTIVE_INST_VALU"), "wave_cycles": e.get("SQ_WAVE_CYCLES"),
+            "waves": e.get("SQ_WAVES"), "source": os.path.relpath(path, ROOT)}
 
 
 def _sync_max(x, world, dev):
