@@ -58,6 +58,18 @@ MPJ_FN double mpj_fabs(double x) { return __builtin_fabs(x); }
 MPJ_FN int mpj_isnan(double x) { return x != x; }
 /* Julia `round(::Float64)` = RoundNearest (ties to even) = rint in the default mode. */
 MPJ_FN double mpj_round(double x) { return __builtin_rint(x); }
+/* Julia `max` / `min` for Float64 (base/math.jl): NaN-propagating (C fmax/fmin drop a NaN operand)
+ * and -0.0 < +0.0:  max(x, y) = ifelse((y > x) | (signbit(y) < signbit(x)), ifelse(isnan(x), x, y),
+ * ifelse(isnan(y), y, x)), min with < and > swapped. */
+MPJ_FN int mpj_signbit(double x) { return (int)(mpj_hi(x) >> 31); }
+MPJ_FN double mpj_jmax(double x, double y) {
+  const int ty = (y > x) | (mpj_signbit(y) < mpj_signbit(x));
+  return ty ? (mpj_isnan(x) ? x : y) : (mpj_isnan(y) ? y : x);
+}
+MPJ_FN double mpj_jmin(double x, double y) {
+  const int ty = (y < x) | (mpj_signbit(y) > mpj_signbit(x));
+  return ty ? (mpj_isnan(x) ? x : y) : (mpj_isnan(y) ? y : x);
+}
 
 /* ---------------------------------------------------------------- sin/cos */
 /* FDLIBM k_sin.c / k_cos.c (Julia base/special/trig.jl sin_kernel/cos_kernel). */

@@ -225,13 +225,17 @@ __device__ __forceinline__ void philox_normal2(const MppiDev& P, unsigned scene,
   z[1] = rr * sn;
 }
 
-// SampleMPPIControl + PushInBounds (MPPIUtils.jl:5-20): u = clamp(u_nom + L z, CL, CU)
+// SampleMPPIControl + PushInBounds (MPPIUtils.jl:5-20): u = min(max(u_nom + L z, CL), CU) with Julia's
+// min / max (mpj_jmin / mpj_jmax): v_max_f64 / v_min_f64 already order -0.0 < +0.0, so only a NaN
+// sample needs the select that keeps it NaN (the IEEE maxNum/minNum drop it).
 __device__ __forceinline__ void sample_ctrl(const MppiDev& P, const double* z, const double* un, double* u) {
   const double n0 = P.L[0] * z[0];
   const double n1 = P.L[3] * z[1] + P.L[2] * z[0];
   const double v0 = n0 + un[0], v1 = n1 + un[1];
-  u[0] = __builtin_fmin(__builtin_fmax(v0, P.CL[0]), P.CU[0]);
-  u[1] = __builtin_fmin(__builtin_fmax(v1, P.CL[1]), P.CU[1]);
+  const double c0 = __builtin_fmin(__builtin_fmax(v0, P.CL[0]), P.CU[0]);
+  const double c1 = __builtin_fmin(__builtin_fmax(v1, P.CL[1]), P.CU[1]);
+  u[0] = v0 != v0 ? v0 : c0;
+  u[1] = v1 != v1 ? v1 : c1;
 }
 
 __device__ __forceinline__ void draw_ctrl(const MppiDev& P, const double* noise_s, const double* unom_s,

@@ -217,14 +217,15 @@ void or_philox_normal2(uint64_t seed, uint64_t offset, uint32_t scene, uint32_t 
   z[1] = rr * sn;
 }
 
-/* SampleMPPIControl + PushInBounds, MPPIUtils.jl:5-20: u = clamp(u_nom + L z). */
+/* SampleMPPIControl + PushInBounds, MPPIUtils.jl:5-20: u = min(max(u_nom + L z, CL), CU) with
+ * Julia's min / max (a NaN sample stays NaN; -0.0 < +0.0). */
 static void sample_ctrl(const mp_mppi_params* p, const double* L, const double* unom,
                         const double* z, double* u) {
   double n0 = L[0] * z[0];
   double n1 = L[3] * z[1] + L[2] * z[0];
   double v0 = n0 + unom[0], v1 = n1 + unom[1];
-  u[0] = fmin(fmax(v0, p->CL[0]), p->CU[0]);
-  u[1] = fmin(fmax(v1, p->CL[1]), p->CU[1]);
+  u[0] = mpj_jmin(mpj_jmax(v0, p->CL[0]), p->CU[0]);
+  u[1] = mpj_jmin(mpj_jmax(v1, p->CL[1]), p->CU[1]);
 }
 
 /*
