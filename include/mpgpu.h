@@ -325,6 +325,23 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                int32_t* n_nodes, int64_t* pop_seq, int32_t* n_states, double* states_out,
                int32_t* rs_len, double* rs_path);
 
+/* retrievePath + cubic_fit (PathPlanning/HybridAstar/src/hybrid_astar_utils.jl:100-177) for B planned
+ * scenarios, one block each: actualpath = [starting_states, cubic_fit(states[:,i], states[:,i+1]) (100
+ * points each, i over the hybrid_astar_states reversed to start -> goal order), RSpath_final], its
+ * cumulative arc length path_length, tol_length = path_length[end], and the 50 samples of
+ * x/y/ψ_interp_dense at LinRange(0, tol_length, 50) that x/y/ψ_interp are built on.
+ * in : start[B][3] (starting_states), n_states[B] and states[B][state_stride][3] as mp_ha_plan returns
+ *      them (goal side first; n_states = 0: nothing found, nothing retrieved), rs_len[B],
+ *      rs_path[B][501][3] (RSpath_final).
+ * out: n_points[B] = 1 + 100 (n_states - 1) + rs_len (0 if n_states = 0), tol_length[B],
+ *      samples[B][50][3] (x, y, ψ at the 50 arc-length knots).
+ * optional (all NULL or path_offset given): path_offset[B+1] (written: scenario b's points are
+ *      [path_offset[b], path_offset[b+1])), actualpath[path_offset[B]][3], path_length[path_offset[B]]. */
+int mp_ha_retrieve_path(mp_ctx* ctx, int32_t B, const double* start, const int32_t* n_states, const double* states,
+                        int32_t state_stride, const int32_t* rs_len, const double* rs_path, int64_t* path_offset,
+                        double* actualpath, double* path_length, int32_t* n_points, double* tol_length,
+                        double* samples);
+
 /* ---------------------------------------------------------- diagnostics */
 /* Evaluate one include/mp_jlmath.h function on the device for n inputs
  * (bit-exactness check against the CPU build).  fn: 0 sin, 1 cos, 2 tan, 3 atan,

@@ -22,10 +22,10 @@ points are exercised from Python ctypes by tests/ with identical layouts.
 """
 module MPGPU
 
-using Interpolations: interpolate, Gridded, Constant, Previous   # as OptimalControl/MPPI/main.jl:3
+using Interpolations: interpolate, Gridded, Constant, Previous, linear_interpolation   # as the reference drivers
 
 export MPPIPlan, MPPIClosedLoop, planHybridAstar!, mppi_plan_batch, mppi_closed_loop_batch, rollout_batch, ha_expand, ha_rs_connect,
-       ha_allpath, ilqr_backward!, ilqr_forward!, ilqr_solve!
+       ha_allpath, retrieve_batch!, ilqr_backward!, ilqr_forward!, ilqr_solve!
 
 const libmpgpu = get(ENV, "MPGPU_LIB", joinpath(@__DIR__, "..", "motionplanning_amd", "lib", "libmpgpu.so"))
 
@@ -345,6 +345,48 @@ end
 
 """Batched FindNewNode device part for B popped nodes (3, B): neighbour states (3, n, B),
 Encode indices (n, B) (0 = out of bounds), collision-free flags (n, B), rs heuristics (n, B)."""
+"""
+    retrieve_batch!(has)
+
+retrievePath (hybrid_astar_utils.jl:129-177, with cubic_fit :100-127) for planned searchers in one launch
+(mp_ha_retrieve_path): sets `r.actualpath` (3 × L), `r.tol_length` and `r.x_interp`, `r.y_interp`,
+`r.ψ_interp` = `linear_interpolation(LinRange(0, tol_length, 50), samples)` as the reference builds them.
+Pass it as `plan_batch!(has; retrieve = nothing)` then call this once for the whole batch (the
+reference's own `retrievePath` per searcher stays available through `retrieve = retrievePath`).
+"""
+function retrieve_batch!(has::AbstractVector)
+    B = length(has)
+    ok(h) = h.r.hybrid_astar_states !== nothing && size(h.r.hybrid_astar_states, 2) > 0
+    ns = Int32[ok(h) ? size(h.r.hybrid_astar_states, 2) : 0 for h in has]
+    stride = max(1, maximum(ns))
+    start = reduce(hcat, [Float64.(h.s.starting_states) for h in has])
+    states = zeros(3, stride, B); rl = zeros(Int32, B); rs = zeros(3, 501, B)
+    for (b, h) in enumerate(has)
+        ns[b] == 0 && continue
+        states[:, 1:ns[b], b] = h.r.hybrid_astar_states
+        rl[b] = size(h.r.RSpath_final, 2)
+        rs[:, 1:rl[b], b] = h.r.RSpath_final
+    end
+    tot = sum(n == 0 ? 0 : 1 + 100 * (n - 1) + r for (n, r) in zip(ns, rl))
+    off = zeros(Int64, B + 1); pts = zeros(3, max(tot, 1)); plen = zeros(max(tot, 1))
+    np_ = zeros(Int32, B); tol = zeros(B); smp = zeros(3, 50, B)
+    c = ctx()
+    check(GC.@preserve start ns states rl rs off pts plen np_ tol smp ccall((:mp_ha_retrieve_path, libmpgpu), Cint,
+        (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Int32, Ptr{Int32}, Ptr{Float64}, Ptr{Int64},
+         Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}),
+        c, B, start, ns, states, stride, rl, rs, off, pts, plen, np_, tol, smp), c)
+    for (b, h) in enumerate(has)
+        ns[b] == 0 && continue
+        h.r.actualpath = pts[:, off[b]+1:off[b+1]]
+        h.r.tol_length = tol[b]
+        knots = LinRange(0, tol[b], 50)
+        h.r.x_interp = linear_interpolation(knots, smp[1, :, b])
+        h.r.y_interp = linear_interpolation(knots, smp[2, :, b])
+        h.r.ψ_interp = linear_interpolation(knots, smp[3, :, b])
+    end
+    return has
+end
+
 function ha_expand(p::HaParams, node::Matrix{Float64}, goal::Matrix{Float64}, walls::Array{Float64,3})
     B = size(node, 2); n = Int(p.n_prim)
     nb = zeros(3, n, B); idx = zeros(Int64, n, B); fr = zeros(UInt8, n, B); h = zeros(n, B)

@@ -1062,6 +1062,146 @@ __global__ __launch_bounds__(BKT) void ha_book_kernel(HaDev P, HaSearch Q, IterA
 }
 
 
+
+// ------------------------------------------------------------- path finishing
+// retrievePath + cubic_fit (hybrid_astar_utils.jl:100-177) for a planned scenario, one block each:
+// the start state, a 100-point cubic between every pair of consecutive hybrid_astar_states (reversed
+// to start -> goal order) and RSpath_final make actualpath; its cumulative arc length and the 50
+// samples of the re-interpolated path at LinRange(0, tol_length, 50) (x_interp, y_interp, ψ_interp).
+constexpr int RFIT = 100;  // num_path of cubic_fit (:101)
+constexpr int RSAMP = 50;  // steps of retrievePath (:167)
+constexpr int RT = 256;
+
+// cubic_fit's coefficients (:101-111): [xg³ xg²; 3xg² 2xg] \ (pinv) [yg; tan ψg] in the frame of `cur`.
+// pinv through the closed-form 2x2 SVD of the iLQR sweep (oracle/or_ilqr.c or_pinv2).
+__device__ __forceinline__ void cubic_params(const double* cur, const double* nxt, double* out) {
+  double ns[3];
+  change_basis(cur, nxt, 1.0, ns);
+  const double xg = ns[0], yg = ns[1], pg = ns[2];
+  const double M[4] = {xg * xg * xg, xg * xg, 3 * (xg * xg), 2 * xg};
+  const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
+  const double Q = mpj_sqrt(E * E + H * H), R = mpj_sqrt(F * F + G * G);
+  const double sx = Q + R, sy = Q - R;
+  const double a1 = mpj_atan2(G, F), a2 = mpj_atan2(H, E);
+  const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
+  double st, ct, sp, cp;
+  mpj_sincos(th, &st, &ct);
+  mpj_sincos(ph, &sp, &cp);
+  const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
+  const double tol = 4.440892098500626e-16 * smax;
+  const double i1 = __builtin_fabs(sx) > tol ? 1.0 / sx : 0.0;
+  const double i2 = __builtin_fabs(sy) > tol ? 1.0 / sy : 0.0;
+  const double P0 = ct * i1 * cp - st * i2 * sp, P1 = ct * i1 * sp + st * i2 * cp;
+  const double P2 = -st * i1 * cp - ct * i2 * sp, P3 = -st * i1 * sp + ct * i2 * cp;
+  const double b0 = yg, b1 = mpj_tan(pg);
+  out[0] = P0 * b0 + P1 * b1;
+  out[1] = P2 * b0 + P3 * b1;
+  out[2] = xg;
+}
+
+// Point k of cubic_fit(cur, ·) (:113-126): x = LinRange(0, xg, 100)[k], y = p1·x³ + p2·x², ψ = atan(3p1·x² +
+// 2p2·x), rotated by ψ0 (Rmat·path .+ [x0; y0]) and ψ + ψ0.
+__device__ __forceinline__ void cubic_point(const double* cur, const double* prm, int k, double* o) {
+  const double t = (double)k / (RFIT - 1);
+  const double x = (1 - t) * 0.0 + t * prm[2];
+  const double y = prm[0] * (x * x * x) + prm[1] * (x * x);
+  const double psi = mpj_atan((3 * prm[0]) * (x * x) + (2 * prm[1]) * x);
+  double s0, c0;
+  mpj_sincos(cur[2], &s0, &c0);
+  o[0] = (c0 * x + (-s0) * y) + cur[0];
+  o[1] = (s0 * x + c0 * y) + cur[1];
+  o[2] = psi + cur[2];
+}
+
+// pts[off..][3] / plen[off..]: the dense actualpath and its arc length (the host sizes the ragged
+// buffers from n_states and rs_len); seg[b][segstride][3]: cubic_params per segment.
+__global__ __launch_bounds__(RT) void ha_retrieve_kernel(const double* start, const int* n_states,
+                                                         const double* states, int sstride, const int* rs_len,
+                                                         const double* rs_path, const long long* off, double* pts,
+                                                         double* plen, double* seg, int segstride, int* npts,
+                                                         double* tol, double* samples) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int n = n_states[b];
+  double* smp = samples + (size_t)b * RSAMP * 3;
+  if (n < 1) {  // not found: planHybridAstar! leaves no path to retrieve
+    if (tid == 0) {
+      npts[b] = 0;
+      tol[b] = 0.0;
+    }
+    for (int i = tid; i < RSAMP * 3; i += RT) smp[i] = 0.0;
+    return;
+  }
+  const int nseg = n - 1, nr = rs_len[b];
+  const int L = 1 + RFIT * nseg + nr;
+  double* P = pts + off[b] * 3;
+  double* S = plen + off[b];
+  const double* st = states + (size_t)b * sstride * 3;  // goal side first: start->goal state i = st[n-1-i]
+  double* sg = seg + (size_t)b * segstride * 3;
+  for (int t = tid; t < nseg; t += RT) cubic_params(st + 3 * (n - 1 - t), st + 3 * (n - 2 - t), sg + 3 * t);
+  __syncthreads();
+  for (int q = tid; q < L; q += RT) {
+    double o[3];
+    if (q == 0) {
+      o[0] = start[3 * b];
+      o[1] = start[3 * b + 1];
+      o[2] = start[3 * b + 2];
+    } else if (q <= RFIT * nseg) {
+      const int t = (q - 1) / RFIT, k = (q - 1) - RFIT * t;
+      cubic_point(st + 3 * (n - 1 - t), sg + 3 * t, k, o);
+    } else {
+      const double* r = rs_path + ((size_t)b * MAXPATH + (q - 1 - RFIT * nseg)) * 3;
+      o[0] = r[0];
+      o[1] = r[1];
+      o[2] = r[2];
+    }
+    P[3 * q] = o[0];
+    P[3 * q + 1] = o[1];
+    P[3 * q + 2] = o[2];
+  }
+  __syncthreads();
+  // ds = sqrt.(sum((p[:, 2:end] - p[:, 1:end-1]).^2, dims = 1)) (:153), then the running sum in order
+  for (int q = tid + 1; q < L; q += RT) {
+    const double dx = P[3 * q] - P[3 * (q - 1)], dy = P[3 * q + 1] - P[3 * (q - 1) + 1];
+    S[q] = mpj_sqrt(dx * dx + dy * dy);
+  }
+  __syncthreads();
+  __shared__ double sh_tot;
+  if (tid == 0) {
+    double acc = 0.0;
+    S[0] = 0.0;
+    for (int q = 1; q < L; q++) {
+      acc = acc + S[q];
+      S[q] = acc;
+    }
+    npts[b] = L;
+    tol[b] = acc;
+    sh_tot = acc;
+  }
+  __syncthreads();
+  // x/y/ψ_interp_dense at traver_s_list = LinRange(0, tol_length, 50) (:167-170): Interpolations.jl
+  // Gridded(Linear()): the last knot <= s (clamped to the last interval), weights (1-δ, δ)
+  if (tid < RSAMP) {
+    const double t = (double)tid / (RSAMP - 1);
+    const double sv = (1 - t) * 0.0 + t * sh_tot;
+    int lo = 0, hi = L - 1;  // largest i with S[i] <= sv
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (S[mid] <= sv) lo = mid;
+      else hi = mid - 1;
+    }
+    const int i = lo < L - 1 ? lo : (L > 1 ? L - 2 : 0);
+    if (L == 1) {
+      smp[3 * tid] = P[0];
+      smp[3 * tid + 1] = P[1];
+      smp[3 * tid + 2] = P[2];
+    } else {
+      const double w = S[i + 1] - S[i];
+      const double d = w > 0.0 ? (sv - S[i]) / w : 0.0;  // duplicate knots: the left value (as the oracle)
+      for (int c = 0; c < 3; c++) smp[3 * tid + c] = (1 - d) * P[3 * i + c] + d * P[3 * (i + 1) + c];
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1206,6 +1346,58 @@ int mp_ha_allpath(mp_ctx* ctx, int32_t B, const double* norm_states, double* cos
   if ((st = mp_download(ctx, cost, (const double*)dcost, 48 * (size_t)B))) return st;
   if ((st = mp_download(ctx, cmds, (const double*)dcmds, 48 * 15 * (size_t)B))) return st;
   if ((st = mp_download(ctx, best, (const int32_t*)dbest, (size_t)B))) return st;
+  MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MP_OK;
+}
+
+int mp_ha_retrieve_path(mp_ctx* ctx, int32_t B, const double* start, const int32_t* n_states, const double* states,
+                        int32_t state_stride, const int32_t* rs_len, const double* rs_path, int64_t* path_offset,
+                        double* actualpath, double* path_length, int32_t* n_points, double* tol_length,
+                        double* samples) {
+  if (!ctx) return MP_ERR_INVALID;
+  MP_CHECK(ctx, B >= 1 && start && n_states && states && rs_len && rs_path && n_points && tol_length && samples,
+           "bad arguments to mp_ha_retrieve_path");
+  MP_CHECK(ctx, state_stride >= 1, "state_stride (%d) must be >= 1", state_stride);
+  MP_CHECK(ctx, (actualpath == nullptr) == (path_offset == nullptr) && (path_length == nullptr || path_offset),
+           "actualpath / path_length need path_offset");
+  MP_HIP(ctx, hipSetDevice(ctx->device));
+  // ragged layout: scenario b's points at [off[b], off[b+1])
+  std::vector<long long> off(B + 1, 0);
+  int max_seg = 1;
+  for (int b = 0; b < B; b++) {
+    const int n = n_states[b], nr = rs_len[b];
+    MP_CHECK(ctx, n >= 0 && n <= state_stride, "n_states[%d] = %d outside [0, state_stride]", b, n);
+    MP_CHECK(ctx, nr >= 0 && nr <= MAXPATH, "rs_len[%d] = %d outside [0, %d]", b, nr, MAXPATH);
+    off[b + 1] = off[b] + (n >= 1 ? 1 + (long long)RFIT * (n - 1) + nr : 0);
+    max_seg = std::max(max_seg, n - 1);
+  }
+  if (path_offset)
+    for (int b = 0; b <= B; b++) path_offset[b] = off[b];
+  const size_t tot = (size_t)std::max(off[B], 1LL);
+  int st = MP_OK;
+  const double* dstart = mp_upload(ctx, WS_IO0, start, 3 * (size_t)B, &st);
+  const int* dns = mp_upload(ctx, WS_IO1, n_states, (size_t)B, &st);
+  const double* dst = mp_upload(ctx, WS_IO2, states, 3 * (size_t)state_stride * B, &st);
+  const int* drl = mp_upload(ctx, WS_IO3, rs_len, (size_t)B, &st);
+  const double* drs = mp_upload(ctx, WS_IO4, rs_path, 3 * (size_t)MAXPATH * B, &st);
+  const long long* doff = mp_upload(ctx, WS_IO5, off.data(), (size_t)B + 1, &st);
+  double* dpts = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * 3 * tot);
+  double* dpl = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * tot);
+  double* dseg = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * 3 * (size_t)max_seg * B);
+  int* dnp = (int*)mp_ws(ctx, WS_IO9, sizeof(int) * (size_t)B);
+  double* dtol = (double*)mp_ws(ctx, WS_IO10, sizeof(double) * (size_t)B);
+  double* dsm = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * RSAMP * 3 * (size_t)B);
+  if (st || !dpts || !dpl || !dseg || !dnp || !dtol || !dsm) return st ? st : MP_ERR_NOMEM;
+  hipLaunchKernelGGL(ha_retrieve_kernel, dim3(B), dim3(RT), 0, ctx->stream, dstart, dns, dst, state_stride, drl, drs,
+                     doff, dpts, dpl, dseg, max_seg, dnp, dtol, dsm);
+  MP_HIP(ctx, hipGetLastError());
+  if ((st = mp_download(ctx, n_points, (const int32_t*)dnp, (size_t)B))) return st;
+  if ((st = mp_download(ctx, tol_length, (const double*)dtol, (size_t)B))) return st;
+  if ((st = mp_download(ctx, samples, (const double*)dsm, RSAMP * 3 * (size_t)B))) return st;
+  if (off[B] > 0) {
+    if ((st = mp_download(ctx, actualpath, (const double*)dpts, 3 * (size_t)off[B]))) return st;
+    if ((st = mp_download(ctx, path_length, (const double*)dpl, (size_t)off[B]))) return st;
+  }
   MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return MP_OK;
 }

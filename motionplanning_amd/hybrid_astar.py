@@ -82,7 +82,8 @@ class HybridAstarSettings:
 
 @dataclass
 class HybridAstarResult:
-    """types.jl:54-63 (the interpolants of retrievePath are not built)."""
+    """types.jl:54-63; actualpath / tol_length / x_interp, y_interp, ψ_interp are filled by
+    retrievePath (mp_ha_retrieve_path)."""
 
     found: bool = False
     RSpath_final: np.ndarray = None
@@ -91,6 +92,14 @@ class HybridAstarResult:
     loop_count: int = 0
     n_nodes: int = 0
     pop_sequence: np.ndarray = None
+    actualpath: np.ndarray = None
+    path_length: np.ndarray = None
+    tol_length: float = 0.0
+    interp_knots: np.ndarray = None
+    interp_values: np.ndarray = None
+    x_interp: object = None
+    y_interp: object = None
+    ψ_interp: object = None
 
 
 @dataclass
@@ -192,6 +201,60 @@ def plan_batch(searchers, ctx=None, max_pops=5000):
         r.RSpath_final = rs_path[b, : rs_len[b]].T.copy()
         r.planning_time = dt
     return searchers
+
+
+def retrieve_batch(searchers, ctx=None):
+    """retrievePath (hybrid_astar_utils.jl:129-177, with cubic_fit :100-127) for planned searchers in one
+    launch (mp_ha_retrieve_path): fills r.actualpath (3, L), r.path_length, r.tol_length and the
+    x/y/ψ_interp interpolants over the 50 arc-length knots LinRange(0, tol_length, 50) (linear, as
+    linear_interpolation builds them; evaluated here with numpy on the device-computed knot values)."""
+    ctx = ctx or default_context()
+    B = len(searchers)
+    start = f64([h.s.starting_states for h in searchers])
+    ns = np.array([0 if h.r.hybrid_astar_states is None or not h.r.found else h.r.hybrid_astar_states.shape[1]
+                   for h in searchers], np.int32)
+    stride = max(1, int(ns.max()))
+    states = np.zeros((B, stride, 3))
+    rs_len = np.zeros(B, np.int32)
+    rs = np.zeros((B, 501, 3))
+    for b, h in enumerate(searchers):
+        if ns[b]:
+            states[b, : ns[b]] = h.r.hybrid_astar_states.T
+            rs_len[b] = h.r.RSpath_final.shape[1]
+            rs[b, : rs_len[b]] = h.r.RSpath_final.T
+    tot = int(sum(1 + 100 * (n - 1) + r for n, r in zip(ns, rs_len) if n))
+    off = np.zeros(B + 1, np.int64)
+    pts, plen = np.zeros((max(tot, 1), 3)), np.zeros(max(tot, 1))
+    npts, tol, smp = np.zeros(B, np.int32), np.zeros(B), np.zeros((B, 50, 3))
+    ctx.check(ctx.lib.mp_ha_retrieve_path(ctx.handle, B, ptr(start), ptr(ns), ptr(states), stride, ptr(rs_len),
+                                          ptr(rs), ptr(off), ptr(pts), ptr(plen), ptr(npts), ptr(tol), ptr(smp)))
+    for b, h in enumerate(searchers):
+        r = h.r
+        if not ns[b]:
+            continue
+        a, e = int(off[b]), int(off[b + 1])
+        r.actualpath = pts[a:e].T.copy()
+        r.path_length = plen[a:e].copy()
+        r.tol_length = float(tol[b])
+        r.interp_knots = configs_linrange(0.0, r.tol_length, 50)
+        r.interp_values = smp[b].copy()
+        k, v = r.interp_knots, r.interp_values
+        r.x_interp = lambda s, k=k, v=v: np.interp(s, k, v[:, 0])
+        r.y_interp = lambda s, k=k, v=v: np.interp(s, k, v[:, 1])
+        r.ψ_interp = lambda s, k=k, v=v: np.interp(s, k, v[:, 2])
+    return searchers
+
+
+def retrievePath(h, ctx=None):
+    """retrievePath(hybrid_astar) (hybrid_astar_utils.jl:129-177) for one planned searcher."""
+    retrieve_batch([h], ctx=ctx)
+    return None
+
+
+def configs_linrange(a, b, n):
+    from .configs import julia_linrange
+
+    return julia_linrange(a, b, n)
 
 
 def planHybridAstar_(h, ctx=None, max_pops=5000):

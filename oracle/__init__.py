@@ -245,6 +245,8 @@ def _ha():
         L.or_ha_rs_heuristic.argtypes = [P, _V, _V]
         L.or_change_basis.restype = None
         L.or_change_basis.argtypes = [_V, _V, _D, _V]
+        L.or_ha_retrieve.restype = ctypes.c_int
+        L.or_ha_retrieve.argtypes = [_V, ctypes.c_int, _V, ctypes.c_int, _V, _V, _V, _V, _V]
         L.or_ha_plan.restype = ctypes.c_int
         L.or_ha_plan.argtypes = [P] + [_V] * 12
         L._ha_ready = True
@@ -312,3 +314,17 @@ def ha_plan(p, start, goal, walls, sc, pc):
                              ptr(states), ptr(rl), ptr(rs))
     return dict(found=bool(found), pops=int(pops[0]), n_nodes=int(nn[0]), pop_seq=seq[: pops[0]],
                 states=states[: ns[0]], rs_path=rs[: rl[0]])
+
+
+def ha_retrieve(start, states, rs_path):
+    """retrievePath + cubic_fit (hybrid_astar_utils.jl:100-177): states (n, 3) goal side first as
+    planned, rs_path (m, 3).  Returns dict(actualpath (L, 3), path_length (L,), tol_length, samples (50, 3))."""
+    start = np.ascontiguousarray(start, np.float64)
+    states = np.ascontiguousarray(states, np.float64).reshape(-1, 3)
+    rs_path = np.ascontiguousarray(rs_path, np.float64).reshape(-1, 3)
+    n, nr = states.shape[0], rs_path.shape[0]
+    L = 1 + 100 * (n - 1) + nr if n else 1
+    pts, plen = np.zeros((L, 3)), np.zeros(L)
+    tol, smp = np.zeros(1), np.zeros((50, 3))
+    m = _ha().or_ha_retrieve(ptr(start), n, ptr(states), nr, ptr(rs_path), ptr(pts), ptr(plen), ptr(tol), ptr(smp))
+    return dict(actualpath=pts[:m], path_length=plen[:m], tol_length=tol[0], samples=smp, n_points=m)

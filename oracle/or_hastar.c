@@ -532,3 +532,71 @@ int or_ha_plan(const mp_ha_params* p, const double* start, const double* goal, c
   free(S.nodes); free(S.keys); free(S.vals); free(open); free(nbs); free(idx); free(fr); free(h); free(path);
   return found;
 }
+
+/* ---------------------------------------------------------------- path finishing */
+void or_pinv2(const double* M, double* P); /* or_ilqr.c: LinearAlgebra.pinv for a 2x2 */
+
+/* cubic_fit, hybrid_astar_utils.jl:100-127: 100 points [x y ψ] from cur toward nxt. */
+static void or_cubic_fit(const double* cur, const double* nxt, double* out /* [100][3] */) {
+  double ns[3];
+  or_change_basis(cur, nxt, 1.0, ns);
+  const double xg = ns[0], yg = ns[1], pg = ns[2];
+  /* A = [xg^3 xg^2; 3*xg^2 2*xg] (x^3 = x*x*x, Julia literal_pow), params = pinv(A)*[yg; tan(ψg)] */
+  const double A[4] = {xg * xg * xg, xg * xg, 3 * (xg * xg), 2 * xg};
+  double Pm[4];
+  or_pinv2(A, Pm);
+  const double b0 = yg, b1 = mpj_tan(pg);
+  const double p1 = Pm[0] * b0 + Pm[1] * b1, p2 = Pm[2] * b0 + Pm[3] * b1;
+  const double s0 = mpj_sin(cur[2]), c0 = mpj_cos(cur[2]);
+  for (int k = 0; k < 100; k++) {
+    const double t = (double)k / 99; /* LinRange(0, xg, 100): (1-t)*0 + t*xg */
+    const double x = (1 - t) * 0.0 + t * xg;
+    const double y = p1 * (x * x * x) + p2 * (x * x);
+    const double psi = mpj_atan((3 * p1) * (x * x) + (2 * p2) * x);
+    out[3 * k] = (c0 * x + (-s0) * y) + cur[0]; /* Rmat*path[1:2,:] .+ [x0; y0] */
+    out[3 * k + 1] = (s0 * x + c0 * y) + cur[1];
+    out[3 * k + 2] = psi + cur[2];
+  }
+}
+
+/* retrievePath, :129-177, one scenario.  states: hybrid_astar_states as planned (goal side first),
+ * n of them; rs[nr][3] RSpath_final.  pts[1 + 100(n-1) + nr][3] (actualpath columns), plen[...]
+ * (cumulative arc length), samples[50][3] (x/y/ψ_interp_dense at LinRange(0, tol_length, 50); the
+ * Interpolations.jl Gridded(Linear()) rule: last knot <= s, clamped to the last interval, weights
+ * (1-δ, δ); a zero-width interval -- actualpath repeats points wherever an RS segment turns in place
+ * or two consecutive states differ only in ψ -- takes its left value: a convention, since Julia's
+ * result there depends on the (absent, unpinned) Interpolations.jl version).  Returns the number of points (0 when n == 0: nothing to retrieve). */
+int or_ha_retrieve(const double* start, int n, const double* states, int nr, const double* rs, double* pts,
+                   double* plen, double* tol, double* samples) {
+  if (n < 1) {
+    *tol = 0.0;
+    memset(samples, 0, sizeof(double) * 150);
+    return 0;
+  }
+  const int L = 1 + 100 * (n - 1) + nr;
+  memcpy(pts, start, sizeof(double) * 3);
+  for (int i = 0; i + 1 < n; i++) /* states reversed: start -> goal */
+    or_cubic_fit(states + 3 * (n - 1 - i), states + 3 * (n - 2 - i), pts + 3 * (1 + 100 * i));
+  memcpy(pts + 3 * (1 + 100 * (n - 1)), rs, sizeof(double) * 3 * nr);
+  plen[0] = 0.0;
+  for (int q = 1; q < L; q++) {
+    const double dx = pts[3 * q] - pts[3 * (q - 1)], dy = pts[3 * q + 1] - pts[3 * (q - 1) + 1];
+    plen[q] = plen[q - 1] + sqrt(dx * dx + dy * dy);
+  }
+  *tol = plen[L - 1];
+  for (int j = 0; j < 50; j++) {
+    const double t = (double)j / 49;
+    const double s = (1 - t) * 0.0 + t * *tol;
+    int i = 0;
+    while (i + 1 < L && plen[i + 1] <= s) i++;
+    if (L == 1) {
+      memcpy(samples + 3 * j, pts, sizeof(double) * 3);
+      continue;
+    }
+    if (i > L - 2) i = L - 2;
+    const double w = plen[i + 1] - plen[i];
+    const double d = w > 0.0 ? (s - plen[i]) / w : 0.0; /* duplicate knots: the left value */
+    for (int c = 0; c < 3; c++) samples[3 * j + c] = (1 - d) * pts[3 * i + c] + d * pts[3 * (i + 1) + c];
+  }
+  return L;
+}

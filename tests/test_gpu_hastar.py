@@ -113,3 +113,29 @@ def test_allpath_bitexact(ctx):
         assert np.array_equal(cost[b], co, equal_nan=True)  # NaN candidates (e.g. ns = 0) included
         assert np.array_equal(cmds[b], mo, equal_nan=True)
     assert best[len(ns) - 5] == 0 and cost[len(ns) - 5, 0] == 2.0  # straight ahead: LSL, cost d
+
+
+def test_retrieve_path_batch_bitexact(ctx):
+    """retrievePath + cubic_fit (hybrid_astar_utils.jl:100-177) for a planned cfg4-shaped batch in one
+    launch (mp_ha_retrieve_path) vs the oracle, bit for bit: actualpath, path_length, tol_length and the 50
+    x/y/ψ samples; scenarios without a path retrieve nothing.  (Rmat*path and pinv(A)*B are evaluated
+    without FMA, and duplicate arc-length knots take their left value: Julia's BLAS and Interpolations.jl
+    are absent, so those two points are parity unpinned vs Julia.)"""
+    hs = ha.scenario_batch(48, seed=6)
+    ha.plan_batch(hs, ctx=ctx)
+    ha.retrieve_batch(hs, ctx=ctx)
+    found = 0
+    for h in hs:
+        if not h.r.found:
+            assert h.r.actualpath is None
+            continue
+        found += 1
+        ref = oracle.ha_retrieve(h.s.starting_states, h.r.hybrid_astar_states.T, h.r.RSpath_final.T)
+        assert np.array_equal(h.r.actualpath.T, ref["actualpath"])
+        assert np.array_equal(h.r.path_length, ref["path_length"])
+        assert h.r.tol_length == ref["tol_length"]
+        assert np.array_equal(h.r.interp_values, ref["samples"])
+        assert np.isfinite(h.r.interp_values).all()
+        s = np.linspace(0, h.r.tol_length, 7)
+        assert np.isfinite(h.r.x_interp(s)).all() and np.isfinite(h.r.ψ_interp(s)).all()
+    assert found > 10

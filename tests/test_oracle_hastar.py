@@ -78,3 +78,34 @@ def test_driver_scenes_match_survey_probe():
         # the path ends at the goal pose and starts at the popped node
         assert np.abs(r["rs_path"][-1, :2] - h.s.ending_states[:2]).max() < 1e-2  # Euler, 100 steps/segment
         assert np.array_equal(r["rs_path"][0], r["states"][0])
+
+
+def test_retrieve_path_structure():
+    """retrievePath + cubic_fit (hybrid_astar_utils.jl:100-177) on the driver scene's plan: the start
+    column, one 100-point cubic per consecutive pair of (reversed) hybrid_astar_states that starts on
+    its state and ends on the next one, RSpath_final last; arc length non-decreasing; the 50 samples
+    run from the start (s = 0) to the RS path's end (s = tol_length)."""
+    h = ha.driver_searcher(ha.PERPENDICULAR)
+    p = ha.params_of(h)
+    sc, pc = oracle.ha_neighbor_origin(h.s.expand_time, h.s.steer_set, h.s.gear_set)
+    r = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+    assert r["found"]
+    st = r["states"][::-1]  # start -> goal
+    out = oracle.ha_retrieve(h.s.starting_states, r["states"], r["rs_path"])
+    n, m = st.shape[0], r["rs_path"].shape[0]
+    P = out["actualpath"]
+    assert out["n_points"] == 1 + 100 * (n - 1) + m == P.shape[0]
+    np.testing.assert_array_equal(P[0], h.s.starting_states)
+    for i in range(n - 1):
+        seg = P[1 + 100 * i: 1 + 100 * (i + 1)]
+        np.testing.assert_array_equal(seg[0, :2], st[i, :2])
+        np.testing.assert_allclose(seg[-1, :2], st[i + 1, :2], atol=1e-9)  # the cubic reaches the next state
+    np.testing.assert_array_equal(P[1 + 100 * (n - 1):], r["rs_path"])
+    L = out["path_length"]
+    assert L[0] == 0.0 and np.all(np.diff(L) >= 0) and L[-1] == out["tol_length"]
+    S = out["samples"]
+    np.testing.assert_allclose(S[0], P[0], atol=1e-12)
+    np.testing.assert_allclose(S[-1], P[-1], atol=1e-12)
+    # a sample is the linear interpolation of actualpath at its arc length
+    s = out["tol_length"] * 17 / 49
+    np.testing.assert_allclose(S[17, 0], np.interp(s, L, P[:, 0]), atol=1e-9)
