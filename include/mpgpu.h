@@ -342,6 +342,49 @@ int mp_ha_retrieve_path(mp_ctx* ctx, int32_t B, const double* start, const int32
                         double* actualpath, double* path_length, int32_t* n_points, double* tol_length,
                         double* samples);
 
+/* ------------------------------------------------------- path tracker */
+/* Settings of the Hybrid A* path tracker (PathPlanning/HybridAstar/main_Tracker.jl:42-72). */
+typedef struct mp_track_params {
+  int32_t n_ref;      /* refined_length = LinRange(0, tol_length, n_ref): 1000 (:42); <= 2048           */
+  int32_t max_steps;  /* safety cap on simulation steps (the reference loops until the closest point
+                         is the last one, :84)                                                          */
+  double dt_sim;      /* 1e-3 (:67)                                                                     */
+  double look_ahead;  /* look_ahead_dist 1.0 (:57)                                                      */
+  double p_gain;      /* 10 (:58)                                                                       */
+  double i_gain;      /* 0.1 (:59)                                                                      */
+  double veh_len;     /* veh_param[1] = vehicle_size[1] (:50)                                           */
+  double max_sa;      /* veh_param[3] = max_δf + 0.1 (:52)                                              */
+  int32_t his_stride; /* states_his: keep the state after every his_stride-th update (0: none)          */
+  int32_t reserved;
+} mp_track_params;
+
+#define MP_TRACK_DONE 0    /* the closest reference point reached the last one (main_Tracker.jl:84-89) */
+#define MP_TRACK_MAXSTEP 1 /* max_steps simulation steps ran without reaching it                         */
+#define MP_TRACK_NOPATH 2  /* tol_length not > 0 (no planned path: "Can't find a path", :31-35)         */
+#define MP_TRACK_EMPTY 3   /* an empty findclosest window (argmin of an empty range: a Julia error)      */
+
+/*
+ * mp_ha_track — the HA* -> tracker hand-off and the tracker closed loop of
+ * PathPlanning/HybridAstar/main_Tracker.jl:42-137 for B planned scenarios in lockstep, one wavefront
+ * each.  x_ref/y_ref/ψ_ref = x/y/ψ_interp(refined_length) (:42-46, Interpolations.jl linear
+ * interpolation on the n_samples knots LinRange(0, tol_length, n_samples)); then per step
+ * (simulation_idx = 1, 2, ...): findclosest (tracker_utils.jl:38-43) inside the time windows of
+ * :82-90, inverseKinematic (tracker_utils.jl:15-36), the look-ahead point and its findclosest
+ * (:97-108), the cross-track PI correction with clamp (:110-119) and the kinematic Euler step
+ * (tracker_utils.jl:1-13, :121).
+ * in : start_real[B][3] (cur_states = starting_real, :64), tol_length[B] and samples[B][n_samples][3]
+ *      as mp_ha_retrieve_path returns them (x/y/ψ_interp values at their knots).
+ * out: n_steps[B] (simulation_idx when the loop ended), status[B] (MP_TRACK_*),
+ *      final_state[B][3] (cur_states), err_acc[B] (err_accumulated),
+ * optional (NULL to skip): ref_out[B][n_ref][3] (x_ref, y_ref, ψ_ref: the hand-off),
+ *      his[B][his_cap][3]: states_his (:122) every his_stride-th update, row 0 = starting_real;
+ *      rows written = min(his_cap, (n_steps - 1) / his_stride + 1).
+ */
+int mp_ha_track(mp_ctx* ctx, const mp_track_params* p, int32_t B, const double* start_real,
+                const double* tol_length, const double* samples, int32_t n_samples, int32_t* n_steps,
+                int32_t* status, double* final_state, double* err_acc, double* ref_out, double* his,
+                int32_t his_cap);
+
 /* ---------------------------------------------------------- diagnostics */
 /* Evaluate one include/mp_jlmath.h function on the device for n inputs
  * (bit-exactness check against the CPU build).  fn: 0 sin, 1 cos, 2 tan, 3 atan,

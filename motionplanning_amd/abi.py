@@ -119,6 +119,28 @@ class HAParams(ctypes.Structure):
     ]
 
 
+class TrackParams(ctypes.Structure):
+    """mp_track_params (include/mpgpu.h) — the tracker settings of HybridAstar/main_Tracker.jl:42-72."""
+
+    _fields_ = [
+        ("n_ref", ctypes.c_int32),
+        ("max_steps", ctypes.c_int32),
+        ("dt_sim", ctypes.c_double),
+        ("look_ahead", ctypes.c_double),
+        ("p_gain", ctypes.c_double),
+        ("i_gain", ctypes.c_double),
+        ("veh_len", ctypes.c_double),
+        ("max_sa", ctypes.c_double),
+        ("his_stride", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+MP_TRACK_DONE = 0
+MP_TRACK_MAXSTEP = 1
+MP_TRACK_NOPATH = 2
+MP_TRACK_EMPTY = 3
+
 # (name, restype, argtypes) for every symbol declared in include/mpgpu.h
 _V = ctypes.c_void_p
 _I = ctypes.c_int32
@@ -155,6 +177,7 @@ SIGNATURES = {
     "mp_ha_allpath": (ctypes.c_int, [_V, _I, _V, _V, _V, _V]),
     "mp_ha_plan": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I] + [_V] * 11),
     "mp_ha_retrieve_path": (ctypes.c_int, [_V, _I, _V, _V, _V, _I] + [_V] * 8),
+    "mp_ha_track": (ctypes.c_int, [_V, ctypes.POINTER(TrackParams), _I, _V, _V, _V, _I] + [_V] * 6 + [_I]),
     "mp_math_eval": (ctypes.c_int, [_V, _I, ctypes.c_int64, _V, _V, _V]),
 }
 

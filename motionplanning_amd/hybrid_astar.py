@@ -100,6 +100,7 @@ class HybridAstarResult:
     x_interp: object = None
     y_interp: object = None
     ψ_interp: object = None
+    tracking: dict = None  # main_Tracker.jl's simulation (tracker.track_batch)
 
 
 @dataclass
