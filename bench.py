@@ -351,6 +351,49 @@ def bench_hastar(ctx, world, rank, cpu=False):
         cp, n, dt = timed_pool(work, 3.0, T, limit=len(hs))
         out["cpu_baseline"] = {"value": cp / dt, "unit": "node expansions/s", "cores": T, "kind": "port",
                                "sample": f"{n} scenarios ({cp} pops) in {dt:.1f} s on {T} threads, scalar C oracle"}
+    out["tracker"] = bench_tracker(ctx, world, rank, hs, cpu=cpu)
+    return out
+
+
+def bench_tracker(ctx, world, rank, hs, cpu=False):
+    """The HA* -> tracker hand-off + tracker closed loop (HybridAstar/main_Tracker.jl:42-137) for the
+    scenarios this rank planned in bench_hastar: retrievePath (mp_ha_retrieve_path) then every found
+    path tracked in lockstep (mp_ha_track, one wave per scenario) until its closest point is the last.
+    Unit: one tracker simulation step (1 ms of simulated time: three time argmins, two findclosest
+    windows, inverseKinematic, PI correction, kinematic Euler step)."""
+    from motionplanning_amd import distributed as D
+    from motionplanning_amd import tracker
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    D.track_sharded(hs, ctx=ctx)  # warm-up (workspaces) on the same batch
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g = D.track_sharded(hs, ctx=ctx)
+    el = _sync_max(time.perf_counter() - t0, world, dev)
+    steps = int(g["n_steps"].sum())
+    done = int((g["status"] == tracker.MP_TRACK_DONE).sum())
+    out = {"metric": "HA* path tracker simulation steps/s (retrievePath + main_Tracker.jl loop), configs[3] paths",
+           "value": steps / el, "ms_total": el * 1e3, "tracked": done,
+           "no_path": int((g["status"] == tracker.MP_TRACK_NOPATH).sum()), "total_steps": steps,
+           "max_steps_per_scenario": int(g["n_steps"].max()), "scaling": "strong", "dtype": "f64",
+           "valid": done == int((g["status"] != tracker.MP_TRACK_NOPATH).sum()),
+           "bound": "latency (one serial 1 kHz loop per scenario, one wave each)"}
+    if cpu:
+        import oracle
+
+        mine = [h for h in hs if h.r.tracking is not None and h.r.tracking["status"] == "done"]
+        p = tracker.params_of(tracker.settings_for(mine[0]))
+
+        def work(i):
+            h = mine[i]
+            return oracle.track(p, h.s.starting_real, h.r.tol_length, h.r.interp_values)["n_steps"]
+
+        T = cpu_threads()
+        cs, n, dt = timed_pool(work, 3.0, T, limit=len(mine))
+        out["cpu_baseline"] = {"value": cs / dt, "unit": "tracker steps/s", "cores": T, "kind": "port",
+                               "sample": f"{n} tracked paths ({cs} steps) in {dt:.1f} s on {T} threads, scalar C "
+                                         "oracle (full-scan argmins as the reference)"}
     return out
 
 

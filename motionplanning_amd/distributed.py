@@ -137,6 +137,29 @@ def hybrid_astar_sharded(searchers, planner=None, ctx=None, max_pops=5000):
     return dict(found=g[:, 0].astype(bool), pops=g[:, 1], n_nodes=g[:, 2], rs_len=g[:, 3])
 
 
+def track_sharded(searchers, ctx=None, settings=None, runner=None):
+    """retrievePath + the main_Tracker.jl loop for this rank's shard of a planned batch (the same
+    [a, b) split as hybrid_astar_sharded, so each rank tracks what it planned).  Every rank returns
+    the gathered {status, n_steps} for the whole batch.  `runner(mine)` replaces the device calls
+    (the gloo tests run the oracle there)."""
+    from . import hybrid_astar as ha
+    from . import tracker
+
+    rank, world = _world()
+    n = len(searchers)
+    a, b = shard_bounds(n, rank, world)
+    mine = searchers[a:b]
+    if mine and runner is not None:
+        runner(mine)
+    elif mine:
+        ha.retrieve_batch(mine, ctx=ctx)
+        tracker.track_batch(mine, ctx=ctx, settings=settings)
+    inv = {v: k for k, v in tracker.STATUS.items()}
+    out = np.array([[inv[h.r.tracking["status"]], h.r.tracking["n_steps"]] for h in mine], np.int64).reshape(-1, 2)
+    g = all_gather_rows(out, n)
+    return dict(status=g[:, 0], n_steps=g[:, 1])
+
+
 # ------------------------------------------------------------------ iLQR
 def ilqr_solve_sharded(p, X, U, planner=None, ctx=None):
     """ilqr_solve over B instances split across ranks; returns gathered (X, U, J, iters)."""

@@ -57,6 +57,23 @@ def _ha_oracle_planner(hs):
         r = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
         h.r.found, h.r.loop_count, h.r.n_nodes = r["found"], r["pops"], r["n_nodes"]
         h.r.RSpath_final = r["rs_path"].T
+        h.r.hybrid_astar_states = r["states"].T
+
+
+TRACK_STEPS = 2000
+
+
+def _track_oracle_runner(hs):
+    from motionplanning_amd import tracker
+
+    p = tracker.params_of(tracker.TrackerSettings(max_steps=TRACK_STEPS))
+    for h in hs:
+        tol, smp = 0.0, np.zeros((50, 3))
+        if h.r.found:
+            ret = oracle.ha_retrieve(h.s.starting_states, h.r.hybrid_astar_states.T, h.r.RSpath_final.T)
+            tol, smp = ret["tol_length"], ret["samples"]
+        t = oracle.track(p, h.s.starting_real, tol, smp)
+        h.r.tracking = dict(status=tracker.STATUS[t["status"]], n_steps=t["n_steps"])
 
 
 def _ilqr_inputs():
@@ -85,10 +102,12 @@ def _worker(rank, world, port, outdir):
         m = D.mppi_plan_sharded(p, X0, goal, unom, obstacles=obs, planner=_oracle_mppi)
         hs = ha.scenario_batch(N_HA, seed=4)
         h = D.hybrid_astar_sharded(hs, planner=_ha_oracle_planner)
+        t = D.track_sharded(hs, runner=_track_oracle_runner)
         pi, X, U = _ilqr_inputs()
         Xs, Us, J, it = D.ilqr_solve_sharded(pi, X, U, planner=_ilqr_oracle_planner)
         np.savez(os.path.join(outdir, f"r{rank}.npz"), **{f"m_{k}": v for k, v in m.items()},
-                 **{f"h_{k}": v for k, v in h.items()}, i_X=Xs, i_U=Us, i_J=J, i_it=it)
+                 **{f"h_{k}": v for k, v in h.items()},
+                 **{f"t_{k}": v for k, v in t.items()}, i_X=Xs, i_U=Us, i_J=J, i_it=it)
     finally:
         dist.destroy_process_group()
 
@@ -128,6 +147,12 @@ def test_world2_gloo_matches_single_process(tmp_path):
     assert np.array_equal(r0["h_found"], [h.r.found for h in hs])
     assert np.array_equal(r0["h_pops"], [h.r.loop_count for h in hs])
     assert np.array_equal(r0["h_n_nodes"], [h.r.n_nodes for h in hs])
+    _track_oracle_runner(hs)  # the tracker hand-off of the planned shards, gathered
+    from motionplanning_amd import tracker
+
+    inv = {v: k for k, v in tracker.STATUS.items()}
+    assert np.array_equal(r0["t_status"], [inv[h.r.tracking["status"]] for h in hs])
+    assert np.array_equal(r0["t_n_steps"], [h.r.tracking["n_steps"] for h in hs])
     pi, X, U = _ilqr_inputs()
     Xs, Us, J, it = _ilqr_oracle_planner(pi, X, U)
     assert np.array_equal(r0["i_X"], Xs) and np.array_equal(r0["i_U"], Us)
