@@ -11,6 +11,8 @@ hot-path functions below take over the reference's names on the same searcher ob
   * `planHybridAstar!(ha)`              PathPlanning/HybridAstar/src/hybrid_astar_utils.jl:235-296
   * `RS_connected`, `FindNewNode` device parts (`ha_rs_connect`, `ha_expand`)
   * iLQR passes (`ilqr_backward!`, `ilqr_forward!`, `ilqr_solve!`)  OptimalControl/ILQR/ILQR.jl:44-88
+  * `retrieve_batch!` (retrievePath + cubic_fit, hybrid_astar_utils.jl:100-177) and `track_batch!`
+    (the HA* -> tracker hand-off and tracker loop of PathPlanning/HybridAstar/main_Tracker.jl:42-137)
 
 Errors: every non-zero status is re-raised as `error(mp_last_error(ctx))`, the style of
 the reference's own validation (MPPI/src/setup.jl:19-38).  Arrays are passed in Julia's
@@ -25,7 +27,7 @@ module MPGPU
 using Interpolations: interpolate, Gridded, Constant, Previous, linear_interpolation   # as the reference drivers
 
 export MPPIPlan, MPPIClosedLoop, planHybridAstar!, mppi_plan_batch, mppi_closed_loop_batch, rollout_batch, ha_expand, ha_rs_connect,
-       ha_allpath, retrieve_batch!, ilqr_backward!, ilqr_forward!, ilqr_solve!
+       ha_allpath, retrieve_batch!, track_batch!, ilqr_backward!, ilqr_forward!, ilqr_solve!
 
 const libmpgpu = get(ENV, "MPGPU_LIB", joinpath(@__DIR__, "..", "motionplanning_amd", "lib", "libmpgpu.so"))
 
@@ -354,6 +356,8 @@ retrievePath (hybrid_astar_utils.jl:129-177, with cubic_fit :100-127) for planne
 Pass it as `plan_batch!(has; retrieve = nothing)` then call this once for the whole batch (the
 reference's own `retrievePath` per searcher stays available through `retrieve = retrievePath`).
 """
+const SAMPLES = WeakKeyDict{Any,Matrix{Float64}}()
+
 function retrieve_batch!(has::AbstractVector)
     B = length(has)
     ok(h) = h.r.hybrid_astar_states !== nothing && size(h.r.hybrid_astar_states, 2) > 0
@@ -377,6 +381,7 @@ function retrieve_batch!(has::AbstractVector)
         c, B, start, ns, states, stride, rl, rs, off, pts, plen, np_, tol, smp), c)
     for (b, h) in enumerate(has)
         ns[b] == 0 && continue
+        SAMPLES[h] = smp[:, :, b]     # the knot values, for track_batch!
         h.r.actualpath = pts[:, off[b]+1:off[b+1]]
         h.r.tol_length = tol[b]
         knots = LinRange(0, tol[b], 50)
@@ -385,6 +390,55 @@ function retrieve_batch!(has::AbstractVector)
         h.r.ψ_interp = linear_interpolation(knots, smp[3, :, b])
     end
     return has
+end
+
+struct TrackParams     # mp_track_params (main_Tracker.jl:42-72)
+    n_ref::Int32
+    max_steps::Int32
+    dt_sim::Float64
+    look_ahead::Float64
+    p_gain::Float64
+    i_gain::Float64
+    veh_len::Float64
+    max_sa::Float64
+    his_stride::Int32
+    reserved::Int32
+end
+
+"""
+    track_batch!(has; look_ahead_dist = 1.0, p_gain = 10, i_gain = 0.1, dt_sim = 1e-3, max_sa = max_δf + 0.1, ...)
+
+The tracker of PathPlanning/HybridAstar/main_Tracker.jl:42-137 for every planned + retrieved searcher
+(`retrieve_batch!` first) in one launch (mp_ha_track, one wavefront per searcher): the hand-off
+x/y/ψ_ref = x/y/ψ_interp(LinRange(0, tol_length, 1000)), then findclosest / inverseKinematic /
+look-ahead PI / kinematic Euler steps of 1 ms from `starting_real` until the closest reference point
+is the last one.  Returns, per searcher, `(; status, n_steps, states_his (3 × rows, every his_stride-th
+update), cur_states, err_accumulated, x_ref, y_ref, ψ_ref)`; `status` is :done, :max_steps, :no_path or
+:empty_window.  (The reference's plotting/gif of the loop is not reproduced.)
+"""
+function track_batch!(has::AbstractVector; look_ahead_dist = 1.0, p_gain = 10, i_gain = 0.1, dt_sim = 1e-3,
+                      max_sa = pi / 6 + 0.1, n_ref = 1000, max_steps = 200_000, his_stride = 1, his_cap = 30_000)
+    B = length(has)
+    start = reduce(hcat, [Float64.(h.s.starting_real) for h in has])
+    tol = [haskey(SAMPLES, h) ? Float64(h.r.tol_length) : 0.0 for h in has]
+    smp = zeros(3, 50, B)
+    for (b, h) in enumerate(has)
+        haskey(SAMPLES, h) && (smp[:, :, b] = SAMPLES[h])
+    end
+    p = TrackParams(n_ref, max_steps, dt_sim, look_ahead_dist, p_gain, i_gain, Float64(has[1].s.vehicle_size[1]),
+                    max_sa, his_stride, 0)
+    n = zeros(Int32, B); st = zeros(Int32, B); fin = zeros(3, B); ea = zeros(B)
+    ref = zeros(3, n_ref, B); his = zeros(3, his_cap, B)
+    c = ctx()
+    check(GC.@preserve start tol smp n st fin ea ref his ccall((:mp_ha_track, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{TrackParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32, Ptr{Int32}, Ptr{Int32},
+         Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int32),
+        c, p, B, start, tol, smp, 50, n, st, fin, ea, ref, his, his_cap), c)
+    names = (:done, :max_steps, :no_path, :empty_window)
+    return [(; status = names[st[b] + 1], n_steps = Int(n[b]),
+              states_his = his[:, 1:(n[b] == 0 ? 1 : min(his_cap, (n[b] - 1) ÷ his_stride + 1)), b],
+              cur_states = fin[:, b], err_accumulated = ea[b],
+              x_ref = ref[1, :, b], y_ref = ref[2, :, b], ψ_ref = ref[3, :, b]) for b in 1:B]
 end
 
 function ha_expand(p::HaParams, node::Matrix{Float64}, goal::Matrix{Float64}, walls::Array{Float64,3})
