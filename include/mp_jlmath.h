@@ -71,6 +71,35 @@ MPJ_FN double mpj_jmin(double x, double y) {
   return ty ? (mpj_isnan(x) ? x : y) : (mpj_isnan(y) ? y : x);
 }
 
+/* Repeated addition q_k = RN(q_{k-1} + c), k = 1..K (createActPath's heading recurrence and the running
+ * sums of a straight segment, ReedsSheppsUtils.jl:440-466) in closed form.  When q_0, q_1 = RN(q_0 + c)
+ * and q_0 + K·d (d = q_1 - q_0, exact) share sign and binade [2^e, 2^(e+1)), lie at least one ulp
+ * u = 2^(e-52) inside it (two at the top), and q_0 + c is not a rounding tie, every step adds exactly d:
+ * the real q_k + c equals q_{k+1} + err with the same TwoSum error |err| < u/2 on the same u-grid, so
+ * q_k = q_0 + k·d = fma(k, d, q_0) (a representable multiple of u).  c == 0 is always closed: q_k = q_1
+ * for k >= 1.  Returns 0 when the closed form does not apply (the caller adds serially). */
+MPJ_FN int mpj_rep_add_ok(double q0, double c, int K, double* d) {
+  const double q1 = q0 + c;
+  *d = 0.0;
+  if (c == 0.0) return 1;
+  const double dd = q1 - q0;
+  const double qK = mpj_fma((double)K, dd, q0);
+  const uint32_t e0 = mpj_hi(q0) >> 20; /* sign + exponent */
+  if ((mpj_hi(q1) >> 20) != e0 || (mpj_hi(qK) >> 20) != e0) return 0;
+  const uint32_t ex = e0 & 0x7ffu;
+  if (ex < 54u || ex >= 0x7ffu) return 0; /* zero, subnormal, tiny; Inf / NaN */
+  const double lo = mpj_from_words(ex << 20, 0), u = mpj_from_words((ex - 52u) << 20, 0);
+  const double hi = 2.0 * lo;
+  const double a0 = mpj_fabs(q0), aK = mpj_fabs(qK);
+  const double mn = a0 < aK ? a0 : aK, mx = a0 < aK ? aK : a0;
+  if (!(mn >= lo + u) || !(mx <= hi - 2.0 * u)) return 0;
+  const double bb = q1 - q0; /* TwoSum: the exact rounding error of q0 + c */
+  const double err = (q0 - (q1 - bb)) + (c - bb);
+  if (mpj_fabs(err) == 0.5 * u) return 0;
+  *d = dd;
+  return 1;
+}
+
 /* ---------------------------------------------------------------- sin/cos */
 /* FDLIBM k_sin.c / k_cos.c (Julia base/special/trig.jl sin_kernel/cos_kernel). */
 #define MPJ_S1 (-1.66666666666666324348e-01)

@@ -348,6 +348,7 @@ struct IterArgs {
   const int* scene_of;   // active slot -> scene index (nullptr: slot = scene)
   const int* active;     // per-scene live flag (device-resident search), nullptr = all
   const double* wtab;    // [B][nw][34] wall corners (10) + SAT tables (24), nullptr = compute
+  const int* n_live;     // device count of the scene_of list (nullptr: n_active)
   int n_active;
   int do_rs, do_exp;
   // RS_connected outputs (per scene)
@@ -391,16 +392,21 @@ __device__ __forceinline__ OutRef out_ref(const IterArgs& A, int s, int n_prim) 
 #endif
 constexpr int HW = HA_WAVES;
 constexpr int HT = 64 * HW;
-constexpr int WPW = 12 / HW;  // Reeds–Shepp words per wave
 static_assert(12 % HW == 0, "HA_WAVES must divide the 12 Reeds-Shepp words");
+// Tail shape, for iterations with few scenes still searching (the latency-bound end of a batched
+// plan): 12 waves per block (one Reeds-Shepp word per wave) and 4 neighbours per expansion block
+// (16 blocks per scene: the collision sweep is one pose per thread), so a lone scene's iteration
+// spreads over 17 CUs instead of 5.
+constexpr int HW_TAIL = 12, NBG_TAIL = 4;
 
 // allpath + findmin split over the block's HW waves: wave w evaluates words WPW·w+1..WPW·(w+1) for
 // its lanes' candidates (lane&3 = variant of the state in `s`), the per-wave winners are
 // combined in LDS in word order with the same total order (rs_before).  Every wave returns
 // the block-wide winner for its lanes; *best_id is the winning candidate id.
-template <bool CMD>
+template <bool CMD, int HWt>
 __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* best_id, double* sh_c, int* sh_i,
                                                 double* cmd_out = nullptr) {
+  constexpr int WPW = 12 / HWt;  // Reeds–Shepp words per wave
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, var = lane & 3;
   double q[3];
   rs_variant(s, var, q);
@@ -433,7 +439,7 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   __syncthreads();
   double v = sh_c[lane];
   int ix = sh_i[lane];
-  for (int w = 1; w < HW; w++) {
+  for (int w = 1; w < HWt; w++) {
     const double ov = sh_c[64 * w + lane];
     const int oi = sh_i[64 * w + lane];
     if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; }
@@ -463,7 +469,9 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
 
 // One search iteration's device work for the block (role by blockIdx: RS_connected or a
 // 16-neighbour group).  Returns false (block-uniformly) when the block has nothing to do.
+template <int HWt, int NBGt>
 __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) {
+  constexpr int HT = 64 * HWt, NBG = NBGt;
   __shared__ double wp[MAXW * 10];
   __shared__ double wpre[MAXW * 24];
   __shared__ double cmd[15];
@@ -477,7 +485,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   __shared__ int sh_n;
   const int per = 1 + (P.n_prim + NBG - 1) / NBG;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
-  if (slot >= A.n_active) return false;
+  if (slot >= (A.n_live ? *A.n_live : A.n_active)) return false;  // past the live-scene list
   if (item == 0 && !A.do_rs) return false;
   if (item > 0 && !A.do_exp) return false;
   const bool rs = item == 0;  // block-uniform role: RS_connected, else a 16-neighbour group
@@ -554,7 +562,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     double ns[3];
     change_basis(node, goal, P.minR, ns);
     HTIME(2);
-    cb = rs_best_split<true>(ns, tid, &best, red_c, red_i, cmd);
+    cb = rs_best_split<true, HWt>(ns, tid, &best, red_c, red_i, cmd);
     HTIME(3);
     // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment, all segments
     // at once -- the heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt over every step (one lane),
@@ -567,19 +575,27 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       nseg++;
     }
     const int nst = 100 * nseg;
-    if (tid == 0) {
-      double q = node[2];
-      psi_s[0] = q;
-      for (int seg = 0; seg < nseg; seg++) {
-        const double dt = __builtin_fabs(cmd[seg * 3]) / 100;
-        const double c = (cmd[seg * 3 + 2] * cmd[seg * 3 + 1]) * dt;
+    // the heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt, segment by segment: all 100 steps at once when
+    // the closed form of repeated addition applies (mpj_rep_add_ok: same bits), else on one lane
+    if (tid == 0) psi_s[0] = node[2];
+    __syncthreads();
+    for (int seg = 0; seg < nseg; seg++) {
+      const double q0 = psi_s[seg * 100];
+      const double dt = __builtin_fabs(cmd[seg * 3]) / 100;
+      const double c = (cmd[seg * 3 + 2] * cmd[seg * 3 + 1]) * dt;
+      double d;
+      if (mpj_rep_add_ok(q0, c, 100, &d)) {
+        for (int k = tid; k < 100; k += HT) psi_s[seg * 100 + k + 1] = c == 0.0 ? q0 + c : mpj_fma(k + 1, d, q0);
+      } else if (tid == 0) {
+        double q = q0;
         for (int k = 0; k < 100; k++) {
           q = q + c;
           psi_s[seg * 100 + k + 1] = q;
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
+    HTIME(6);
     for (int t = tid; t < nst; t += HT) {  // per-step increments
       const int seg = t / 100;
       const double dt = __builtin_fabs(cmd[seg * 3]) / 100, v = cmd[seg * 3 + 1];
@@ -592,43 +608,68 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       iy_s[t] = d1 * dt;
       path_s[3 * (t + 1) + 2] = psi_s[t + 1];
     }
+    if (tid == 0) {
+      path_s[0] = node[0];
+      path_s[1] = node[1];
+    }
     __syncthreads();
-    if (tid == 0 || tid == 64) {  // running sums in order: x on wave 0, y on wave 1
-      const int c = tid == 0 ? 0 : 1;
-      const double* inc = c == 0 ? ix_s : iy_s;
-      double acc = node[c];
-      path_s[c] = acc;
-      // batches of 20 increments into registers first: the LDS reads then pipeline instead of
-      // each waiting behind the previous path store (the compiler cannot disprove aliasing)
-      for (int t0 = 0; t0 < nst; t0 += 20) {  // nst is a multiple of 100
-        double v[20];
+    HTIME(7);
+    // running sums in order, segment by segment: a straight segment (every increment the same bits)
+    // in closed form, else x on wave 0's first lane and y on wave 1's
+    for (int seg = 0; seg < nseg; seg++) {
+      const int t0 = seg * 100;
+      const double x0 = path_s[3 * t0], y0 = path_s[3 * t0 + 1];
+      const double ix = ix_s[t0], iy = iy_s[t0];
+      const bool same = __double_as_longlong(psi_s[t0]) == __double_as_longlong(psi_s[t0 + 1]) &&
+                        cmd[seg * 3 + 2] * cmd[seg * 3 + 1] == 0.0;  // ψ constant over the segment
+      double dx, dy;
+      const bool cx = same && mpj_rep_add_ok(x0, ix, 100, &dx), cy = same && mpj_rep_add_ok(y0, iy, 100, &dy);
+      for (int k = tid; k < 100; k += HT) {
+        if (cx) path_s[3 * (t0 + k + 1)] = ix == 0.0 ? x0 + ix : mpj_fma(k + 1, dx, x0);
+        if (cy) path_s[3 * (t0 + k + 1) + 1] = iy == 0.0 ? y0 + iy : mpj_fma(k + 1, dy, y0);
+      }
+      if ((tid == 0 && !cx) || (tid == 64 && !cy)) {
+        const int c = tid == 0 ? 0 : 1;
+        const double* inc = c == 0 ? ix_s : iy_s;
+        double acc = c == 0 ? x0 : y0;
+        // batches of 20 increments into registers first: the LDS reads then pipeline instead of
+        // each waiting behind the previous path store (the compiler cannot disprove aliasing)
+        for (int u0 = t0; u0 < t0 + 100; u0 += 20) {
+          double v[20];
 #pragma unroll
-        for (int u = 0; u < 20; u++) v[u] = inc[t0 + u];
+          for (int u = 0; u < 20; u++) v[u] = inc[u0 + u];
 #pragma unroll
-        for (int u = 0; u < 20; u++) {
-          acc = acc + v[u];
-          path_s[3 * (t0 + u + 1) + c] = acc;
+          for (int u = 0; u < 20; u++) {
+            acc = acc + v[u];
+            path_s[3 * (u0 + u + 1) + c] = acc;
+          }
         }
       }
+      __syncthreads();
     }
+    HTIME(8);
     if (tid == 0) path_s[2] = node[2];
     __syncthreads();
     const int n = nst + 1;
     for (int i = tid; i < 3 * n; i += HT) R.path[i] = path_s[i];
     if (tid == 0) sh_n = n;
+    HTIME(4);
     sweep(n > 5 ? (n - 1) / 5 + 1 : 1);  // block_collision_check on poses 1:5:end
+    HTIME(5);
   } else {
     // dg_cost first (primitive poses 1:5:n_col): rs_heuristic is only used for neighbours that
     // are collision-free and in bounds, so a group without one skips the 48 RS candidates
     sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
+    HTIME(4);
     __syncthreads();
+    HTIME(5);
     int any = 0;
     for (int q = 0; q < nk; q++) any |= (g_ix[q] != 0) & g_free[q];
     if (any) {  // block-uniform
       double ns[3];
       change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
       HTIME(2);
-      cb = rs_best_split<false>(ns, tid, &best, red_c, red_i);
+      cb = rs_best_split<false, HWt>(ns, tid, &best, red_c, red_i);
       HTIME(3);
     }
   }
@@ -648,7 +689,10 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   return true;
 }
 
-__global__ __launch_bounds__(HT) void ha_iter_kernel(HaDev P, IterArgs A) { ha_iter_body(P, A); }
+template <int HWt, int NBGt>
+__global__ __launch_bounds__(64 * HWt) void ha_iter_kernel(HaDev P, IterArgs A) {
+  ha_iter_body<HWt, NBGt>(P, A);
+}
 
 
 // allpath over B normalised states: 16 states per wave, lanes 4j..4j+3 = the four variants
@@ -728,7 +772,7 @@ int need_prims(mp_ctx* ctx, const mp_ha_params* p) {
 int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
   if (A.n_active <= 0) return MP_OK;
   mp_time_begin(ctx);
-  hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(A.n_active * (1 + (D.n_prim + NBG - 1) / NBG))), dim3(HT), 0,
+  hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(A.n_active * (1 + (D.n_prim + NBG - 1) / NBG))), dim3(HT), 0,
                      ctx->stream, D, A);
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
@@ -779,6 +823,7 @@ struct HaSearch {
   double* states;        // [B][mp][3] hybrid_astar_states (goal side first)
   double* node;          // [B][3] popped node state: the next iteration's input
   int* live;             // [mp + 2] scenes still searching after iteration i
+  int* lst;              // [2][B] those scenes' indices (iteration i writes list i & 1, in any order)
 };
 enum { SI_NNODES = 0, SI_NOPEN, SI_LOOP, SI_CUR, SI_ACTIVE, SI_FOUND, SI_NSTATES, SI_RSLEN, SI_N };
 
@@ -1049,7 +1094,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   // ---- next popfirst!
   const bool go = ha_pop(Q, B, b, n_open, loop, tid);
   if (tid == 0) {
-    if (go) atomicAdd(Q.live + it, 1);
+    if (go) Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;
     else {
       Q.sc_i[SI_ACTIVE * B + b] = 0;
       Q.sc_i[SI_NOPEN * B + b] = n_open;
@@ -1058,7 +1103,10 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
 }
 
 __global__ __launch_bounds__(BKT) void ha_book_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
-  ha_book(P, Q, A, B, it, blockIdx.x);
+  // the scenes live entering this iteration: the list the previous iteration's bookkeeping wrote
+  // (iteration 1: every scene, inactive ones return at once)
+  if (A.n_live && (int)blockIdx.x >= *A.n_live) return;
+  ha_book(P, Q, A, B, it, A.scene_of ? A.scene_of[blockIdx.x] : (int)blockIdx.x);
 }
 
 
@@ -1426,7 +1474,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 24 +
-                                           sizeof(int) * (mp + 2) + 256 * 32);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 2 * nB + 256 * 32);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -1457,6 +1505,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.states = (double*)take(nB * mp * 24);
   Q.node = (double*)take(nB * 24);
   Q.live = (int*)take(sizeof(int) * (mp + 2));
+  Q.lst = (int*)take(sizeof(int) * 2 * nB);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
@@ -1502,12 +1551,25 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   hipEvent_t ev[NCK];
   for (int i = 0; i < NCK; i++) MP_HIP(ctx, hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   auto cleanup = [&] { for (int i = 0; i < NCK; i++) hipEventDestroy(ev[i]); };
-  const int per = 1 + (np + NBG - 1) / NBG;
+  const int per = 1 + (np + NBG - 1) / NBG, per_tail = 1 + (np + NBG_TAIL - 1) / NBG_TAIL;
+  // iteration it >= 2 works on the compact list of scenes still live (written by the previous
+  // bookkeeping launch, count on the device); the host sizes the grids by the last live count it has
+  // seen (an upper bound: it only decreases) and switches to the tail shape once that many scenes
+  // fit in about two blocks per CU
+  const int tail_blocks = 512;
+  int known = B;
   int chunk = 0, checked = 0;
   bool finished = false;
   for (int it = 1; it <= mp && !finished; it++) {
-    hipLaunchKernelGGL(ha_iter_kernel, dim3((unsigned)(B * per)), dim3(HT), 0, ctx->stream, D, A);
-    hipLaunchKernelGGL(ha_book_kernel, dim3(B), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
+    A.scene_of = it == 1 ? nullptr : Q.lst + ((it - 1) & 1) * B;
+    A.n_live = it == 1 ? nullptr : Q.live + (it - 1);
+    A.n_active = known;
+    if (known * per_tail <= tail_blocks)
+      hipLaunchKernelGGL((ha_iter_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)), dim3(64 * HW_TAIL), 0,
+                         ctx->stream, D, A);
+    else
+      hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
+    hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
     if (it % CH == 0 || it == mp) {
       const int slot = chunk % NCK;
@@ -1525,6 +1587,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         if (q == hipErrorNotReady) break;
         if (q != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "event wait failed"); }
         if (hl[cs] == 0) { finished = true; break; }
+        known = std::min(known, std::max(hl[cs], 1));
         checked++;
       }
     }
