@@ -304,6 +304,21 @@ __device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const 
   return 1;
 }
 
+// one (wall, direction) term of pose_free: d = 0 SAT(wall, vehicle), d = 1 SAT(vehicle, wall); the pose
+// is free iff every term of every wall is 1 (ConvexCollision = SAT(wall, veh) && SAT(veh, wall))
+__device__ __forceinline__ int pose_free_part(const HaDev& P, const double* q, const double* wp, const double* wpre,
+                                              int w, int d) {
+  double sq, cq;
+  mpj_sincos_bl(q[2], &sq, &cq);
+  const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
+  const double yaw = mpj_modpi_bl(q[2]);
+  double sy = sq, cy = cq;
+  if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);
+  double vp[10];
+  rect_pts(x, y, cy, sy, P.L2, P.W2, vp);
+  return d == 0 ? sat_pre(wpre + 24 * w, vp) : sat(vp, wp + 10 * w);
+}
+
 // transform (hybrid_astar_utils.jl:459-481) with the node's cos/sin given
 __device__ __forceinline__ void transform_cs(const double* node, double c, double s, const double* q, double* o) {
   o[0] = q[0] * c - q[1] * s + node[0];
@@ -535,13 +550,17 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   HTIME(1);
   __syncthreads();
   const int j = lane >> 2;
-  // collision sweep: (neighbour, pose) pairs of this group, or the RS path's poses
+  // collision sweep: (neighbour, pose) pairs of this group, or the RS path's poses; the tail shape
+  // (threads to spare) splits every pose into its 2·n_walls SAT terms, one per thread
+  constexpr bool SPLIT = HWt == HW_TAIL;
   auto sweep = [&](int npose) {
     double nsn = 0.0, ncs = 1.0;
     if (!rs) mpj_sincos_bl(node[2], &nsn, &ncs);
-    const int total = rs ? npose : nk * npose;
+    const int parts = SPLIT ? 2 * nw : 1;
+    const int total = (rs ? npose : nk * npose) * parts;
     for (int t = tid; t < total; t += HT) {
-      const int jn = rs ? 0 : t / npose, jp = rs ? t : t - jn * npose;
+      const int tp = SPLIT ? t / parts : t, part = SPLIT ? t - tp * parts : 0;
+      const int jn = rs ? 0 : tp / npose, jp = rs ? tp : tp - jn * npose;
       if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
       if (!g_free[jn]) continue;  // already colliding: block_collision_check stops at its first hit
       double q[3];
@@ -552,7 +571,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       } else {
         transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
       }
-      if (!pose_free(P, q, wp, wpre, nw)) g_free[jn] = 0;  // every writer stores 0
+      const int fr = SPLIT ? pose_free_part(P, q, wp, wpre, part >> 1, part & 1) : pose_free(P, q, wp, wpre, nw);
+      if (!fr) g_free[jn] = 0;  // every writer stores 0
     }
   };
   double cb = 0.0;
