@@ -40,9 +40,16 @@ __device__ int* g_ha_dbg;
     if (threadIdx.x == 0)                                                                          \
       reinterpret_cast<unsigned long long*>(g_ha_dbg + 64 * 64)[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// bookkeeping-kernel stamps of scene b at [b][16] after the iteration kernel's 4096 blocks
+#define BTIME(i)                                                                                   \
+  do {                                                                                             \
+    if (threadIdx.x == 0 && it == 20)                                                              \
+      reinterpret_cast<unsigned long long*>(g_ha_dbg + 64 * 64)[(4096 + b) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define HMARK(ph)
 #define HTIME(i)
+#define BTIME(i)
 #endif
 
 struct HaDev {
@@ -854,6 +861,33 @@ __device__ __forceinline__ bool key_before(double af, long long as, double cf, l
   return as < cs;
 }
 
+// lane exchanges without LDS round trips: DPP row operations, v_readlane
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ long long dpp_l(long long x) {
+  const int lo = dpp_i<CTRL>((int)x), hi = dpp_i<CTRL>((int)(x >> 32));
+  return ((long long)hi << 32) | (unsigned int)lo;
+}
+__device__ __forceinline__ long long readlane_l(long long x, int l) {
+  const int lo = __builtin_amdgcn_readlane((int)x, l), hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return ((long long)hi << 32) | (unsigned int)lo;
+}
+// (f, seq, pos) <- the open-list-order minimum of itself and the DPP partner's (pos < 0: none)
+template <int CTRL>
+__device__ __forceinline__ void key_min_dpp(double& f, long long& sq, int& p) {
+  const double of = __longlong_as_double(dpp_l<CTRL>(__double_as_longlong(f)));
+  const long long os = dpp_l<CTRL>(sq);
+  const int op = dpp_i<CTRL>(p);
+  if (op >= 0 && (p < 0 || key_before(of, os, f, sq))) {
+    f = of;
+    sq = os;
+    p = op;
+  }
+}
+
 // popfirst! for scene b (a 256-thread block): the least (f, seq) open entry, found by a
 // strided scan (4 independent entry loads in flight per thread) and a wave then block
 // reduction (the key order is total, so the reduction order does not matter); wave 0 removes
@@ -864,9 +898,24 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   __shared__ double r_f[BKT / 64];
   __shared__ long long r_s[BKT / 64];
   __shared__ int r_p[BKT / 64];
+  __shared__ double r_pay[BKT / 64][5];  // the wave winner's entry: g, Encode index, state
+  __shared__ int r_id[BKT / 64];
   const size_t base = (size_t)b * Q.C;
   if (n_open == 0 || loop >= Q.mp) return false;
   const int lane = tid & 63, wave = tid >> 6;
+  const int last = n_open - 1;
+  // the last entry (moved into the winner's place) does not depend on the scan: loaded first
+  double fl = 0.0, gl = 0.0, stl = 0.0;
+  long long sl = 0, il = 0;
+  int lid = 0;
+  if (tid < 64) {
+    fl = Q.of[base + last];
+    gl = Q.og[base + last];
+    sl = Q.oseq[base + last];
+    il = Q.oix[base + last];
+    lid = Q.oid[base + last];
+    if (lane < 3) stl = Q.ost[(base + last) * 3 + lane];
+  }
   double bf = __builtin_inf();
   long long bs = 0x7fffffffffffffffLL;
   int bp = -1;
@@ -885,33 +934,59 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
       if (p < n_open && (bp < 0 || key_before(fv[u], sv[u], bf, bs))) { bf = fv[u]; bs = sv[u]; bp = p; }
     }
   }
+  // the thread's own best entry's payload, loaded now so that its latency hides behind the reductions
+  // (no dependent load after the winner is known)
+  int pid = 0;
+  double pg = 0.0, pix = 0.0, p0s = 0.0, p1s = 0.0, p2s = 0.0;
+  if (bp >= 0) {
+    pid = Q.oid[base + bp];
+    pg = Q.og[base + bp];
+    pix = __longlong_as_double(Q.oix[base + bp]);
+    p0s = Q.ost[(base + bp) * 3];
+    p1s = Q.ost[(base + bp) * 3 + 1];
+    p2s = Q.ost[(base + bp) * 3 + 2];
+  }
+  const int own = bp;
+  // wave minimum: quad xor 1 / xor 2, half-row and row mirrors, then the four rows by v_readlane
+  key_min_dpp<0xB1>(bf, bs, bp);
+  key_min_dpp<0x4E>(bf, bs, bp);
+  key_min_dpp<0x141>(bf, bs, bp);
+  key_min_dpp<0x140>(bf, bs, bp);
+  {
+    double wf = __longlong_as_double(readlane_l(__double_as_longlong(bf), 0));
+    long long ws = readlane_l(bs, 0);
+    int wp_ = __builtin_amdgcn_readlane(bp, 0);
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const double of_ = __shfl_xor(bf, o);
-    const long long os = __shfl_xor(bs, o);
-    const int op = __shfl_xor(bp, o);
-    if (op >= 0 && (bp < 0 || key_before(of_, os, bf, bs))) { bf = of_; bs = os; bp = op; }
+    for (int r = 1; r < 4; r++) {
+      const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(bf), 16 * r));
+      const long long os = readlane_l(bs, 16 * r);
+      const int op = __builtin_amdgcn_readlane(bp, 16 * r);
+      if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
+    }
+    bf = wf;
+    bs = ws;
+    bp = wp_;
   }
   if (lane == 0) { r_f[wave] = bf; r_s[wave] = bs; r_p[wave] = bp; }
+  if (bp >= 0 && own == bp) {  // the one lane that scanned the wave's winning position
+    r_id[wave] = pid;
+    r_pay[wave][0] = pg;
+    r_pay[wave][1] = pix;
+    r_pay[wave][2] = p0s;
+    r_pay[wave][3] = p1s;
+    r_pay[wave][4] = p2s;
+  }
   __syncthreads();
   if (tid >= 64) return true;
+  int ww = 0;
   for (int w = 1; w < BKT / 64; w++) {
     const int op = r_p[w];
-    if (op >= 0 && (bp < 0 || key_before(r_f[w], r_s[w], bf, bs))) { bf = r_f[w]; bs = r_s[w]; bp = op; }
+    if (op >= 0 && (bp < 0 || key_before(r_f[w], r_s[w], bf, bs))) { bf = r_f[w]; bs = r_s[w]; bp = op; ww = w; }
   }
-  // the winning entry (one dependent load) and the last entry (moved into its place)
-  const int last = n_open - 1;
-  const int id = Q.oid[base + bp];
-  const double gw = Q.og[base + bp];
-  const long long iw = Q.oix[base + bp];
-  double stw = 0.0, stl = 0.0;
-  if (lane < 3) {
-    stw = Q.ost[(base + bp) * 3 + lane];
-    stl = Q.ost[(base + last) * 3 + lane];
-  }
-  const double fl = Q.of[base + last], gl = Q.og[base + last];
-  const long long sl = Q.oseq[base + last], il = Q.oix[base + last];
-  const int lid = Q.oid[base + last];
+  const int id = r_id[ww];
+  const double gw = r_pay[ww][0];
+  const long long iw = __double_as_longlong(r_pay[ww][1]);
+  const double stw = lane < 3 ? r_pay[ww][2 + lane] : 0.0;
   if (bp != last) {
     if (lane == 0) {
       Q.of[base + bp] = fl;
@@ -977,11 +1052,32 @@ __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B
 __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, int B, int it, int b) {
   __shared__ int s_nopen;
   const int tid = threadIdx.x, lane = tid & 63;
-  if (!Q.sc_i[SI_ACTIVE * B + b]) return;
+  BTIME(0);
   const size_t base = (size_t)b * Q.C;
   const int np = P.n_prim;
+  // one round of independent loads: the scene's counters and wave 0's neighbour record (lane k)
+  const int active = Q.sc_i[SI_ACTIVE * B + b];
+  const int rs_ok = A.rs_ok[b];
   const int loop = Q.sc_i[SI_LOOP * B + b];
-  if (A.rs_ok[b]) {  // RS_connected: path found -> hybrid_astar_states by the parent chain
+  const int n_open0 = Q.sc_i[SI_NOPEN * B + b];
+  const int nn0 = Q.sc_i[SI_NNODES * B + b];
+  const long long ctr = Q.ctr[b];
+  const double cur_g = Q.cur_g[b];
+  const long long cidx = Q.cur_ix[b];
+  long long ix = 0;
+  int frk = 0;
+  double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
+  if (tid < np) {
+    ix = A.idx[(size_t)b * np + tid];
+    frk = A.fr[(size_t)b * np + tid];
+    hk = A.h[(size_t)b * np + tid];
+    nb0 = A.nb[((size_t)b * np + tid) * 3];
+    nb1 = A.nb[((size_t)b * np + tid) * 3 + 1];
+    nb2 = A.nb[((size_t)b * np + tid) * 3 + 2];
+  }
+  if (!active) return;
+  BTIME(1);
+  if (rs_ok) {  // RS_connected: path found -> hybrid_astar_states by the parent chain
     if (tid == 0) {
       Q.sc_i[SI_FOUND * B + b] = 1;
       Q.sc_i[SI_ACTIVE * B + b] = 0;
@@ -1001,23 +1097,29 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
     }
     return;
   }
+  BTIME(2);
   if (tid < 64) {
     // ---- FindNewNode (:391-447): only the first valid occurrence of an Encode index in this
     // expansion can change anything (every neighbour has the same tentative g)
-    int n_open = Q.sc_i[SI_NOPEN * B + b];
+    int n_open = n_open0;
     const int k = lane;
-    const long long ix = k < np ? A.idx[(size_t)b * np + k] : 0;
-    const bool valid = k < np && ix != 0 && A.fr[(size_t)b * np + k];
+    const bool valid = k < np && ix != 0 && frk;
     const long long vix = valid ? ix : 0;
+    BTIME(8);
+    // lane k is a duplicate when an earlier valid lane holds the same Encode index: every lane reads
+    // the 64 indices from LDS (uniform addresses: broadcast reads, all independent)
+    __shared__ long long s_vix[64];
+    s_vix[k] = vix;
+    __builtin_amdgcn_wave_barrier();
     bool dup = false;
 #pragma unroll 16
-    for (int j = 0; j < 64; j++) {  // lane exchange (no LDS round trip), loads independent of k
-      const long long oj = __shfl(vix, j);
-      dup = dup | (j < k && oj == ix);
+    for (int j = 0; j < 64; j++) {  // unconditional reads: no exec-masked branch per j
+      const long long oj = s_vix[j];
+      dup = dup | ((oj == ix) & (j < k));
     }
     const bool first = valid && !dup;
-    const double tg = Q.cur_g[b] + P.expand_time;
-    const long long cidx = Q.cur_ix[b];
+    BTIME(3);
+    const double tg = cur_g + P.expand_time;
     double th = 0.0, tf = 0.0;
     int id = -1;
     bool chg = false, app = false, isnew = false;
@@ -1026,7 +1128,6 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
     double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;  // the node's state and Encode index (its open entry)
     long long nix = ix;
     if (first) {
-      const double hk = A.h[(size_t)b * np + k];
       th = __builtin_fmax(hk, 0.0);
       if (hk != hk) th = hk;
       tf = tg + th;
@@ -1053,17 +1154,16 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
       } else {
         isnew = true;
         app = true;
-        nst0 = A.nb[((size_t)b * np + k) * 3];
-        nst1 = A.nb[((size_t)b * np + k) * 3 + 1];
-        nst2 = A.nb[((size_t)b * np + k) * 3 + 2];
+        nst0 = nb0;
+        nst1 = nb1;
+        nst2 = nb2;
       }
     }
+    BTIME(4);
     const unsigned long long m_new = __ballot(isnew), m_chg = __ballot(chg), m_app = __ballot(app);
     const unsigned long long below = (1ull << k) - 1;  // lanes < k
     const int n_new = __popcll(m_new), n_chg = __popcll(m_chg), n_app = __popcll(m_app);
-    const int nn0 = Q.sc_i[SI_NNODES * B + b];
     if (isnew) id = nn0 + __popcll(m_new & below);
-    const long long ctr = Q.ctr[b];
     // in-place updates keep their previous list order: rank by the old key among the changed
     int r = 0;
     for (unsigned long long m = m_chg; m; m &= m - 1) {
@@ -1109,10 +1209,13 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
       s_nopen = n_open;
     }
   }
+  BTIME(5);
   __syncthreads();  // the open-list writes of wave 0 before the block-wide scan
+  BTIME(6);
   const int n_open = s_nopen;
   // ---- next popfirst!
   const bool go = ha_pop(Q, B, b, n_open, loop, tid);
+  BTIME(7);
   if (tid == 0) {
     if (go) Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;
     else {

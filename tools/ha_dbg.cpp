@@ -67,6 +67,19 @@ int main() {
       printf("\n");
     }
   }
+  {  // a short plan of the same scene: phase stamps of the last bookkeeping launch (scene 0)
+    memset(buf, 0, 1 << 20);
+    p.max_pops = 40;
+    const double start[3] = {7, 0, M_PI / 2};
+    int32_t found, pops, nn, ns, rl;
+    static int64_t seq[40];
+    static double st[40 * 3], rs[501 * 3];
+    printf("plan %d\n", mp_ha_plan(ctx, &p, 1, start, goal, walls, &found, &pops, &nn, seq, &ns, st, &rl, rs));
+    const unsigned long long* t = reinterpret_cast<const unsigned long long*>(buf + 64 * 64) + 4096 * 16;
+    printf("book stamps (cycles from [0]):");
+    for (int i = 1; i < 16; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
+    printf("\npops %d\n", pops);
+  }
   mp_ctx_destroy(ctx);
   return 0;
 }
