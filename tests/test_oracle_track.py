@@ -149,3 +149,29 @@ def test_reference_endpoints_and_no_path():
     got = oracle.track(_params(his_stride=5), h.s.starting_real, 0.0, ret["samples"], his_cap=3)
     assert got["status"] == tracker.MP_TRACK_NOPATH and got["n_steps"] == 0
     assert np.array_equal(got["his"], np.array([h.s.starting_real]))
+
+
+def test_time_argmin_window_guard():
+    """The device's 8-candidate window for argmin(abs.(refined_length .- c)) (tracker.hip argmin_time_lane)
+    equals the full scan whenever its guard s > 4E holds: random tol, n_ref and c, the window logic restated
+    in numpy with the same float64 operations (lerp (1-t)a + tb, t = j/(n-1))."""
+    r = np.random.default_rng(11)
+    eps = 2.220446049250313e-16
+    checked = 0
+    for _ in range(3000):
+        n = int(r.choice([2, 3, 37, 50, 1000, 2048]))
+        tol = float(10 ** r.uniform(-4, 2.5))
+        c = float(r.uniform(0, tol + 3)) if r.random() < 0.9 else float(r.choice([0.0, tol, tol / 2]))
+        t = np.arange(n, dtype=np.float64) / float(n - 1)
+        a, b = 0.0 - c, tol - c
+        v = np.abs((1 - t) * a + t * b)
+        full = int(np.argmin(v))
+        E = 8 * eps * (abs(c) + abs(tol - c) + abs(tol - c) + tol)
+        if not tol / (n - 1) > 4 * E:
+            continue
+        g = min(max(np.rint(c * ((n - 1) / tol)), 0.0), n - 1.0)
+        js = np.clip(int(g) - 3 + np.arange(8), 0, n - 1)
+        win = int(js[np.argmin(v[js])])
+        assert win == full, (n, tol, c)
+        checked += 1
+    assert checked > 2500
