@@ -59,6 +59,14 @@ constexpr bool kFast = true;
 constexpr bool kFwdQuad = false;
 #else
 constexpr bool kFwdQuad = true;  // ilqr_forward_quad_kernel: a lane quad per instance
+#ifndef ILQR_SEARCH_L
+#define ILQR_SEARCH_L 4
+#endif
+constexpr int kSearchL = ILQR_SEARCH_L;  // lanes per line-search trial in mp_ilqr_solve (1 or 4)
+#ifndef ILQR_SEARCH_G
+#define ILQR_SEARCH_G 16
+#endif
+constexpr int kSearchG = ILQR_SEARCH_G;  // trials per instance in the first round (a power of two <= 16)
 #endif
 #if defined(MP_ILQR_FASTSC)
 constexpr bool kFastSC = true;
@@ -1071,14 +1079,18 @@ __device__ __forceinline__ void search_accept(const IlqrDev& P, size_t b, double
 
 // one_round: stop after round 0 and mark the instances still searching in pending[] (their
 // trials G..ls_cap then run all at once in ilqr_search_rest_kernel).
-template <int G>
+// L = lanes per trial: 1 (forward_trial on one lane) or 4 (forward_trial_quad: the trial's
+// exponentials and stage sincos spread over a lane quad, ~2.5x shorter chain per trial).
+template <int G, int L = 1>
 __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
                                                          const double* Kg, double* Xs, double* Us, double* Jcur,
                                                          int* active, int* iters, int* flags, int* n_active,
                                                          int one_round, int* pending) {
-  constexpr int IPW = 64 / G;  // instances per wave
-  const int lane = threadIdx.x, g = lane % G, sub = lane / G;
-  const int b0 = blockIdx.x * IPW + sub;
+  constexpr int GL = G * L;     // lanes per instance
+  constexpr int IPW = 64 / GL;  // instances per wave
+  static_assert(GL <= 64 && 64 % GL == 0, "G*L must divide 64");
+  const int lane = threadIdx.x, g = (lane % GL) / L, sub = lane % L, inst = lane / GL;
+  const int b0 = blockIdx.x * IPW + inst;
   const bool live = b0 < B && active[b0];
   if (__all(!live)) return;
   const size_t b = b0 < B ? b0 : B - 1;
@@ -1093,24 +1105,30 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   double Jn = J;
   int mw = -1;  // accepted trial index
   bool searching = live;
+  // lanes that report a trial's outcome: every lane (L = 1) or the quad's first
+  constexpr unsigned long long lead = L == 1 ? ~0ull : 0x1111111111111111ull;
   for (int r = 0; __any(searching) && !(one_round && r > 0); r++) {
     const int m = r * G + g;
-    const bool mine = searching && m <= P.ls_cap;
+    const bool mine = searching && m <= P.ls_cap;  // uniform over a trial's lanes
     double jt = 0.0;
     if (mine) {
-      int d = 0;
-      jt = forward_trial<false>(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, d);
+      if (L == 4) {
+        jt = forward_trial_quad(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, sub);
+      } else {
+        int d = 0;
+        jt = forward_trial<false>(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, d);
+      }
     }
     const bool stop = mine && (!(jt >= J) || m == P.ls_cap);
-    const unsigned long long bal = __ballot(stop);
-    const unsigned long long grp = (bal >> (sub * G)) & (G == 64 ? ~0ull : ((1ull << G) - 1));
-    const int gw = grp ? __builtin_ctzll(grp) : 0;
-    const double jw = __shfl(jt, sub * G + gw);  // every lane takes part in the exchange
+    const unsigned long long bal = __ballot(stop) & lead;
+    const unsigned long long grp = (bal >> (inst * GL)) & (GL == 64 ? ~0ull : ((1ull << GL) - 1));
+    const int gw = grp ? __builtin_ctzll(grp) / L : 0;
+    const double jw = __shfl(jt, inst * GL + gw * L);  // every lane takes part in the exchange
     if (searching && grp) {
       Jn = jw;
       mw = r * G + gw;
       searching = false;
-      // the instance's G lanes copy the winning slot together, 8 loads in flight per lane before
+      // the instance's lanes copy the winning slot together, 8 loads in flight per lane before
       // the stores (instead of the winner alone, one dependent load->store at a time): the
       // winner's slot stores are released at workgroup scope (the same wave) and L1 is
       // invalidated before the reads
@@ -1119,23 +1137,24 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
       const double* Xw = Xs + ((size_t)gw * B + b) * N * 4;
       const double* Uw = Us + ((size_t)gw * B + b) * N * 2;
       const size_t nx = N * 4, nt = N * 6;
-      for (size_t i0 = (size_t)g; i0 < nt; i0 += 8 * G) {
+      const int li = lane % GL;
+      for (size_t i0 = (size_t)li; i0 < nt; i0 += 8 * GL) {
         double v[8];
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-          const size_t i = i0 + (size_t)e * G;
+          const size_t i = i0 + (size_t)e * GL;
           v[e] = i < nx ? Xw[i] : i < nt ? Uw[i - nx] : 0.0;
         }
 #pragma unroll
         for (int e = 0; e < 8; e++) {
-          const size_t i = i0 + (size_t)e * G;
+          const size_t i = i0 + (size_t)e * GL;
           if (i < nx) Xb[i] = v[e];
           else if (i < nt) Ub[i - nx] = v[e];
         }
       }
     }
   }
-  if (!live || g != 0) return;
+  if (!live || (lane % GL) != 0) return;
   if (searching) {  // one_round only: trials G..ls_cap follow in ilqr_search_rest_kernel
     pending[b] = 1;
     return;
@@ -1144,20 +1163,29 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
 }
 
 // Trials G..ls_cap of the instances still searching after round 0, all at once: block (b, w)
-// runs trials m = G + 64w + lane into slots [b][m-G] (Xs2/Us2/Jt), and the first stopping
-// trial is the least m whose loop test would end the reference's halving loop (atomicMin).
-template <int G>
+// runs trials m = G + (64/L)w + lane/L into slots [b][m-G] (Xs2/Us2/Jt), one lane (L = 1) or a
+// lane quad (L = 4) per trial, and the first stopping trial is the least m whose loop test would
+// end the reference's halving loop (atomicMin).
+template <int G, int L = 1>
 __global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                               const double* k, const double* Kg, const double* Jcur,
                                                               const int* pending, double* Xs2, double* Us2,
                                                               double* Jt, int* winm) {
-  const int b = blockIdx.x, m = G + 64 * (int)blockIdx.y + (int)threadIdx.x;
-  if (!pending[b] || m > P.ls_cap) return;
+  const int b = blockIdx.x, sub = (int)threadIdx.x % L, m = G + (64 / L) * (int)blockIdx.y + (int)threadIdx.x / L;
+  if (!pending[b] || m > P.ls_cap) return;  // uniform over a trial's lanes
   const size_t N = P.N, T2 = (size_t)(P.ls_cap + 1 - G), t = (size_t)(m - G);
-  int d = 0;
-  const double jt = forward_trial<false>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
-                                         ldexp(1.0, -m), Xs2 + ((size_t)b * T2 + t) * N * 4,
-                                         Us2 + ((size_t)b * T2 + t) * N * 2, true, d);
+  double jt;
+  if (L == 4) {
+    jt = forward_trial_quad(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
+                            ldexp(1.0, -m), Xs2 + ((size_t)b * T2 + t) * N * 4, Us2 + ((size_t)b * T2 + t) * N * 2,
+                            true, sub);
+  } else {
+    int d = 0;
+    jt = forward_trial<false>(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
+                              ldexp(1.0, -m), Xs2 + ((size_t)b * T2 + t) * N * 4, Us2 + ((size_t)b * T2 + t) * N * 2,
+                              true, d);
+  }
+  if (sub != 0) return;
   Jt[(size_t)b * T2 + t] = jt;
   if (!(jt >= Jcur[b]) || m == P.ls_cap) atomicMin(winm + b, m);
 }
@@ -1404,12 +1432,13 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   double* dU = (double*)mp_upload(ctx, WS_IO1, U, 2 * N * B, &st);
   double* dk = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * 2 * (N - 1) * B);
   double* dK = (double*)mp_ws(ctx, WS_IO3, sizeof(double) * 8 * (N - 1) * B);
-  // trial slots for the G-wide line search: G = 16 (1024 waves at B = 4096) while the slots stay
-  // within 1 GiB of HBM (and the context's workspace cap), else 4, else 1 (the sequential loop)
+  // trial slots for the G-wide line search: G = kSearchG = 16 trials per instance on lane quads
+  // (4096 waves at B = 4096) while the slots stay within 1 GiB of HBM (and the context's workspace
+  // cap), else 4 single-lane trials, else 1 (the sequential loop)
   auto fits = [&](size_t g) {  // X slots 32 B, U slots 16 B per (trial, instance, knot)
     return g * B * N * 48 <= ((size_t)1 << 30) && (!ctx->ws_limit || g * B * N * 32 <= ctx->ws_limit);
   };
-  const int G = fits(16) ? 16 : fits(4) ? 4 : 1;
+  const int G = fits(kSearchG) ? kSearchG : fits(4) ? 4 : 1;
   double* dXn = (double*)mp_ws(ctx, WS_IO4, sizeof(double) * 4 * N * B * G);
   double* dUn = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 2 * N * B * G);
   double* dJ = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * B);
@@ -1419,11 +1448,11 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   int* dit = dint + B;
   int* dfl = dint + 2 * B;
   int* dn = dint + 3 * B;
-  // trials G..ls_cap in one pass for the instances still searching after round 0 (G = 16 only),
+  // trials G..ls_cap in one pass for the instances still searching after round 0 (G = kSearchG only),
   // while their slots fit in 8 GiB, in half of the free device memory and in the context's
   // workspace cap.  Otherwise -- or when allocating them fails -- the G-wide kernel runs its
   // rounds to the end: the same accepted trials (tests/test_gpu_ilqr.py), more latency.
-  const size_t T2 = G == 16 && D.ls_cap + 1 > G ? (size_t)(D.ls_cap + 1 - G) : 0;
+  const size_t T2 = G == kSearchG && D.ls_cap + 1 > G ? (size_t)(D.ls_cap + 1 - G) : 0;
   bool rest = T2 > 0 && T2 * B * N * 48 <= ((size_t)8 << 30) &&
               mp_ws_affordable(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2, 0.5) &&
               mp_ws_affordable(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2, 0.25);
@@ -1448,14 +1477,16 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     if ((st = run_backward(ctx, D, B, dX, dU, dact, dk, dK))) return st;
     MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
     mp_time_begin(ctx);
-    const dim3 gs((unsigned)((B + 64 / G - 1) / (64 / G)));
+    // G = 16: a lane quad per trial (4 waves per SIMD at B = 4096); the narrower fallbacks one lane
+    const int ipw = G == kSearchG ? 64 / (kSearchG * kSearchL) : 64 / G;
+    const dim3 gs((unsigned)((B + ipw - 1) / ipw));
     if (rest) {
       MP_HIP(ctx, hipMemsetAsync(dpw, 0, sizeof(int) * B, ctx->stream));             // pending
       MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));      // winm = 0x7f7f7f7f
     }
-    if (G == 16)
-      hipLaunchKernelGGL(ilqr_search_kernel<16>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn,
-                         rest ? 1 : 0, dpw);
+    if (G == kSearchG)
+      hipLaunchKernelGGL((ilqr_search_kernel<kSearchG, kSearchL>), gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact,
+                         dit, dfl, dn, rest ? 1 : 0, dpw);
     else if (G == 4)
       hipLaunchKernelGGL(ilqr_search_kernel<4>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn,
                          0, dpw);
@@ -1464,10 +1495,10 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
                          0, dpw);
     MP_HIP(ctx, hipGetLastError());
     if (rest) {
-      hipLaunchKernelGGL(ilqr_search_rest_kernel<16>, dim3((unsigned)B, (unsigned)((T2 + 63) / 64)), b1, 0, ctx->stream, D,
-                         B, dX, dU, dk, dK, dJ, dpw, dXs2, dUs2, dJt, dpw + B);
+      hipLaunchKernelGGL((ilqr_search_rest_kernel<kSearchG, kSearchL>), dim3((unsigned)B, (unsigned)((T2 + 64 / kSearchL - 1) /
+                         (64 / kSearchL))), b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dJ, dpw, dXs2, dUs2, dJt, dpw + B);
       MP_HIP(ctx, hipGetLastError());
-      hipLaunchKernelGGL(ilqr_search_finish_kernel<16>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dpw, dXs2,
+      hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dpw, dXs2,
                          dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn);
       MP_HIP(ctx, hipGetLastError());
     }
