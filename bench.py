@@ -293,6 +293,16 @@ def bench_ilqr(ctx, world, rank, cpu=False, reps=20, B=4096, N=100):
            "value": world * units * reps / el, "kernel_rate": world * units / (kms * 1e-3), "kernel_ms": kms,
            "ms_per_pass": el / reps * 1e3, "dtype": "f64", "scaling": "weak", "valid": bool(np.isfinite(Jn).all()),
            "bound": "latency (fp64 FD derivatives; serial Riccati sweep per instance)"}
+    # the whole ILQR.jl loop (mp_ilqr_solve: backward + 16-wide quad line search per iteration, at most
+    # 60 iterations; instances that never find a decrease stop at max_ls and are reported, not hidden)
+    ps = ilqr.params(N=N, max_iter=60)
+    ilqr.ilqr_solve(ps, X, U, ctx=ctx)
+    t0 = time.perf_counter()
+    Xs, Us, Js, its, okk = ilqr.ilqr_solve(ps, X, U, ctx=ctx)
+    es = _sync_max(time.perf_counter() - t0, world, dev)
+    out["solve"] = {"workload": f"mp_ilqr_solve, {B} instances x H={N}, max_iter 60", "ms": es * 1e3,
+                    "iterations_max": int(its.max()), "iterations_mean": float(its.mean()),
+                    "all_converged": bool(okk)}
     if cpu:
         import oracle
 
