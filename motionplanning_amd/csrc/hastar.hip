@@ -294,10 +294,26 @@ __device__ __forceinline__ int sat_pre(const double* pre, const double* other) {
   return 0;
 }
 
-// vehicle pose q=[x,y,ψ] (rear axle) against all walls (corners wp and SAT tables wpre in
-// LDS); 1 = free
+// Wall table row: corners (10) + wall-side SAT table (24) + [center x, center y, far²] (3).
+// far² = (√2 (r_vehicle + r_wall) + 1e-6)², r = a rectangle's circumradius.  When the vehicle's
+// centre is farther than that from a wall's centre, ConvexCollision(wall, vehicle) is false for
+// certain: each rectangle has an edge normal within 45° of the centre-to-centre direction d, along
+// which the centres are >= |d|/√2 apart while each rectangle projects within its circumradius of
+// its centre, so BOTH SeparatingAxisTheorem calls find a separating axis -- with a gap of >= 1e-6 m
+// against rounding errors below 1e-12 m at these coordinates.  Such walls skip their SAT pair
+// (the booleans, hence every planner decision, are unchanged; tests/test_oracle_hastar.py checks
+// the bound against the oracle's SAT).
+constexpr int WT = 37;
+__device__ __forceinline__ double wall_far2(const HaDev& P, const double* wl) {
+  const double rv = mpj_sqrt(P.L2 * P.L2 + P.W2 * P.W2), rw = mpj_sqrt(wl[3] * wl[3] + wl[4] * wl[4]);
+  const double f = 1.4142135623730951 * (rv + rw) * (1 + 1e-12) + 1e-6;
+  return f * f;
+}
+
+// vehicle pose q=[x,y,ψ] (rear axle) against all walls (corners wp, SAT tables wpre and centres /
+// far² wc in LDS); 1 = free
 __device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const double* wp, const double* wpre,
-                                         int nw) {
+                                         const double* wc, int nw) {
   double sq, cq;
   mpj_sincos_bl(q[2], &sq, &cq);
   const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
@@ -306,18 +322,23 @@ __device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const 
   if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);  // |ψ| > π: the wrapped yaw's own sin/cos
   double vp[10];
   rect_pts(x, y, cy, sy, P.L2, P.W2, vp);
-  for (int i = 0; i < nw; i++)
+  for (int i = 0; i < nw; i++) {
+    const double dx = x - wc[3 * i], dy = y - wc[3 * i + 1];
+    if (dx * dx + dy * dy > wc[3 * i + 2]) continue;  // far from this wall: separated for certain
     if (!(sat_pre(wpre + 24 * i, vp) && sat(vp, wp + 10 * i))) return 0;
+  }
   return 1;
 }
 
 // one (wall, direction) term of pose_free: d = 0 SAT(wall, vehicle), d = 1 SAT(vehicle, wall); the pose
 // is free iff every term of every wall is 1 (ConvexCollision = SAT(wall, veh) && SAT(veh, wall))
 __device__ __forceinline__ int pose_free_part(const HaDev& P, const double* q, const double* wp, const double* wpre,
-                                              int w, int d) {
+                                              const double* wc, int w, int d) {
   double sq, cq;
   mpj_sincos_bl(q[2], &sq, &cq);
   const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
+  const double fx = x - wc[3 * w], fy = y - wc[3 * w + 1];
+  if (fx * fx + fy * fy > wc[3 * w + 2]) return 1;  // far from this wall: separated for certain
   const double yaw = mpj_modpi_bl(q[2]);
   double sy = sq, cy = cq;
   if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);
@@ -369,7 +390,7 @@ struct IterArgs {
   const double* pc;      // [n_prim][n_col][3]
   const int* scene_of;   // active slot -> scene index (nullptr: slot = scene)
   const int* active;     // per-scene live flag (device-resident search), nullptr = all
-  const double* wtab;    // [B][nw][34] wall corners (10) + SAT tables (24), nullptr = compute
+  const double* wtab;    // [B][nw][WT] wall corners (10) + SAT tables (24) + centre, far², nullptr = compute
   const int* n_live;     // device count of the scene_of list (nullptr: n_active)
   int n_active;
   int do_rs, do_exp;
@@ -496,6 +517,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   constexpr int HT = 64 * HWt, NBG = NBGt;
   __shared__ double wp[MAXW * 10];
   __shared__ double wpre[MAXW * 24];
+  __shared__ double wc[MAXW * 3];
   __shared__ double cmd[15];
   __shared__ double psi_s[MAXPATH], ix_s[MAXPATH], iy_s[MAXPATH];
   __shared__ double path_s[MAXPATH * 3];
@@ -524,17 +546,21 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   // wall corners (Block2Pts) and their SAT tables in LDS: precomputed once per plan
   // (ha_wall_kernel) or evaluated here
   if (A.wtab) {
-    for (int i = tid; i < nw * 34; i += HT) {
-      const double v = A.wtab[(size_t)s * nw * 34 + i];
-      const int w = i / 34, e = i - 34 * w;
+    for (int i = tid; i < nw * WT; i += HT) {
+      const double v = A.wtab[(size_t)s * nw * WT + i];
+      const int w = i / WT, e = i - WT * w;
       if (e < 10) wp[10 * w + e] = v;
-      else wpre[24 * w + e - 10] = v;
+      else if (e < 34) wpre[24 * w + e - 10] = v;
+      else wc[3 * w + e - 34] = v;
     }
   } else {
     for (int i = tid; i < nw; i += HT) {
       const double* wl = A.walls + ((size_t)s * nw + i) * 5;
       rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], wp + 10 * i);
       sat_base_pre(wp + 10 * i, wpre + 24 * i);
+      wc[3 * i] = wl[0];
+      wc[3 * i + 1] = wl[1];
+      wc[3 * i + 2] = wall_far2(P, wl);
     }
   }
   if (tid < NBG) g_free[tid] = 1;
@@ -578,7 +604,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       } else {
         transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
       }
-      const int fr = SPLIT ? pose_free_part(P, q, wp, wpre, part >> 1, part & 1) : pose_free(P, q, wp, wpre, nw);
+      const int fr = SPLIT ? pose_free_part(P, q, wp, wpre, wc, part >> 1, part & 1) : pose_free(P, q, wp, wpre, wc, nw);
       if (!fr) g_free[jn] = 0;  // every writer stores 0
     }
   };
@@ -806,14 +832,17 @@ int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
   return MP_OK;
 }
 
-// Block2Pts + the wall-side SAT tables (pose independent) once per plan: [B][nw][34]
+// Block2Pts + the wall-side SAT tables (pose independent) + centre / far² once per plan: [B][nw][WT]
 __global__ __launch_bounds__(64) void ha_wall_kernel(HaDev P, int B, const double* walls, double* wtab) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= B * P.n_walls) return;
   const double* wl = walls + (size_t)i * 5;
-  double* o = wtab + (size_t)i * 34;
+  double* o = wtab + (size_t)i * WT;
   rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], o);
   sat_base_pre(o, o + 10);
+  o[34] = wl[0];
+  o[35] = wl[1];
+  o[36] = wall_far2(P, wl);
 }
 
 // ------------------------------------------------ device-resident search state
@@ -1642,7 +1671,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.rs_path = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * nB * MAXPATH * 3);
   if (st || !A.h || !A.nb || !A.idx || !A.fr || !A.rs_ok || !A.rs_len || !A.rs_path) return st ? st : MP_ERR_NOMEM;
   if (p->n_walls) {
-    double* wt = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * nB * p->n_walls * 34);
+    double* wt = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * nB * p->n_walls * WT);
     if (!wt) return MP_ERR_NOMEM;
     hipLaunchKernelGGL(ha_wall_kernel, dim3((unsigned)((B * p->n_walls + 63) / 64)), dim3(64), 0, ctx->stream, D, B,
                        A.walls, wt);

@@ -109,3 +109,26 @@ def test_retrieve_path_structure():
     # a sample is the linear interpolation of actualpath at its arc length
     s = out["tol_length"] * 17 / 49
     np.testing.assert_allclose(S[17, 0], np.interp(s, L, P[:, 0]), atol=1e-9)
+
+
+def test_far_wall_skip_bound():
+    """hastar.hip skips a wall's SAT pair when the vehicle centre is farther than √2·(r_vehicle + r_wall)
+    + 1e-6 from the wall centre (r = circumradius): ConvexCollision must then report 'separated' for
+    certain.  Random walls / vehicle poses just beyond the bound (and the driver scenes' walls), checked
+    with the oracle's SeparatingAxisTheorem in both orders."""
+    r = np.random.default_rng(17)
+    L2, W2 = 1.5, 1.0
+    rv = math.hypot(L2, W2)
+    walls = [list(w) for w in ha.PERPENDICULAR["walls"] + ha.PARALLEL["walls"]]
+    walls += [[r.uniform(-5, 10), r.uniform(-2, 10), r.uniform(-math.pi, math.pi), r.uniform(0.2, 4), r.uniform(0.2, 2)]
+              for _ in range(40)]
+    n = 0
+    for w in walls:
+        far = math.sqrt(2) * (rv + math.hypot(w[3], w[4])) + 1e-6
+        for _ in range(150):
+            ang, psi = r.uniform(-math.pi, math.pi), r.uniform(-math.pi, math.pi)
+            d = far * (1 + r.uniform(0, 0.02)) + r.uniform(0, 1e-6)
+            cx, cy = w[0] + d * math.cos(ang), w[1] + d * math.sin(ang)
+            assert oracle.ha_convex_free(_rect(w), _rect([cx, cy, psi, L2, W2])), (w, cx, cy, psi)
+            n += 1
+    assert n == len(walls) * 150
