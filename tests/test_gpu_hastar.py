@@ -139,3 +139,47 @@ def test_retrieve_path_batch_bitexact(ctx):
         s = np.linspace(0, h.r.tol_length, 7)
         assert np.isfinite(h.r.x_interp(s)).all() and np.isfinite(h.r.ψ_interp(s)).all()
     assert found > 10
+
+
+def test_bench_batch_full_size_bitexact(ctx):
+    """configs[3] at full size -- the bench's own 256-scenario batch (scenario_batch(256, seed=4)) -- planned
+    on the device (mp_ha_plan, the tail shape included) vs 256 oracle plans (threaded: the ctypes calls
+    release the GIL): found flags, pop counts, node counts, pop sequences, hybrid_astar_states and
+    RSpath_final, bit for bit; then retrievePath + the tracker for every found path vs the oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from motionplanning_amd import tracker
+
+    hs = ha.scenario_batch(256, seed=4)
+    ha.plan_batch(hs, ctx=ctx)
+    h0 = hs[0]
+    p = ha.params_of(h0)
+    sc, pc = oracle.ha_neighbor_origin(h0.s.expand_time, h0.s.steer_set, h0.s.gear_set)
+
+    def ref(h):
+        return oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+
+    with ThreadPoolExecutor(16) as ex:
+        refs = list(ex.map(ref, hs))
+    assert sum(h.r.loop_count for h in hs) == sum(r["pops"] for r in refs) == 54466
+    for h, r in zip(hs, refs):
+        assert h.r.found == r["found"] and h.r.loop_count == r["pops"] and h.r.n_nodes == r["n_nodes"]
+        assert np.array_equal(h.r.pop_sequence, r["pop_seq"])
+        if r["found"]:
+            assert np.array_equal(h.r.hybrid_astar_states.T, r["states"])
+            assert np.array_equal(h.r.RSpath_final.T, r["rs_path"])
+    ha.retrieve_batch(hs, ctx=ctx)
+    tracker.track_batch(hs, ctx=ctx)
+    tp = tracker.params_of(tracker.settings_for(hs[0]))
+    found = [h for h in hs if h.r.found]
+
+    def track_ref(h):
+        return oracle.track(tp, h.s.starting_real, h.r.tol_length, h.r.interp_values)
+
+    with ThreadPoolExecutor(16) as ex:
+        trs = list(ex.map(track_ref, found))
+    for h, t in zip(found, trs):
+        tr = h.r.tracking
+        assert tr["status"] == tracker.STATUS[t["status"]] and tr["n_steps"] == t["n_steps"]
+        assert np.array_equal(tr["final_state"], t["final"]) and tr["err_accumulated"] == t["err_acc"]
+    assert len(found) == 169
