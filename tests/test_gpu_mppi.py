@@ -207,3 +207,33 @@ def test_jlmath_bitexact(ctx):
             continue
         cpu = np.array([oracle.m(names[fn], a, b) if fn in (4, 18) else oracle.m(names[fn], a) for a, b in zip(x, y)])
         assert np.array_equal(out.view(np.int64), cpu.view(np.int64)), (fn, names[fn], x[out.view(np.int64) != cpu.view(np.int64)][:5])
+
+
+def test_bench_workload_full_size_bitexact(ctx):
+    """The headline bench workload itself (bench.py run(): configs[4] per-GPU shard = 8 scenes x configs[1],
+    K=8192, H=50, occupancy grid, device Philox noise seeded 20260415, step offset 3, final rollout on
+    the side stream) vs 8 oracle MPPIPlan solves with the same Philox stream (threaded): every rollout's
+    cost, feasibility, controls and states bit for bit, MPPICtrl / final trajectory within the stated
+    tolerance."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from motionplanning_amd.abi import MP_NOISE_PHILOX
+
+    S = 8
+    c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415)
+    p = c["params"]
+    p.offset = 3
+    p.final_stream = 1
+    X0 = np.tile(c["X0"], (S, 1))
+    X0[:, 1] = np.linspace(-0.5, 0.5, S)
+    goal = np.tile(c["goal"], (S, 1))
+    grid = np.tile(c["grid"], (S, 1, 1))
+    gpu = mppi_plan_batch(p, X0, goal, np.zeros((S, p.H, 2)), None, grid, None, collect=True, ctx=ctx)
+
+    def ref(s):
+        return oracle.mppi_plan(p, X0[s], goal[s], np.zeros((p.H, 2)), None, c["grid"], None, scene=s, collect=True)
+
+    with ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(ref, range(S)))
+    for s in range(S):
+        _check_plan(gpu, refs[s], s=s)
