@@ -1760,7 +1760,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     max_ns = std::max(max_ns, n_states[b]);
     max_rs = std::max(max_rs, rs_len[b]);
   }
-  for (size_t i = 0; i < nB * mp; i++) pop_seq[i] = -1;
+  // -1 past every scene's pops: the device copy below covers columns [0, max_loop) (its memset
+  // already padded them), the host fills the rest of each row
+  for (size_t b = 0; b < nB; b++) std::fill(pop_seq + b * mp + max_loop, pop_seq + (b + 1) * mp, (int64_t)-1);
   if (max_loop > 0)
     MP_HIP(ctx, hipMemcpy2DAsync(pop_seq, sizeof(int64_t) * mp, Q.pop_seq, sizeof(long long) * mp,
                                  sizeof(long long) * max_loop, nB, hipMemcpyDeviceToHost, ctx->stream));

@@ -182,9 +182,9 @@ def plan_batch(searchers, ctx=None, max_pops=5000):
     found = np.zeros(B, np.int32)
     pops = np.zeros(B, np.int32)
     n_nodes = np.zeros(B, np.int32)
-    pop_seq = np.full((B, max_pops), -1, np.int64)
+    pop_seq = np.empty((B, max_pops), np.int64)  # the library writes every entry (-1 past the pops)
     n_states = np.zeros(B, np.int32)
-    states = np.zeros((B, max_pops, 3))
+    states = np.empty((B, max_pops, 3))  # rows [0, n_states) written; nothing else is read
     rs_len = np.zeros(B, np.int32)
     rs_path = np.zeros((B, 501, 3))
     t0 = time.time()
