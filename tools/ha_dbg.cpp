@@ -1,4 +1,10 @@
-// Standalone Hybrid A* RS_connected driver for kernel debugging (build with -DHA_DEBUG).
+// Standalone Hybrid A* driver for kernel debugging and phase timing (s_memtime stamps of the RS_connected
+// block, the expansion blocks and one mid-search bookkeeping launch).  Build:
+//   bash tools/build_variant.sh dbg "-DHA_DEBUG"
+//   hipcc --offload-arch=gfx950 -O2 -std=c++17 -o tools/ha_dbg tools/ha_dbg.cpp -Lmotionplanning_amd/lib \
+//         -lmpgpu_dbg -Wl,-rpath,'$ORIGIN/../motionplanning_amd/lib'
+// (the stamps themselves wait for outstanding loads, so they perturb what they time: use them for
+// shares, not absolute latencies)
 #include <cmath>
 #include <cstdio>
 #include <cstring>
