@@ -131,3 +131,28 @@ def test_dev_entry_points_match_host(ctx):
     assert np.array_equal(dk.cpu().numpy(), k) and np.array_equal(dK.cpu().numpy(), K)
     assert np.array_equal(dXn.cpu().numpy(), Xn) and np.array_equal(dUn.cpu().numpy(), Un)
     assert np.array_equal(dJn.cpu().numpy(), Jn)
+
+
+def test_solve_configs2_horizon_bitexact(ctx):
+    """mp_ilqr_solve at configs[2]'s horizon (H=100, max_iter 60 as in the bench) on 256 of its instances
+    vs the oracle's sequential loop (threaded): iteration counts, costs, states and controls bit for bit
+    -- the 16-wide quad line search, the all-remaining-trials pass and the max_ls stops included."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    B, N = 256, 100
+    p = ilqr.params(N=N, max_iter=60)
+    x0, U0 = ilqr.cfg3_instances(B, N, seed=3)
+    X0, _ = ilqr.ilqr_rollout(p, x0, U0, ctx=ctx)
+    X, U, J, it, ok = ilqr.ilqr_solve(p, X0, U0, ctx=ctx)
+
+    def ref(b):
+        return oracle.ilqr_solve(p, X0[b], U0[b])
+
+    with ThreadPoolExecutor(16) as ex:
+        refs = list(ex.map(ref, range(B)))
+    stalled = 0
+    for b, (Xo, Uo, Jo, ito, flags) in enumerate(refs):
+        assert it[b] == ito and J[b] == Jo, (b, it[b], ito)
+        assert np.array_equal(X[b], Xo) and np.array_equal(U[b], Uo)
+        stalled += bool(flags & 1)
+    assert stalled > 0  # the rest pass (trials 16..max_ls) was exercised
