@@ -63,6 +63,10 @@ constexpr bool kFwdQuad = true;  // ilqr_forward_quad_kernel: a lane quad per in
 #define ILQR_SEARCH_L 4
 #endif
 constexpr int kSearchL = ILQR_SEARCH_L;  // lanes per line-search trial in mp_ilqr_solve (1 or 4)
+#ifndef ILQR_ONEPASS_MAX
+#define ILQR_ONEPASS_MAX 512
+#endif
+constexpr int kOnePassMax = ILQR_ONEPASS_MAX;  // active instances up to which the search is one pass
 #ifndef ILQR_SEARCH_G
 #define ILQR_SEARCH_G 16
 #endif
@@ -963,14 +967,24 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
 #pragma unroll
     for (int r = 0; r < 4; r++) Xn[r] = x[r];
   double J = 0.0;
+  // knot i's inputs were loaded during knot i-1 (the loads are off the x chain; loading them at the
+  // top of the knot put an L2 round trip on it)
+  double xr[4], Kr[8], kr[2], ur[2];
+#pragma unroll
+  for (int r = 0; r < 4; r++) xr[r] = X[r];
+#pragma unroll
+  for (int r = 0; r < 8; r++) Kr[r] = Kg[r];
+  kr[0] = k[0]; kr[1] = k[1];
+  ur[0] = U[0]; ur[1] = U[1];
   for (int i = 0; i < N - 1; i++) {
-    double xr[4], Kr[8], kr[2], ur[2];
+    const int in = i + 2 < N ? i + 1 : i;  // knot i+1 (clamped)
+    double nxr[4], nK[8], nk[2], nu[2];
 #pragma unroll
-    for (int r = 0; r < 4; r++) xr[r] = X[4 * i + r];
+    for (int r = 0; r < 4; r++) nxr[r] = X[4 * in + r];
 #pragma unroll
-    for (int r = 0; r < 8; r++) Kr[r] = Kg[8 * i + r];
-    kr[0] = k[2 * i]; kr[1] = k[2 * i + 1];
-    ur[0] = U[2 * i]; ur[1] = U[2 * i + 1];
+    for (int r = 0; r < 8; r++) nK[r] = Kg[8 * in + r];
+    nk[0] = k[2 * in]; nk[1] = k[2 * in + 1];
+    nu[0] = U[2 * in]; nu[1] = U[2 * in + 1];
     double dx[4], u[2];
 #pragma unroll
     for (int r = 0; r < 4; r++) dx[r] = x[r] - xr[r];
@@ -1017,6 +1031,12 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
 #pragma unroll
     for (int r = 0; r < 4; r++) x[r] = xn[r];
     if (wr) Xn[4 * (i + 1) + sub] = xn[sub];
+#pragma unroll
+    for (int r = 0; r < 4; r++) xr[r] = nxr[r];
+#pragma unroll
+    for (int r = 0; r < 8; r++) Kr[r] = nK[r];
+    kr[0] = nk[0]; kr[1] = nk[1];
+    ur[0] = nu[0]; ur[1] = nu[1];
   }
   if (wr && sub < 2) Un[2 * (N - 1) + sub] = 0.0;
   return J + terminal(P.variant, x);
@@ -1052,6 +1072,44 @@ __global__ __launch_bounds__(64) void ilqr_forward_kernel(IlqrDev P, int B, cons
   if (live) Jn[b] = J;
 }
 
+// The trial fixpoint m*: the least m in [0, ls_cap] with (U_e + 2^-m k_e) == U_e bit for bit for
+// every control entry e of the instance (ls_cap + 1 if there is none).  A trial's control at knot i
+// is u = (U_i + α k_i) + K_i (x - X_i), and only the first sum depends on α = 2^-m: for m ≥ m*,
+// fl(2^-m k) shrinks towards zero with the sign of k (fl is monotone), so U ≤ U + fl(2^-m k) ≤
+// U + fl(2^-m* k) (or ≥ ≥) and its rounding is sandwiched to U_e (signed zeros: equality at m* needs
+// fl(2^-m* k) = ±0 with the sign that keeps U, and every later term is the same zero).  Every trial
+// m ≥ m* therefore evaluates the same controls from the same x_0, i.e. is bit-identical to trial m*:
+// if trial m* does not decrease J, neither does any later one, and the reference's halving loop runs
+// on to its break at ls_cap (floor or max_ls) and accepts that trial -- trial m*'s outputs.  So the
+// search never evaluates a trial beyond m*; trial m* stops it, reported as ls_cap unless it
+// decreases J.  (Measured at configs[2]: m* = 51..75, against ls_cap = 199 for the
+// OptimalControl variant, whose stalling instances ran all 200 trials.)
+__device__ __forceinline__ bool fixed_at(double u, double kv, int m) {
+  const double v = u + ldexp(1.0, -m) * kv;  // the trial's first sum, same operations
+  return __double_as_longlong(v) == __double_as_longlong(u);
+}
+
+// m* over the instance's 2(N-1) control entries, on the GL lanes of a group (li = lane in group).
+template <int GL>
+__device__ int trial_fixpoint(const IlqrDev& P, const double* U, const double* k, int li) {
+  const int ne = 2 * (P.N - 1), cap = P.ls_cap;
+  int ms = 0;
+  for (int e = li; e < ne; e += GL) {
+    const double u = U[e], kv = k[e];
+    if (fixed_at(u, kv, ms)) continue;  // the entry's own m* is <= the running max
+    int lo = ms + 1, hi = cap + 1;      // least m in (ms, cap] with fixed_at, else cap + 1
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (fixed_at(u, kv, mid)) hi = mid;
+      else lo = mid + 1;
+    }
+    ms = lo;
+  }
+#pragma unroll
+  for (int o = 1; o < GL; o <<= 1) ms = max(ms, __shfl_xor(ms, o));
+  return ms;
+}
+
 // ILQR.jl:70-88 after the backward sweep: line search, accept, convergence test, with the
 // halving trials evaluated G at a time.  Trial m of the reference loop runs at alpha = 2^-m
 // (repeated halving of 1.0 is exact), so the m-th trial is a pure function of m and the G lanes
@@ -1085,7 +1143,7 @@ template <int G, int L = 1>
 __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
                                                          const double* Kg, double* Xs, double* Us, double* Jcur,
                                                          int* active, int* iters, int* flags, int* n_active,
-                                                         int one_round, int* pending) {
+                                                         int one_round, int* pending, int* mstar) {
   constexpr int GL = G * L;     // lanes per instance
   constexpr int IPW = 64 / GL;  // instances per wave
   static_assert(GL <= 64 && 64 % GL == 0, "G*L must divide 64");
@@ -1102,6 +1160,7 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   const double* kb = k + b * (N - 1) * 2;
   const double* Kb = Kg + b * (N - 1) * 8;
   const double J = Jcur[b];
+  const int ms = trial_fixpoint<GL>(P, Ub, kb, lane % GL);  // no trial beyond m* (see trial_fixpoint)
   double Jn = J;
   int mw = -1;  // accepted trial index
   bool searching = live;
@@ -1109,7 +1168,7 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   constexpr unsigned long long lead = L == 1 ? ~0ull : 0x1111111111111111ull;
   for (int r = 0; __any(searching) && !(one_round && r > 0); r++) {
     const int m = r * G + g;
-    const bool mine = searching && m <= P.ls_cap;  // uniform over a trial's lanes
+    const bool mine = searching && m <= P.ls_cap && m <= ms;  // uniform over a trial's lanes
     double jt = 0.0;
     if (mine) {
       if (L == 4) {
@@ -1119,7 +1178,7 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
         jt = forward_trial<false>(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, d);
       }
     }
-    const bool stop = mine && (!(jt >= J) || m == P.ls_cap);
+    const bool stop = mine && (!(jt >= J) || m == P.ls_cap || m == ms);
     const unsigned long long bal = __ballot(stop) & lead;
     const unsigned long long grp = (bal >> (inst * GL)) & (GL == 64 ? ~0ull : ((1ull << GL) - 1));
     const int gw = grp ? __builtin_ctzll(grp) / L : 0;
@@ -1127,6 +1186,7 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
     if (searching && grp) {
       Jn = jw;
       mw = r * G + gw;
+      if (mw == ms && jw >= J) mw = P.ls_cap;  // trials m*..ls_cap are trial m*: the loop breaks at ls_cap
       searching = false;
       // the instance's lanes copy the winning slot together, 8 loads in flight per lane before
       // the stores (instead of the winner alone, one dependent load->store at a time): the
@@ -1157,23 +1217,36 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   if (!live || (lane % GL) != 0) return;
   if (searching) {  // one_round only: trials G..ls_cap follow in ilqr_search_rest_kernel
     pending[b] = 1;
+    mstar[b] = ms;
     return;
   }
   search_accept(P, b, J, Jn, mw, Jcur, active, iters, flags, n_active);
 }
 
-// Trials G..ls_cap of the instances still searching after round 0, all at once: block (b, w)
-// runs trials m = G + (64/L)w + lane/L into slots [b][m-G] (Xs2/Us2/Jt), one lane (L = 1) or a
-// lane quad (L = 4) per trial, and the first stopping trial is the least m whose loop test would
-// end the reference's halving loop (atomicMin).
+// Trials first..min(m*, ls_cap) of the pending instances, all at once: block (b, w) runs trials
+// m = first + (64/L)w + lane/L into slots [b][m-first] (Xs2/Us2/Jt, T2 per instance), one lane
+// (L = 1) or a lane quad (L = 4) per trial, and the first stopping trial is the least m whose loop
+// test would end the reference's halving loop (atomicMin).  first = G after the G-wide round 0
+// (m* from it in mstar[]); first = 0 is the one-pass search of every active instance (pending =
+// active), each block computing m* itself and block w = 0 publishing it.
 template <int G, int L = 1>
 __global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                               const double* k, const double* Kg, const double* Jcur,
-                                                              const int* pending, double* Xs2, double* Us2,
-                                                              double* Jt, int* winm) {
-  const int b = blockIdx.x, sub = (int)threadIdx.x % L, m = G + (64 / L) * (int)blockIdx.y + (int)threadIdx.x / L;
-  if (!pending[b] || m > P.ls_cap) return;  // uniform over a trial's lanes
-  const size_t N = P.N, T2 = (size_t)(P.ls_cap + 1 - G), t = (size_t)(m - G);
+                                                              const int* pending, int* mstar, double* Xs2,
+                                                              double* Us2, double* Jt, int* winm, int first,
+                                                              size_t T2) {
+  const int b = blockIdx.x, sub = (int)threadIdx.x % L, m = first + (64 / L) * (int)blockIdx.y + (int)threadIdx.x / L;
+  if (!pending[b]) return;
+  const size_t N = P.N, t = (size_t)(m - first);
+  int ms;
+  if (first == 0) {
+    if (m - (int)threadIdx.x / L > P.ls_cap) return;  // the block's first trial (uniform)
+    ms = trial_fixpoint<64>(P, U + b * N * 2, k + b * (N - 1) * 2, threadIdx.x);
+    if (blockIdx.y == 0 && threadIdx.x == 0) mstar[b] = ms;
+  } else {
+    ms = mstar[b];
+  }
+  if (m > P.ls_cap || m > ms) return;  // uniform over a trial's lanes
   double jt;
   if (L == 4) {
     jt = forward_trial_quad(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
@@ -1187,26 +1260,29 @@ __global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, 
   }
   if (sub != 0) return;
   Jt[(size_t)b * T2 + t] = jt;
-  if (!(jt >= Jcur[b]) || m == P.ls_cap) atomicMin(winm + b, m);
+  if (!(jt >= Jcur[b]) || m == P.ls_cap || m == ms) atomicMin(winm + b, m);
 }
 
 // Accept the winning trial of each pending instance: 64 lanes copy its slot into X/U.
 template <int G>
 __global__ __launch_bounds__(64) void ilqr_search_finish_kernel(IlqrDev P, int B, double* X, double* U,
-                                                                const int* pending, const double* Xs2,
-                                                                const double* Us2, const double* Jt, const int* winm,
-                                                                double* Jcur, int* active, int* iters, int* flags,
-                                                                int* n_active) {
+                                                                const int* pending, const int* mstar,
+                                                                const double* Xs2, const double* Us2, const double* Jt,
+                                                                const int* winm, double* Jcur, int* active, int* iters,
+                                                                int* flags, int* n_active, int first, size_t T2) {
   const size_t b = blockIdx.x;
   if (!pending[b]) return;
-  const size_t N = P.N, T2 = (size_t)(P.ls_cap + 1 - G);
+  const size_t N = P.N;
   const int mw = winm[b];
-  const size_t t = (size_t)(mw - G);
+  const size_t t = (size_t)(mw - first);
   const double* Xw = Xs2 + ((size_t)b * T2 + t) * N * 4;
   const double* Uw = Us2 + ((size_t)b * T2 + t) * N * 2;
   for (size_t i = threadIdx.x; i < N * 4; i += 64) X[b * N * 4 + i] = Xw[i];
   for (size_t i = threadIdx.x; i < N * 2; i += 64) U[b * N * 2 + i] = Uw[i];
-  if (threadIdx.x == 0) search_accept(P, b, Jcur[b], Jt[(size_t)b * T2 + t], mw, Jcur, active, iters, flags, n_active);
+  if (threadIdx.x == 0) {
+    const double J = Jcur[b], Jn = Jt[(size_t)b * T2 + t];
+    search_accept(P, b, J, Jn, mw == mstar[b] && Jn >= J ? P.ls_cap : mw, Jcur, active, iters, flags, n_active);
+  }
 }
 
 // Initial guess roll out (ILQR.jl:31-37) with TotalCost accumulated in order.
@@ -1452,17 +1528,18 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   // while their slots fit in 8 GiB, in half of the free device memory and in the context's
   // workspace cap.  Otherwise -- or when allocating them fails -- the G-wide kernel runs its
   // rounds to the end: the same accepted trials (tests/test_gpu_ilqr.py), more latency.
-  const size_t T2 = G == kSearchG && D.ls_cap + 1 > G ? (size_t)(D.ls_cap + 1 - G) : 0;
+  // Slots for trials 0..ls_cap, so that the same buffers serve the one-pass search (below).
+  const size_t T2 = G == kSearchG && D.ls_cap + 1 > G ? (size_t)(D.ls_cap + 1) : 0;
   bool rest = T2 > 0 && T2 * B * N * 48 <= ((size_t)8 << 30) &&
               mp_ws_affordable(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2, 0.5) &&
               mp_ws_affordable(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2, 0.25);
   double *dXs2 = nullptr, *dUs2 = nullptr, *dJt = nullptr;
-  int* dpw = nullptr;  // pending[B], winm[B]
+  int* dpw = nullptr;  // pending[B], winm[B], mstar[B]
   if (rest) {
     dXs2 = (double*)mp_ws(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2);
     dUs2 = dXs2 ? (double*)mp_ws(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2) : nullptr;
     dJt = dUs2 ? (double*)mp_ws(ctx, WS_IO12, sizeof(double) * B * T2) : nullptr;
-    dpw = dJt ? (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 2 * (size_t)B) : nullptr;
+    dpw = dJt ? (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 3 * (size_t)B) : nullptr;
     if (!dXs2 || !dUs2 || !dJt || !dpw) {
       rest = false;      // fall back to the multi-round 16-wide search
       ctx->err.clear();  // (the failed allocation left a message; mp_ws already cleared the HIP error)
@@ -1473,10 +1550,29 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   MP_HIP(ctx, hipGetLastError());
   int* hn = (int*)mp_pinned(ctx, sizeof(int));
   if (!hn) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
+  // One-pass search: once at most kOnePassMax instances are active (the host's last poll), every
+  // active instance's trials 0..min(m*, ls_cap) run in one launch (m* = 51..75 measured, so ~4
+  // waves per instance) -- the round-0 latency chain and the rest chain become one.
+  int n_act = B;
   for (int outer = 0; outer <= D.max_iter + 1; outer++) {
     if ((st = run_backward(ctx, D, B, dX, dU, dact, dk, dK))) return st;
     MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
     mp_time_begin(ctx);
+    if (rest && n_act <= kOnePassMax) {
+      MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));  // winm = 0x7f7f7f7f
+      hipLaunchKernelGGL((ilqr_search_rest_kernel<kSearchG, kSearchL>),
+                         dim3((unsigned)B, (unsigned)((T2 + 64 / kSearchL - 1) / (64 / kSearchL))), b1, 0, ctx->stream, D,
+                         B, dX, dU, dk, dK, dJ, dact, dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, 0, T2);
+      MP_HIP(ctx, hipGetLastError());
+      hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dact,
+                         dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, 0, T2);
+      MP_HIP(ctx, hipGetLastError());
+      mp_time_end(ctx);
+      MP_HIP(ctx, hipMemcpyAsync(hn, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+      MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      if ((n_act = *hn) == 0) break;
+      continue;
+    }
     // G = 16: a lane quad per trial (4 waves per SIMD at B = 4096); the narrower fallbacks one lane
     const int ipw = G == kSearchG ? 64 / (kSearchG * kSearchL) : 64 / G;
     const dim3 gs((unsigned)((B + ipw - 1) / ipw));
@@ -1486,26 +1582,27 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     }
     if (G == kSearchG)
       hipLaunchKernelGGL((ilqr_search_kernel<kSearchG, kSearchL>), gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact,
-                         dit, dfl, dn, rest ? 1 : 0, dpw);
+                         dit, dfl, dn, rest ? 1 : 0, dpw, dpw ? dpw + 2 * B : nullptr);
     else if (G == 4)
       hipLaunchKernelGGL(ilqr_search_kernel<4>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn,
-                         0, dpw);
+                         0, dpw, nullptr);
     else
       hipLaunchKernelGGL(ilqr_search_kernel<1>, gs, b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn,
-                         0, dpw);
+                         0, dpw, nullptr);
     MP_HIP(ctx, hipGetLastError());
     if (rest) {
       hipLaunchKernelGGL((ilqr_search_rest_kernel<kSearchG, kSearchL>), dim3((unsigned)B, (unsigned)((T2 + 64 / kSearchL - 1) /
-                         (64 / kSearchL))), b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dJ, dpw, dXs2, dUs2, dJt, dpw + B);
+                         (64 / kSearchL))), b1, 0, ctx->stream, D, B, dX, dU, dk, dK, dJ, dpw, dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, kSearchG,
+                         T2);
       MP_HIP(ctx, hipGetLastError());
-      hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dpw, dXs2,
-                         dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn);
+      hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dpw, dpw + 2 * B,
+                         dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, kSearchG, T2);
       MP_HIP(ctx, hipGetLastError());
     }
     mp_time_end(ctx);
     MP_HIP(ctx, hipMemcpyAsync(hn, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (*hn == 0) break;
+    if ((n_act = *hn) == 0) break;
   }
   std::vector<int> hfl(B);
   if ((st = mp_download(ctx, X, (const double*)dX, 4 * N * B))) return st;

@@ -134,12 +134,13 @@ def test_dev_entry_points_match_host(ctx):
 
 
 def test_solve_configs2_horizon_bitexact(ctx):
-    """mp_ilqr_solve at configs[2]'s horizon (H=100, max_iter 60 as in the bench) on 256 of its instances
+    """mp_ilqr_solve at configs[2]'s horizon (H=100, max_iter 60 as in the bench) on 640 of its instances
     vs the oracle's sequential loop (threaded): iteration counts, costs, states and controls bit for bit
-    -- the 16-wide quad line search, the all-remaining-trials pass and the max_ls stops included."""
+    -- the 16-wide quad round 0 + remaining-trials pass while more than 512 instances are active, the
+    one-pass search after, the trial-fixpoint cutoff and the max_ls stops included."""
     from concurrent.futures import ThreadPoolExecutor
 
-    B, N = 256, 100
+    B, N = 640, 100
     p = ilqr.params(N=N, max_iter=60)
     x0, U0 = ilqr.cfg3_instances(B, N, seed=3)
     X0, _ = ilqr.ilqr_rollout(p, x0, U0, ctx=ctx)

@@ -14,6 +14,7 @@ from motionplanning_amd.abi import ptr
 from motionplanning_amd.context import default_context
 
 B, N, reps = 4096, 100, 20
+solve_only = "--solve-only" in sys.argv
 ctx = default_context(0)
 ctx.lib.mp_ctx_kernel_timing(ctx.handle, 1)
 dev = torch.device("cuda", 0)
@@ -30,7 +31,7 @@ with torch.cuda.stream(stream):
     dal = torch.ones(B, dtype=torch.float64, device=dev)
     ctx.synchronize()
     ms, cnt = ctypes.c_double(), ctypes.c_int32()
-    for name, fn in (
+    for name, fn in () if solve_only else (
         ("backward", lambda: ctx.lib.mp_ilqr_backward_dev(ctx.handle, ctypes.byref(p), B, ptr(dX), ptr(dU), ptr(dk),
                                                           ptr(dK))),
         ("forward", lambda: ctx.lib.mp_ilqr_forward_dev(ctx.handle, ctypes.byref(p), B, ptr(dX), ptr(dU), ptr(dk),
@@ -46,6 +47,20 @@ with torch.cuda.stream(stream):
         el = (time.perf_counter() - t0) / reps
         ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
         print(f"{name}: {el * 1e3:.3f} ms wall, {ms.value / reps:.3f} ms kernel", flush=True)
+    if "--alpha-mix" in sys.argv:  # forward trial cost vs the spread of alpha inside a wave (16 instances)
+        for label, a in (("alpha 1", torch.ones(B, dtype=torch.float64)),
+                         ("alpha 2^-(b%16)", torch.ldexp(torch.ones(B, dtype=torch.float64), -(torch.arange(B) % 16))),
+                         ("alpha 2^-(b/256)", torch.ldexp(torch.ones(B, dtype=torch.float64), -(torch.arange(B) // 256))),
+                         ("alpha 2^-20", torch.full((B,), 2.0 ** -20, dtype=torch.float64))):
+            dal.copy_(a)
+            ctx.synchronize()
+            ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+            for _ in range(reps):
+                ctx.check(ctx.lib.mp_ilqr_forward_dev(ctx.handle, ctypes.byref(p), B, ptr(dX), ptr(dU), ptr(dk), ptr(dK),
+                                                      ptr(dal), ptr(dXn), ptr(dUn), ptr(dJn)))
+            ctx.synchronize()
+            ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+            print(f"forward {label}: {ms.value / reps:.3f} ms kernel", flush=True)
 t0 = time.perf_counter()
 Xs, Us, Js, it, ok = ilqr.ilqr_solve(ilqr.params(N=N, max_iter=60), X, U, ctx=ctx)
 print(f"solve: {(time.perf_counter() - t0) * 1e3:.1f} ms, iterations max {it.max()} mean {it.mean():.1f}, ok {ok}")
