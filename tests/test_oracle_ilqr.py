@@ -135,3 +135,52 @@ def test_parking_variant_runs():
     assert np.isfinite(J) and np.isfinite(X).all()
     assert flags in (0, 2)  # the script oscillates; max_iter may end it
     del J0
+
+
+def _fixpoint(U, k, cap):
+    """ilqr.hip trial_fixpoint restated: least m in [0, cap] with U + 2^-m k == U bit for bit for every
+    control entry (cap + 1 if none)."""
+    u, kk = U[:-1].reshape(-1), k.reshape(-1)
+    for m in range(cap + 1):
+        if np.array_equal((u + np.ldexp(1.0, -m) * kk).view(np.int64), u.view(np.int64)):
+            return m
+    return cap + 1
+
+
+def test_trial_fixpoint_trials_are_identical():
+    """The line-search cutoff of ilqr.hip (trial_fixpoint): every trial m >= m* is bit-identical to trial m*
+    (controls, states and cost), so the device never evaluates one beyond m*.  Checked on the oracle's
+    forward trial along real solves of configs[2] instances, OptimalControl (stalling instances reach
+    max_ls there) and Parking; plus the sandwich on random entries, signed zeros and subnormals included."""
+    cases = 0
+    for variant, N in ((ilqr.MP_ILQR_OPTIMALCONTROL, 100), (ilqr.MP_ILQR_PARKING, 30)):
+        p = ilqr.params(N=N, variant=variant, max_iter=60)
+        x0, U0 = ilqr.cfg3_instances(12, N, seed=5)
+        for b in range(12):
+            X, J = oracle.ilqr_rollout(p, x0[b], U0[b])
+            U = U0[b].copy()
+            for _ in range(6):
+                k, K = oracle.ilqr_backward(p, X, U)
+                ms = _fixpoint(U, k, 199)
+                assert 0 < ms < 200
+                ref = oracle.ilqr_forward(p, X, U, k, K, np.ldexp(1.0, -ms))
+                for m in (ms + 1, ms + 7, 199):
+                    got = oracle.ilqr_forward(p, X, U, k, K, np.ldexp(1.0, -m))
+                    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]) and got[2] == ref[2]
+                cases += 1
+                a, Jn = 1.0, J
+                while True:  # the reference's halving loop, to move on to the next iterate
+                    Xn, Un, Jn = oracle.ilqr_forward(p, X, U, k, K, a)
+                    a /= 2
+                    if Jn < J or a < 2.0 ** -199:
+                        break
+                X, U, J = Xn, Un, Jn
+    assert cases == 144
+    # the monotone sandwich on raw entries: fixed at m* => fixed at every m > m* (bits)
+    r = np.random.default_rng(2)
+    u = np.concatenate([r.standard_normal(4000) * 10.0 ** r.integers(-300, 300, 4000), [0.0, -0.0, 5e-324, -5e-324]])
+    kk = np.concatenate([r.standard_normal(4000) * 10.0 ** r.integers(-300, 300, 4000), [-0.0, 0.0, 1.0, 0.0]])
+    for m0 in range(0, 1100, 7):
+        t0 = (u + np.ldexp(1.0, -m0) * kk).view(np.int64) == u.view(np.int64)
+        for m in (m0 + 1, m0 + 13, m0 + 200):
+            assert not np.any(t0 & ((u + np.ldexp(1.0, -m) * kk).view(np.int64) != u.view(np.int64)))
