@@ -340,18 +340,20 @@ __device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, c
 
 // Derivative records D[j][q][b] (component-major, instance fastest): thread t = j*B + b, so
 // both the stores here and the backward sweep's per-knot loads are coalesced.
+// list (mp_ilqr_solve): the n active instances in compact order; record i (of instance list[i])
+// then sits in column i.  Without a list, all B instances, column b.
 __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const double* X, const double* U,
-                                                         const int* active, double* D) {
-  const long long Bn = (long long)B * (P.N - 1);
+                                                         const int* list, int n, double* D) {
+  const long long Bn = (long long)n * (P.N - 1);
   long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= Bn) t = Bn - 1;  // tail lanes recompute the last knot (identical values): all lanes stay active
-  const int j = (int)(t / B), b = (int)(t % B);
-  if (active && __all(!active[b])) return;  // wave-uniform skip; stale records of inactive instances are unused
+  const int j = (int)(t / n), i = (int)(t % n);
+  const int b = list ? list[i] : i;
   const double* xs = X + ((size_t)b * P.N + j) * 4;
   const double* us = U + ((size_t)b * P.N + j) * 2;
   const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
   const double u[2] = {us[0], us[1]};
-  double* out = D + (size_t)j * ND * B + b;
+  double* out = D + (size_t)j * ND * B + i;
   int bad = 0;
   knot_derivs<kFastDeriv>(P, s, u, out, (size_t)B, bad);
   if (kFastDeriv && kRedo && __any(bad)) {  // some lane left a straight-line core's range: redo the wave exactly
@@ -810,7 +812,7 @@ __device__ __forceinline__ void backward_sweep_pair(const IlqrDev& P, int B, int
 // wave reads them from LDS and the loader wave keeps the next knot's loads in flight.
 template <int LANES>
 __global__ __launch_bounds__(64 * (LANES + 1)) void ilqr_backward_staged_kernel(IlqrDev P, int B, const double* X,
-                                                                               const double* D, const int* active,
+                                                                               const double* D, const int* list, int n,
                                                                                double* kout, double* Kout) {
   extern __shared__ double recs[];  // [2][ND][64]
   __shared__ int sh_redo;
@@ -818,15 +820,15 @@ __global__ __launch_bounds__(64 * (LANES + 1)) void ilqr_backward_staged_kernel(
   const bool loader = tid >= 64 * LANES;  // the last wave
   const int il = loader ? tid - 64 * LANES : tid / LANES;  // instance within the block's 64
   const int side = LANES == 2 ? (tid & 1) : 0;
-  const int b0 = blockIdx.x * 64 + il;
-  const bool live = b0 < B && (!active || active[b0]);
-  if (!__syncthreads_or(live)) return;  // block-uniform
-  const int b = b0 < B ? b0 : B - 1;
+  const int i0 = blockIdx.x * 64 + il;  // record column (compact index with a list)
+  const bool live = i0 < n;              // every block has a live instance (grid = ceil(n / 64))
+  const int i = live ? i0 : n - 1;       // dead lanes recompute the last one and store nothing
+  const int b = list ? list[i] : i;
   if (tid == 0) sh_redo = 0;  // read only after the sweep's barriers
   if (loader) {
-    record_loader(P, B, b, D, recs, il);
+    record_loader(P, B, i, D, recs, il);
     lds_barrier();  // the compute waves' redo decision
-    if (kFastBwd && kRedo && sh_redo) record_loader(P, B, b, D, recs, il);
+    if (kFastBwd && kRedo && sh_redo) record_loader(P, B, i, D, recs, il);
     return;
   }
   int bad = 0;
@@ -1132,7 +1134,7 @@ __device__ __forceinline__ void search_accept(const IlqrDev& P, size_t b, double
     go = false;
   }
   active[b] = go;
-  if (go) atomicAdd(n_active, 1);
+  if (go) n_active[1 + atomicAdd(n_active, 1)] = (int)b;  // n_active[1..]: the next iteration's compact list
 }
 
 // one_round: stop after round 0 and mark the instances still searching in pending[] (their
@@ -1326,7 +1328,7 @@ __global__ __launch_bounds__(64) void ilqr_rollout_kernel(IlqrDev P, int B, cons
 }
 
 __global__ void ilqr_init_kernel(IlqrDev P, int B, const double* X, const double* U, double* Jcur, int* active,
-                                 int* iters, int* flags) {
+                                 int* iters, int* flags, int* list) {
   const int b0 = blockIdx.x * blockDim.x + threadIdx.x;
   const int b = b0 < B ? b0 : B - 1;  // all lanes active (ballot-based libm)
   const double J = total_cost(P.variant, P.N, X + (size_t)b * P.N * 4, U + (size_t)b * P.N * 2);
@@ -1335,6 +1337,7 @@ __global__ void ilqr_init_kernel(IlqrDev P, int B, const double* X, const double
   active[b] = 1;
   iters[b] = 1;
   flags[b] = 0;
+  list[b] = b;
 }
 
 int make_ilqr(mp_ctx* ctx, const mp_ilqr_params* p, int B, IlqrDev* D) {
@@ -1360,23 +1363,28 @@ int make_ilqr(mp_ctx* ctx, const mp_ilqr_params* p, int B, IlqrDev* D) {
   return MP_OK;
 }
 
-int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const double* dU, const int* active,
+// list/na: the compact list of the na active instances (mp_ilqr_solve), or nullptr/B for all.
+int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const double* dU, const int* list, int na,
                  double* dk, double* dK) {
-  const size_t n = (size_t)B * (D.N - 1);
-  double* dD = (double*)mp_ws(ctx, WS_ILQR0, sizeof(double) * n * ND);
+#if defined(MP_ILQR_UNSTAGED) || defined(MP_ILQR_PAIR)
+  list = nullptr;  // A/B builds: the unstaged sweeps index records by instance; all B run
+  na = B;
+#endif
+  const size_t n = (size_t)na * (D.N - 1);
+  double* dD = (double*)mp_ws(ctx, WS_ILQR0, sizeof(double) * (size_t)B * (D.N - 1) * ND);  // knot stride ND*B
   if (!dD) return MP_ERR_NOMEM;
   mp_time_begin(ctx);  // the timed region covers both kernels of the backward pass
   hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
-                     active, dD);
+                     list, na, dD);
   MP_HIP(ctx, hipGetLastError());
 #if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR)
-  hipLaunchKernelGGL(ilqr_backward_staged_kernel<kBwdStagedLanes>, dim3((B + 63) / 64),
+  hipLaunchKernelGGL(ilqr_backward_staged_kernel<kBwdStagedLanes>, dim3((na + 63) / 64),
                      dim3(64 * (kBwdStagedLanes + 1)), sizeof(double) * 2 * ND * 64, ctx->stream, D, B, dX, dD,
-                     active, dk, dK);
+                     list, na, dk, dK);
 #else
   const int ipb = 64 / kBwdLanes;  // instances per 64-thread block
-  hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + ipb - 1) / ipb), dim3(64), 0, ctx->stream, D, B, dX, dD, active, dk,
-                     dK);
+  hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + ipb - 1) / ipb), dim3(64), 0, ctx->stream, D, B, dX, dD, nullptr,
+                     dk, dK);
 #endif
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
@@ -1423,7 +1431,7 @@ int mp_ilqr_backward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const doub
   double* dk = mp_alloc_out(ctx, WS_IO2, k, 2 * (N - 1) * B, &st);
   double* dK = mp_alloc_out(ctx, WS_IO3, Kg, 8 * (N - 1) * B, &st);
   if (st) return st;
-  if ((st = run_backward(ctx, D, B, dX, dU, nullptr, dk, dK))) return st;
+  if ((st = run_backward(ctx, D, B, dX, dU, nullptr, B, dk, dK))) return st;
   if ((st = mp_download(ctx, k, (const double*)dk, 2 * (N - 1) * B))) return st;
   if ((st = mp_download(ctx, Kg, (const double*)dK, 8 * (N - 1) * B))) return st;
   MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -1472,7 +1480,7 @@ int mp_ilqr_backward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const 
   int st = make_ilqr(ctx, p, B, &D);
   if (st) return st;
   MP_CHECK(ctx, X && U && k && Kg, "required pointer is NULL");
-  return run_backward(ctx, D, B, X, U, nullptr, k, Kg);
+  return run_backward(ctx, D, B, X, U, nullptr, B, k, Kg);
 }
 
 int mp_ilqr_forward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X, const double* U,
@@ -1518,12 +1526,12 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   double* dXn = (double*)mp_ws(ctx, WS_IO4, sizeof(double) * 4 * N * B * G);
   double* dUn = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 2 * N * B * G);
   double* dJ = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * B);
-  int* dint = (int*)mp_ws(ctx, WS_IO7, sizeof(int) * (3 * (size_t)B + 1));
+  int* dint = (int*)mp_ws(ctx, WS_IO7, sizeof(int) * (4 * (size_t)B + 1));
   if (st || !dk || !dK || !dXn || !dUn || !dJ || !dint) return st ? st : MP_ERR_NOMEM;
   int* dact = dint;
   int* dit = dint + B;
   int* dfl = dint + 2 * B;
-  int* dn = dint + 3 * B;
+  int* dn = dint + 3 * B;    // [0] active count, [1..B] their compact list (search_accept)
   // trials G..ls_cap in one pass for the instances still searching after round 0 (G = kSearchG only),
   // while their slots fit in 8 GiB, in half of the free device memory and in the context's
   // workspace cap.  Otherwise -- or when allocating them fails -- the G-wide kernel runs its
@@ -1546,7 +1554,7 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     }
   }
   const dim3 g1((B + 63) / 64), b1(64);
-  hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl);
+  hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl, dn + 1);
   MP_HIP(ctx, hipGetLastError());
   int* hn = (int*)mp_pinned(ctx, sizeof(int));
   if (!hn) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
@@ -1555,7 +1563,8 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   // waves per instance) -- the round-0 latency chain and the rest chain become one.
   int n_act = B;
   for (int outer = 0; outer <= D.max_iter + 1; outer++) {
-    if ((st = run_backward(ctx, D, B, dX, dU, dact, dk, dK))) return st;
+    // the derivative and sweep launches cover the n_act active instances only (compact list)
+    if ((st = run_backward(ctx, D, B, dX, dU, dn + 1, n_act, dk, dK))) return st;
     MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
     mp_time_begin(ctx);
     if (rest && n_act <= kOnePassMax) {
