@@ -1,7 +1,7 @@
 /*
  * ORACLE — test infrastructure only.  CPU restatement of the iLQR sibling:
  * OptimalControl/ILQR/{Dynamics,Cost,GetMatrix,ILQR}.jl and the cost/line-search
- * variant PathPlanning/Parking_ILQR/*.  Scalar C, fp64, reference evaluation order.
+ * variant PathPlanning/Parking_ILQR (all files).  Scalar C, fp64, reference evaluation order.
  *
  * Parity status: there is no reference-produced artifact for this path
  * ("parity unpinned" against Julia).  Anchors: the script's own
