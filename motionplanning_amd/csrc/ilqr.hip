@@ -341,10 +341,13 @@ __device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, c
 // Derivative records D[j][q][b] (component-major, instance fastest): thread t = j*B + b, so
 // both the stores here and the backward sweep's per-knot loads are coalesced.
 // list (mp_ilqr_solve): the n active instances in compact order; record i (of instance list[i])
-// then sits in column i.  Without a list, all B instances, column b.
+// then sits in column i.  Without a list, all B instances, column b.  n_dev: n read on the device
+// (the grid is sized for nmax >= n by a host that has not waited for the count), else n = nmax.
 __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const double* X, const double* U,
-                                                         const int* list, int n, double* D) {
+                                                         const int* list, const int* n_dev, int nmax, double* D) {
+  const int n = n_dev ? *n_dev : nmax;
   const long long Bn = (long long)n * (P.N - 1);
+  if ((long long)blockIdx.x * blockDim.x >= Bn) return;  // block-uniform: past the live records
   long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= Bn) t = Bn - 1;  // tail lanes recompute the last knot (identical values): all lanes stay active
   const int j = (int)(t / n), i = (int)(t % n);
@@ -812,16 +815,19 @@ __device__ __forceinline__ void backward_sweep_pair(const IlqrDev& P, int B, int
 // wave reads them from LDS and the loader wave keeps the next knot's loads in flight.
 template <int LANES>
 __global__ __launch_bounds__(64 * (LANES + 1)) void ilqr_backward_staged_kernel(IlqrDev P, int B, const double* X,
-                                                                               const double* D, const int* list, int n,
-                                                                               double* kout, double* Kout) {
+                                                                               const double* D, const int* list,
+                                                                               const int* n_dev, int nmax, double* kout,
+                                                                               double* Kout) {
   extern __shared__ double recs[];  // [2][ND][64]
   __shared__ int sh_redo;
   const int tid = threadIdx.x;
   const bool loader = tid >= 64 * LANES;  // the last wave
   const int il = loader ? tid - 64 * LANES : tid / LANES;  // instance within the block's 64
   const int side = LANES == 2 ? (tid & 1) : 0;
+  const int n = n_dev ? *n_dev : nmax;
+  if ((int)blockIdx.x * 64 >= n) return;  // block-uniform: the grid covers nmax >= n
   const int i0 = blockIdx.x * 64 + il;  // record column (compact index with a list)
-  const bool live = i0 < n;              // every block has a live instance (grid = ceil(n / 64))
+  const bool live = i0 < n;
   const int i = live ? i0 : n - 1;       // dead lanes recompute the last one and store nothing
   const int b = list ? list[i] : i;
   if (tid == 0) sh_redo = 0;  // read only after the sweep's barriers
@@ -1338,6 +1344,7 @@ __global__ void ilqr_init_kernel(IlqrDev P, int B, const double* X, const double
   iters[b] = 1;
   flags[b] = 0;
   list[b] = b;
+  if (b0 == 0) list[-1] = B;  // the count before the list
 }
 
 int make_ilqr(mp_ctx* ctx, const mp_ilqr_params* p, int B, IlqrDev* D) {
@@ -1363,11 +1370,13 @@ int make_ilqr(mp_ctx* ctx, const mp_ilqr_params* p, int B, IlqrDev* D) {
   return MP_OK;
 }
 
-// list/na: the compact list of the na active instances (mp_ilqr_solve), or nullptr/B for all.
-int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const double* dU, const int* list, int na,
-                 double* dk, double* dK) {
+// list/n_dev/na: the compact list of the *n_dev <= na active instances (mp_ilqr_solve; grids sized
+// for na), or nullptr/nullptr/B for all.
+int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const double* dU, const int* list,
+                 const int* n_dev, int na, double* dk, double* dK) {
 #if defined(MP_ILQR_UNSTAGED) || defined(MP_ILQR_PAIR)
   list = nullptr;  // A/B builds: the unstaged sweeps index records by instance; all B run
+  n_dev = nullptr;
   na = B;
 #endif
   const size_t n = (size_t)na * (D.N - 1);
@@ -1375,12 +1384,12 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
   if (!dD) return MP_ERR_NOMEM;
   mp_time_begin(ctx);  // the timed region covers both kernels of the backward pass
   hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
-                     list, na, dD);
+                     list, n_dev, na, dD);
   MP_HIP(ctx, hipGetLastError());
 #if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR)
   hipLaunchKernelGGL(ilqr_backward_staged_kernel<kBwdStagedLanes>, dim3((na + 63) / 64),
                      dim3(64 * (kBwdStagedLanes + 1)), sizeof(double) * 2 * ND * 64, ctx->stream, D, B, dX, dD,
-                     list, na, dk, dK);
+                     list, n_dev, na, dk, dK);
 #else
   const int ipb = 64 / kBwdLanes;  // instances per 64-thread block
   hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + ipb - 1) / ipb), dim3(64), 0, ctx->stream, D, B, dX, dD, nullptr,
@@ -1431,7 +1440,7 @@ int mp_ilqr_backward(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const doub
   double* dk = mp_alloc_out(ctx, WS_IO2, k, 2 * (N - 1) * B, &st);
   double* dK = mp_alloc_out(ctx, WS_IO3, Kg, 8 * (N - 1) * B, &st);
   if (st) return st;
-  if ((st = run_backward(ctx, D, B, dX, dU, nullptr, B, dk, dK))) return st;
+  if ((st = run_backward(ctx, D, B, dX, dU, nullptr, nullptr, B, dk, dK))) return st;
   if ((st = mp_download(ctx, k, (const double*)dk, 2 * (N - 1) * B))) return st;
   if ((st = mp_download(ctx, Kg, (const double*)dK, 8 * (N - 1) * B))) return st;
   MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -1480,7 +1489,7 @@ int mp_ilqr_backward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const 
   int st = make_ilqr(ctx, p, B, &D);
   if (st) return st;
   MP_CHECK(ctx, X && U && k && Kg, "required pointer is NULL");
-  return run_backward(ctx, D, B, X, U, nullptr, B, k, Kg);
+  return run_backward(ctx, D, B, X, U, nullptr, nullptr, B, k, Kg);
 }
 
 int mp_ilqr_forward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const double* X, const double* U,
@@ -1556,15 +1565,36 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   const dim3 g1((B + 63) / 64), b1(64);
   hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl, dn + 1);
   MP_HIP(ctx, hipGetLastError());
-  int* hn = (int*)mp_pinned(ctx, sizeof(int));
+  int* hn = (int*)mp_pinned(ctx, 2 * sizeof(int));
   if (!hn) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
   // One-pass search: once at most kOnePassMax instances are active (the host's last poll), every
   // active instance's trials 0..min(m*, ls_cap) run in one launch (m* = 51..75 measured, so ~4
   // waves per instance) -- the round-0 latency chain and the rest chain become one.
-  int n_act = B;
+  // The host runs one iteration ahead: after enqueueing iteration t it waits for the active count
+  // after t-1 (copied into hn[(t-1)&1], event-ordered), which bounds iteration t+1's count, so the
+  // GPU never idles between iterations while the host polls.  Launch grids are sized by that bound;
+  // the derivative and sweep kernels read the exact count (dn[0]) on the device, the search kernels
+  // skip inactive instances; once the count reads 0 the iteration just enqueued was a no-op.
+  struct EvPair {
+    hipEvent_t e[2] = {nullptr, nullptr};
+    ~EvPair() { for (hipEvent_t x : e) if (x) (void)hipEventDestroy(x); }
+  } evp;
+  for (int q = 0; q < 2; q++) MP_HIP(ctx, hipEventCreateWithFlags(&evp.e[q], hipEventDisableTiming));
+  int n_act = B;  // upper bound on the active count of the iteration being enqueued
+  auto poll = [&](int outer, bool* stop) -> int {
+    MP_HIP(ctx, hipMemcpyAsync(hn + (outer & 1), dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    MP_HIP(ctx, hipEventRecord(evp.e[outer & 1], ctx->stream));
+    *stop = false;
+    if (outer == 0) return MP_OK;
+    MP_HIP(ctx, hipEventSynchronize(evp.e[(outer - 1) & 1]));
+    const int nprev = hn[(outer - 1) & 1];
+    if (nprev == 0) *stop = true;
+    else n_act = nprev;
+    return MP_OK;
+  };
   for (int outer = 0; outer <= D.max_iter + 1; outer++) {
-    // the derivative and sweep launches cover the n_act active instances only (compact list)
-    if ((st = run_backward(ctx, D, B, dX, dU, dn + 1, n_act, dk, dK))) return st;
+    // the derivative and sweep launches cover the active instances only (compact list dn[1..])
+    if ((st = run_backward(ctx, D, B, dX, dU, dn + 1, dn, n_act, dk, dK))) return st;
     MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
     mp_time_begin(ctx);
     if (rest && n_act <= kOnePassMax) {
@@ -1577,9 +1607,9 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
                          dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, 0, T2);
       MP_HIP(ctx, hipGetLastError());
       mp_time_end(ctx);
-      MP_HIP(ctx, hipMemcpyAsync(hn, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-      MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-      if ((n_act = *hn) == 0) break;
+      bool stop;
+      if ((st = poll(outer, &stop))) return st;
+      if (stop) break;
       continue;
     }
     // G = 16: a lane quad per trial (4 waves per SIMD at B = 4096); the narrower fallbacks one lane
@@ -1609,9 +1639,9 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
       MP_HIP(ctx, hipGetLastError());
     }
     mp_time_end(ctx);
-    MP_HIP(ctx, hipMemcpyAsync(hn, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-    MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if ((n_act = *hn) == 0) break;
+    bool stop;
+    if ((st = poll(outer, &stop))) return st;
+    if (stop) break;
   }
   std::vector<int> hfl(B);
   if ((st = mp_download(ctx, X, (const double*)dX, 4 * N * B))) return st;
