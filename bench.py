@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--final-inline", action="store_true",
                     help="final rollout at the end of the plan kernel (final_stream=0) instead of the side stream")
     ap.add_argument("--no-extras", action="store_true", help="skip the iLQR (configs[2]) and Hybrid A* (configs[3]) lines")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal of N>1 on a one-GPU box: every rank on cuda:0, gloo instead of RCCL")
     return ap.parse_args()
 
 
@@ -63,12 +65,51 @@ def algorithmic_bytes(S, K, H):
     return S * K * per_rollout
 
 
-def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
-    """Time `steps` plan calls of S scenes; returns (elapsed_s_max, kernel_ms_mean, valid)."""
+def host_cpu():
+    """The host CPU model (lscpu's "Model name", from /proc/cpuinfo) and the CPUs this process may use."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count()
+    return {"model": model, "host_cpus": os.cpu_count(), "usable_cpus": usable}
+
+
+def gather_f64(vals, dev):
+    """all_gather of a short float64 vector from every rank -> list of lists (rank order)."""
+    world = dist.get_world_size()
+    on_dev = dist.get_backend() == "nccl"
+    t = torch.tensor(vals, dtype=torch.float64, device=dev if on_dev else "cpu")
+    if on_dev:
+        out = torch.empty((world, len(vals)), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(out, t)
+        return out.cpu().tolist()
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.tolist() for p in parts]
+
+
+def run(a, S, ctx, dev, world, rank, steps, warmup, rotate, cfg5=True):
+    """Time `steps` plan calls of S scenes; returns (elapsed_s_max, kernel_ms_mean, valid, K, H, fc, fields).
+    cfg5: the scenes are rank r's block [rS, (r+1)S) of configs[4]'s 64 (own X0 and own obstacle_field.mat
+    grid each, configs.cfg5_shard); else S copies of configs[1]'s scene."""
     from motionplanning_amd import configs
     from motionplanning_amd.abi import MP_NOISE_PHILOX, ptr
 
-    c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415)
+    if cfg5:
+        c = configs.cfg5_shard(rank * S, S, noise_mode=MP_NOISE_PHILOX, seed=20260415)
+        X0, goal, grid, fields = c["X0"], c["goal"], c["grid"], c["fields"]
+    else:
+        c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415)
+        X0, goal, grid, fields = np.tile(c["X0"], (S, 1)), np.tile(c["goal"], (S, 1)), np.tile(c["grid"], (S, 1, 1)), []
     p = c["params"]
     p.scene_base = rank * S  # global scene ids: rank r plans scenes [rS, (r+1)S) of the job
     p.final_stream = 0 if a.final_inline else 1  # final rollout on the side stream, overlapping the next step
@@ -77,11 +118,9 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
     def t(x, dt=torch.float64):
         return torch.as_tensor(np.ascontiguousarray(x), dtype=dt, device=dev).contiguous()
 
-    X0 = np.tile(c["X0"], (S, 1))
-    X0[:, 1] = np.linspace(-0.5, 0.5, S) if S > 1 else 0.0
-    dX0, dgoal = t(X0), t(np.tile(c["goal"], (S, 1)))
+    dX0, dgoal = t(X0), t(goal)
     dun = t(np.zeros((S, H, 2)))
-    dgrid = t(np.tile(c["grid"], (S, 1, 1)), torch.uint8)
+    dgrid = t(grid, torch.uint8)
     sets = []
     for _ in range(max(1, rotate)):
         sets.append(dict(
@@ -105,8 +144,12 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
             ctx.handle, ctypes.byref(p), S, ptr(dX0), ptr(dgoal), ptr(dun), None, ptr(dgrid), None, ptr(b["U"]),
             ptr(b["traj"]), ptr(b["cost"]), ptr(b["feas"]), ptr(b["rc"]), ptr(b["fc"]), ptr(b["ctraj"]),
             ptr(b["cctrl"]), ptr(b["ccost"]), ptr(b["cfeas"])))
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, b["U"])
+        if world > 1 and dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(gathered, b["U"])  # RCCL, on the library's stream
+        elif world > 1:  # --share-device rehearsal over gloo: host copies
+            parts = [torch.empty((S, H, 2), dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(parts, b["U"].cpu())
+            gathered.copy_(torch.cat(parts))
 
     for i in range(warmup):
         step(i)
@@ -128,31 +171,44 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate):
     ok = all(bool((b["rc"] == K + 1).all().item()) and bool(torch.isfinite(b["cost"]).all().item())
              for b in sets[: min(len(sets), warmup + steps)])
     if world > 1:
-        tt = torch.tensor([elapsed, kern_ms, 0.0 if ok else 1.0], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, ok = float(tt[0]), float(tt[1]), tt[2].item() == 0.0
-    return elapsed, kern_ms, ok, K, H, p.feasibility_count
+        rows = gather_f64([elapsed, kern_ms, 0.0 if ok else 1.0], dev)
+        elapsed, kern_ms = max(r[0] for r in rows), max(r[1] for r in rows)
+        ok = all(r[2] == 0.0 for r in rows)
+    return elapsed, kern_ms, ok, K, H, p.feasibility_count, fields
 
 
 def main():
     a = parse()
+    # `--gpus N` without a launcher: N fresh rank processes of this same command (before any GPU call)
+    from motionplanning_amd.launch import relaunch_if_needed
+
+    status = relaunch_if_needed(a.gpus)
+    if status is not None:
+        sys.exit(status)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = 0 if a.share_device else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.share_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    # which ranks joined, on which GPU (PCI bus id): proof that N ranks ran on N devices
+    pci = getattr(torch.cuda.get_device_properties(gpu), "pci_bus_id", -1)
+    joined = gather_f64([rank, local, gpu, pci], dev) if world > 1 else [[0, local, gpu, pci]]
 
     from motionplanning_amd.context import Context
 
-    ctx = Context(local)
+    ctx = Context(gpu)
     ctx.lib.mp_ctx_kernel_timing(ctx.handle, 1)
     stream = torch.cuda.ExternalStream(ctx.stream, device=dev)
     torch.cuda.set_stream(stream)  # RCCL all_gather is ordered after the plan kernel
 
     S = a.scenes
-    elapsed, kern_ms, ok, K, H, fc = run(a, S, ctx, dev, world, rank, a.steps, a.warmup, a.rotate)
+    elapsed, kern_ms, ok, K, H, fc, fields = run(a, S, ctx, dev, world, rank, a.steps, a.warmup, a.rotate)
     value = world * S * K * H * a.steps / elapsed
     nbytes = algorithmic_bytes(S, K, H)
     achieved = nbytes / (kern_ms * 1e-3) / 1e9
@@ -160,7 +216,10 @@ def main():
         "metric": BASE["metric"],
         "value": value,
         "unit": "rollout-steps/s",
-        "n_gpus": world,
+        "n_gpus": dist.get_world_size() if world > 1 else 1,
+        "ranks": [{"rank": int(r[0]), "local_rank": int(r[1]), "device": int(r[2]), "pci_bus_id": int(r[3])}
+                  for r in joined],
+        "gpus_requested": a.gpus,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
@@ -168,15 +227,19 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded Philox noise drawn on device; cfg1 circles rasterised into a 100x100 grid)",
+        "data": "synthetic (seeded Philox noise drawn on device); per-scene 100x100 occupancy grids rasterised "
+                "from PathPlanning/Scenarios/obstacle_field.mat fields (rescaled, tests/golden/obstacle_fields_64.npz)",
         "config": {
-            "workload": f"configs[4] per-GPU shard: {S} independent scenes per GPU, each configs[1] (MPPI K=8192 "
-                        "H=50 dynamic bicycle, 2-D occupancy-grid cost, full TrajectoryCollection, weights + "
-                        "MPPICtrl + final rollout)",
+            "workload": f"configs[4] per-GPU shard: {S} of the 64 independent scenes per GPU (scene g: own X0 and "
+                        "obstacle_field.mat field g+1), each configs[1] (MPPI K=8192 H=50 dynamic bicycle, 2-D "
+                        "occupancy-grid cost, full TrajectoryCollection, weights + MPPICtrl + final rollout)",
+            "obstacle_fields_rank0": fields,
             "K": K, "H": H, "scenes_per_gpu": S, "feasibility_count": fc,
             "final_rollout": "in plan kernel" if a.final_inline else
                              "side stream (final_stream=1): overlaps the next step's rollouts",
-            "parallelism": f"scene-sharded x{world}" + (" + RCCL all_gather(MPPICtrl)" if world > 1 else ""),
+            "parallelism": f"scene-sharded x{world}" + ((" + gloo all_gather(MPPICtrl), all ranks on cuda:0 "
+                                                          "(--share-device rehearsal)") if a.share_device and world > 1
+                                                         else " + RCCL all_gather(MPPICtrl)" if world > 1 else ""),
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -207,7 +270,7 @@ def main():
                 out["roofline"]["valu"]["simd_busy_source"] = (tr["source"] + " SQ_ACTIVE_INST_VALU / "
                                                                "SQ_WAVE_CYCLES x SQ_WAVES / 1024 SIMDs")
     if not a.no_single and S != 1:
-        e1, k1, ok1, _, _, _ = run(a, 1, ctx, dev, world, rank, a.steps, a.warmup, 12)
+        e1, k1, ok1 = run(a, 1, ctx, dev, world, rank, a.steps, a.warmup, 12, cfg5=False)[:3]
         out["single_scene"] = {
             "workload": "configs[1] exactly: one scene per GPU per step (latency-bound serial chain)",
             "value": world * K * H * a.steps / e1, "ms_per_step": e1 / a.steps * 1e3, "kernel_ms": k1,
@@ -244,9 +307,7 @@ def load_traffic(path, S, K, H):
 def _sync_max(x, world, dev):
     if world == 1:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t[0])
+    return max(r[0] for r in gather_f64([x], dev))
 
 
 def bench_ilqr(ctx, world, rank, cpu=False, reps=20, B=4096, N=100):
@@ -538,7 +599,7 @@ def cpu_baseline(budget_s):
     u1, n1, t1 = timed_pool(work, budget_s / 3, 1)
     T = cpu_threads()
     uT, nT, tT = timed_pool(work, budget_s, T)
-    return {"value": uT / tT, "unit": "rollout-steps/s", "cores": T, "kind": "port",
+    return {"value": uT / tT, "unit": "rollout-steps/s", "cores": T, "kind": "port", "host": host_cpu(),
             "sample": f"{nT} full cfg2 MPPIPlan solves (K=8192, H=50, grid, Philox noise) in {tT:.1f} s on {T} "
                       f"threads (one solve per thread at a time), scalar C oracle, {os.cpu_count()}-CPU host",
             "single_thread": {"value": u1 / t1, "cores": 1, "sample": f"{n1} solves in {t1:.1f} s"}}

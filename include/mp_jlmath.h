@@ -511,8 +511,8 @@ MPJ_FN double mpj_exp(double x) {
   }
   double t = x * x;
   double twopk;
-  if (k >= -1021) twopk = mpj_from_words((uint32_t)(0x3ff00000 + (k << 20)), 0);
-  else twopk = mpj_from_words((uint32_t)(0x3ff00000 + ((k + 1000) << 20)), 0);
+  if (k >= -1021) twopk = mpj_from_words(0x3ff00000u + ((uint32_t)k << 20), 0);
+  else twopk = mpj_from_words(0x3ff00000u + ((uint32_t)(k + 1000) << 20), 0);
   double c = x - t * mpj_fma(t, mpj_fma(t, mpj_fma(t, mpj_fma(t, P5, P4), P3), P2), P1);
   if (k == 0) return 1.0 - ((x * c) / (c - 2.0) - x);
   double y = 1.0 - ((lo - (x * c) / (2.0 - c)) - hi);
@@ -903,7 +903,7 @@ MPJ_FN double mpj_exp_fast(double x, int* bad) {
   const double q = (xr * c) / (2.0 - c);
   const double r0 = 1.0 - ((-q) - xr);
   const double y = 1.0 - ((lo - q) - hi);
-  const double twopk = mpj_from_words((uint32_t)(0x3ff00000 + (k << 20)), 0);
+  const double twopk = mpj_from_words(0x3ff00000u + ((uint32_t)k << 20), 0);
   return MPJ_SEL(k == 0, r0, y * twopk);
 }
 MPJ_FN double mpj_exp_bl(double x) {

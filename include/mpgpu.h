@@ -221,6 +221,36 @@ int mp_mppi_closed_loop(mp_ctx* ctx, const mp_mppi_params* p, const mp_mppi_loop
                         int32_t* n_rows, int32_t* n_replans, double* U_log, double* traj_log, double* cost_log,
                         int32_t* feas_log, int32_t* rc_log);
 
+/* ----------------------------------------------------------- multi-GPU */
+/*
+ * One host process driving several GPUs (the Julia host of OptimalControl/MPPI/main.jl:59-61 keeps
+ * its single process): one context per GPU, joined into one RCCL communicator
+ * (ncclCommInitAll over the contexts' devices, xGMI between MI355X GPUs).  ctxs[i] is rank i; every
+ * call below takes the same array in the same order.  Errors are reported on ctxs[0]
+ * (mp_last_error(ctxs[0])).  RCCL is loaded on first use: MP_ERR_UNSUPPORTED without librccl.
+ * Call mp_comm_destroy before destroying the contexts.
+ */
+int mp_comm_init(mp_ctx** ctxs, int32_t n);
+int mp_comm_destroy(mp_ctx** ctxs, int32_t n);
+/* ncclAllGather of `bytes` bytes per rank: DEVICE buffers send[i] (on ctxs[i]'s GPU) -> recv[i]
+ * ([n][bytes], rank-major), enqueued on every context stream (asynchronous). */
+int mp_comm_allgather_dev(mp_ctx** ctxs, int32_t n, void* const* send, void* const* recv, size_t bytes);
+
+/*
+ * mp_mppi_plan_sharded — multi-ego MPPIPlan (MPPIUtils.jl:169-203) of S independent scenes sharded over
+ * the n GPUs of a communicator: ctxs[r] plans the balanced block [a_r, b_r) of scenes (the first
+ * S mod n ranks take one extra) with Philox counter word p->scene_base + a_r — so every scene draws
+ * the noise it draws in one mp_mppi_plan over all S — then one RCCL all-gather of the per-scene
+ * results (MPPICtrl, final trajectory, cost, flags, counts: (2H + 7(H+1) + 4) doubles per scene) leaves
+ * every GPU holding all S scenes' optimal controls; the host outputs are copied from ctxs[0]'s copy.
+ * Inputs and outputs as mp_mppi_plan over all S scenes (HOST pointers, synchronous); the
+ * TrajectoryCollection stays per GPU and is not returned here.
+ */
+int mp_mppi_plan_sharded(mp_ctx** ctxs, int32_t n, const mp_mppi_params* p, int32_t S, const double* X0,
+                         const double* goal, const double* U_nom, const double* obstacles, const uint8_t* grid,
+                         const double* noise, double* U_out, double* traj_out, double* cost_out,
+                         int32_t* feasible_out, int32_t* rollout_count_out, int32_t* feasible_count_out);
+
 /* ---------------------------------------------------------------- iLQR */
 #define MP_ILQR_NX 4 /* [x, y, ux, ψ]  OptimalControl/ILQR/Dynamics.jl:4-7 */
 #define MP_ILQR_NU 2 /* [ax, δ]                                          */

@@ -8,6 +8,8 @@ hot-path functions below take over the reference's names on the same searcher ob
   * `MPPIPlan(mppi::MPPISearcher)`      OptimalControl/MPPI/src/MPPIUtils.jl:169-203
   * `TrajectoryRollout(mppi, ctrl)`     MPPIUtils.jl:31-57 (batched form: `rollout_batch`)
   * `MPPIClosedLoop(mppi)`              the replan / plant loop of OptimalControl/MPPI/main.jl:49-83
+  * `mppi_plan_sharded` (+ `comm_init`) multi-ego MPPIPlan over all GPUs of the node from one process
+                                        (RCCL all-gather of the optimal controls)
   * `planHybridAstar!(ha)`              PathPlanning/HybridAstar/src/hybrid_astar_utils.jl:235-296
   * `RS_connected`, `FindNewNode` device parts (`ha_rs_connect`, `ha_expand`)
   * iLQR passes (`ilqr_backward!`, `ilqr_forward!`, `ilqr_solve!`)  OptimalControl/ILQR/ILQR.jl:44-88
@@ -26,8 +28,10 @@ module MPGPU
 
 using Interpolations: interpolate, Gridded, Constant, Previous, linear_interpolation   # as the reference drivers
 
-export MPPIPlan, MPPIClosedLoop, planHybridAstar!, mppi_plan_batch, mppi_closed_loop_batch, rollout_batch, ha_expand, ha_rs_connect,
-       ha_allpath, retrieve_batch!, track_batch!, ilqr_backward!, ilqr_forward!, ilqr_solve!
+export MPPIPlan, MPPIClosedLoop, planHybridAstar!, mppi_plan_batch, mppi_plan_sharded, comm_init, mppi_closed_loop_batch,
+       rollout_batch, ha_expand, ha_rs_connect,
+       ha_allpath, ha_neighbor_origin, retrieve_batch!, track_batch!, ilqr_rollout, ilqr_backward!, ilqr_forward!,
+       ilqr_solve!, vehicle_euler!, ctx_join
 
 const libmpgpu = get(ENV, "MPGPU_LIB", joinpath(@__DIR__, "..", "motionplanning_amd", "lib", "libmpgpu.so"))
 
@@ -188,6 +192,7 @@ end
                            δt, goal_radius; obstacles, noise (2,H,K,S,R)) -> NamedTuple
 
 S closed loops of OptimalControl/MPPI/main.jl:55-83 in lockstep on the device (mp_mppi_closed_loop).
+`grid` is the occupancy grid (grid_nx, grid_ny, S) UInt8 of the MppiParams, or `nothing`.
 `hold[i]` is the 1-based row of NominalControls the interpolation picks at plant step i of a
 period.  Returns his (8, max_steps+1, S) with n_rows[s] valid columns (the states_his matrix of
 main.jl per scene), n_replans, and per-replan logs U (2, H, R, S), traj (7, H+1, R, S),
@@ -196,7 +201,7 @@ cost / feasible / rollout_count (R, S).
 function mppi_closed_loop_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Float64},
                                 Unom0::Array{Float64,3}, hold::Vector{Int32}, update_idx::Integer,
                                 max_steps::Integer, δt::Float64, goal_radius::Float64;
-                                obstacles = nothing, noise = nothing, poll_every::Integer = 0)
+                                obstacles = nothing, grid = nothing, noise = nothing, poll_every::Integer = 0)
     S = size(X0, 2); H = Int(p.H)
     R = cld(max_steps, update_idx)
     p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 25)...)
@@ -207,12 +212,14 @@ function mppi_closed_loop_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix
     cost = zeros(max(R, 1), S); feas = zeros(Int32, max(R, 1), S); rc = zeros(Int32, max(R, 1), S)
     nz(a) = a === nothing ? C_NULL : pointer(a)
     c = ctx()
-    st = GC.@preserve X0 goal Unom0 obstacles h0 noise his nr np_ U traj cost feas rc begin
+    grid === nothing || size(grid) == (Int(p.grid_nx), Int(p.grid_ny), S) ||
+        error("grid must be UInt8 (grid_nx, grid_ny, S) = ", (p.grid_nx, p.grid_ny, S))
+    st = GC.@preserve X0 goal Unom0 obstacles grid h0 noise his nr np_ U traj cost feas rc begin
         ccall((:mp_mppi_closed_loop, libmpgpu), Cint,
               (Ptr{Cvoid}, Ref{MppiParams}, Ref{MppiLoopParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
                Ptr{Float64}, Ptr{UInt8}, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32},
                Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Int32}),
-              c, p, lp, S, X0, goal, Unom0, nz(obstacles), C_NULL, h0, nz(noise), his, nr, np_, U, traj, cost,
+              c, p, lp, S, X0, goal, Unom0, nz(obstacles), nz(grid), h0, nz(noise), his, nr, np_, U, traj, cost,
               feas, rc)
     end
     st == MP_ERR_NUMERIC && @warn "MPPI closed loop: NaN rollout cost (outputs written)"
@@ -251,6 +258,88 @@ function MPPIClosedLoop(mppi; update_time = 0.1, δt = 1e-3, sim_time = 15, goal
         mppi.r.RolloutCount = r.rollout_count[R, 1]
     end
     return r.his[:, 1:r.n_rows[1], 1]
+end
+
+"""Order the context stream after the side stream's deferred final rollouts (MppiParams.final_stream = 1)."""
+ctx_join() = (c = ctx(); check(ccall((:mp_ctx_join, libmpgpu), Cint, (Ptr{Cvoid},), c), c))
+
+"""
+    vehicle_euler!(states (7, n), ctrl (2, n), δt, nsteps; his = false) -> (states, his (7, nsteps, n) or nothing)
+
+The closed-loop plant of MPPI/main.jl and DynamicWindow/main.jl:155-156 (`states .+= VehicleDynamics(states,
+u)*δt`, u held) for n vehicles, in place.
+"""
+function vehicle_euler!(states::Matrix{Float64}, ctrl::Matrix{Float64}, δt::Float64, nsteps::Integer; his = false)
+    n = size(states, 2); h = his ? zeros(7, nsteps, n) : nothing
+    c = ctx()
+    check(GC.@preserve states ctrl h ccall((:mp_vehicle_euler, libmpgpu), Cint,
+        (Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Float64, Int32, Ptr{Float64}),
+        c, n, states, ctrl, δt, nsteps, h === nothing ? C_NULL : pointer(h)), c)
+    return states, h
+end
+
+# ------------------------------------------------------ multi-GPU, one process
+const GROUP = Ref{Vector{Ptr{Cvoid}}}(Ptr{Cvoid}[])
+
+"""
+    comm_init(devices = all) -> Vector{Ptr{Cvoid}}
+
+One context per GPU of this node joined into one RCCL communicator (mp_comm_init: ncclCommInitAll,
+xGMI between the MI355X GPUs), created once per process.  The Julia host stays a single process
+(north_star); `mppi_plan_sharded` spreads the scenes over these contexts.
+"""
+function comm_init(devices = nothing)
+    if isempty(GROUP[])
+        nd = Ref{Cint}(0)
+        st = ccall((:mp_device_count, libmpgpu), Cint, (Ref{Cint},), nd)
+        st == MP_OK || error("libmpgpu: ", last_error(Ptr{Cvoid}(C_NULL)))
+        devs = devices === nothing ? collect(0:nd[]-1) : collect(devices)
+        cs = Ptr{Cvoid}[]
+        for d in devs
+            r = Ref{Ptr{Cvoid}}(C_NULL)
+            st = ccall((:mp_ctx_create, libmpgpu), Cint, (Cint, Ref{Ptr{Cvoid}}), d, r)
+            st == MP_OK || error("libmpgpu: ", last_error(Ptr{Cvoid}(C_NULL)))
+            push!(cs, r[])
+        end
+        st = ccall((:mp_comm_init, libmpgpu), Cint, (Ptr{Ptr{Cvoid}}, Int32), cs, length(cs))
+        st == MP_OK || error("libmpgpu: ", last_error(cs[1]))
+        GROUP[] = cs
+        atexit() do
+            g = GROUP[]
+            ccall((:mp_comm_destroy, libmpgpu), Cint, (Ptr{Ptr{Cvoid}}, Int32), g, length(g))
+            foreach(c -> ccall((:mp_ctx_destroy, libmpgpu), Cint, (Ptr{Cvoid},), c), g)
+            GROUP[] = Ptr{Cvoid}[]
+        end
+    end
+    return GROUP[]
+end
+
+"""
+    mppi_plan_sharded(p, X0 (7,S), goal (2,S), Unom (2,H,S); obstacles, grid, noise) -> NamedTuple
+
+Multi-ego MPPIPlan over every GPU of `comm_init()` (mp_mppi_plan_sharded): scenes in balanced blocks per
+GPU, then one RCCL all-gather of the optimal controls, final trajectories, costs and counts.  Same
+results as `mppi_plan_batch` over all S scenes (the noise stream of a scene does not depend on the GPU
+count).  Shapes as `mppi_plan_batch`; no TrajectoryCollection.
+"""
+function mppi_plan_sharded(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Float64}, Unom::Array{Float64,3};
+                           obstacles = nothing, grid = nothing, noise = nothing)
+    cs = comm_init()
+    S = size(X0, 2); H = Int(p.H)
+    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 25)...)
+    U = zeros(2, H, S); traj = zeros(7, H + 1, S); cost = zeros(S)
+    feas = zeros(Int32, S); rc = zeros(Int32, S); fc = zeros(Int32, S)
+    nz(a) = a === nothing ? C_NULL : pointer(a)
+    st = GC.@preserve cs X0 goal Unom obstacles grid noise U traj cost feas rc fc begin
+        ccall((:mp_mppi_plan_sharded, libmpgpu), Cint,
+              (Ptr{Ptr{Cvoid}}, Int32, Ref{MppiParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+               Ptr{Float64}, Ptr{UInt8}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32},
+               Ptr{Int32}, Ptr{Int32}),
+              cs, length(cs), p, S, X0, goal, Unom, nz(obstacles), nz(grid), nz(noise), U, traj, cost, feas, rc, fc)
+    end
+    st == MP_ERR_NUMERIC && @warn "MPPIPlan (sharded): NaN rollout cost (outputs written)"
+    st == MP_ERR_NUMERIC || check(st, cs[1])
+    return (; U, traj, cost, feasible = feas, rollout_count = rc, feasible_count = fc)
 end
 
 """
@@ -292,6 +381,18 @@ function ha_params(ha; max_pops = 5000)
     HaParams(s.vehicle_size[1], s.vehicle_size[2], s.minR, s.expand_time, Tuple(s.resolutions),
              (sb[1, 1], sb[1, 2], sb[2, 1], sb[2, 2], sb[3, 1], sb[3, 2]), length(s.obstacle_list),
              s.num_neighbors, size(s.paths_candi, 2), max_pops)
+end
+
+"""neighbor_origin (hybrid_astar_utils.jl:483-503) computed on the device and installed in the context:
+(states_candi 3×n, paths_candi 3×n_col×n), n = length(gear_set)·length(steer_set)."""
+function ha_neighbor_origin(p::HaParams, steer_set::Vector{Float64}, gear_set::Vector{Float64})
+    n = length(steer_set) * length(gear_set)
+    sc = zeros(3, n); pc = zeros(3, Int(p.n_col), n)
+    c = ctx()
+    check(GC.@preserve steer_set gear_set sc pc ccall((:mp_ha_neighbor_origin, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{HaParams}, Int32, Ptr{Float64}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+        c, p, length(steer_set), steer_set, length(gear_set), gear_set, sc, pc), c)
+    return sc, pc
 end
 
 """Install the searcher's own neighbor_origin table (states_candi 3×n, paths_candi 3×n_col×n):
@@ -425,8 +526,17 @@ function track_batch!(has::AbstractVector; look_ahead_dist = 1.0, p_gain = 10, i
     for (b, h) in enumerate(has)
         haskey(SAMPLES, h) && (smp[:, :, b] = SAMPLES[h])
     end
-    p = TrackParams(n_ref, max_steps, dt_sim, look_ahead_dist, p_gain, i_gain, Float64(has[1].s.vehicle_size[1]),
-                    max_sa, his_stride, 0)
+    vl = unique(Float64(h.s.vehicle_size[1]) for h in has)   # veh_param[1] per searcher (main_Tracker.jl:50)
+    if length(vl) > 1        # one launch per vehicle length, results in the caller's order
+        out = Vector{Any}(undef, B)
+        for L in vl
+            ix = findall(h -> Float64(h.s.vehicle_size[1]) == L, has)
+            out[ix] = track_batch!(has[ix]; look_ahead_dist, p_gain, i_gain, dt_sim, max_sa, n_ref, max_steps,
+                                   his_stride, his_cap)
+        end
+        return out
+    end
+    p = TrackParams(n_ref, max_steps, dt_sim, look_ahead_dist, p_gain, i_gain, vl[1], max_sa, his_stride, 0)
     n = zeros(Int32, B); st = zeros(Int32, B); fin = zeros(3, B); ea = zeros(B)
     ref = zeros(3, n_ref, B); his = zeros(3, his_cap, B)
     c = ctx()
@@ -486,6 +596,15 @@ struct IlqrParams
 end
 IlqrParams(N; variant = 0, dT = 0.05, eps = 1e-3, tol = 1e-6, max_iter = 1000, max_ls = 200) =
     IlqrParams(N, variant, dT, eps, variant == 1 ? 1e-3 : 0.0, tol, max_iter, max_ls)
+
+"""Initial-guess roll out (ILQR.jl:31-37) + TotalCost (Cost.jl:1-8): x0 (4, B), U (2, N, B) -> (X (4, N, B), J (B,))."""
+function ilqr_rollout(p::IlqrParams, x0::Matrix{Float64}, U::Array{Float64,3})
+    B = size(x0, 2); X = zeros(4, Int(p.N), B); J = zeros(B); c = ctx()
+    check(GC.@preserve x0 U X J ccall((:mp_ilqr_rollout, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{IlqrParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+        c, p, B, x0, U, X, J), c)
+    return X, J
+end
 
 """One backward Riccati sweep (ILQR.jl:46-67) for B instances: X (4, N, B), U (2, N, B)
 -> k (2, N-1, B), K (2, 4, N-1, B) (the reference's klist / Klist per instance)."""

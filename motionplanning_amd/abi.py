@@ -179,6 +179,10 @@ SIGNATURES = {
     "mp_ha_retrieve_path": (ctypes.c_int, [_V, _I, _V, _V, _V, _I] + [_V] * 8),
     "mp_ha_track": (ctypes.c_int, [_V, ctypes.POINTER(TrackParams), _I, _V, _V, _V, _I] + [_V] * 6 + [_I]),
     "mp_math_eval": (ctypes.c_int, [_V, _I, ctypes.c_int64, _V, _V, _V]),
+    "mp_comm_init": (ctypes.c_int, [_V, _I]),
+    "mp_comm_destroy": (ctypes.c_int, [_V, _I]),
+    "mp_comm_allgather_dev": (ctypes.c_int, [_V, _I, _V, _V, ctypes.c_size_t]),
+    "mp_mppi_plan_sharded": (ctypes.c_int, [_V, _I, ctypes.POINTER(MPPIParams), _I] + [_V] * 12),
 }
 
 _lib = None

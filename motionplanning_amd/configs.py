@@ -5,6 +5,7 @@ the host-side planner mirror (mppi.py / dwa.py / ilqr.py / hybrid_astar.py),
 the tests and bench.py.
 """
 import math
+import os
 
 import numpy as np
 
@@ -162,3 +163,39 @@ def cfg2(feasibility_count=None, noise_mode=MP_NOISE_EXTERNAL, seed=20260415, wi
 def standard_noise(K, H, seed=20260415):
     """z ~ N(0,1), numpy PCG64(seed), shape (K, H, 2)."""
     return np.random.Generator(np.random.PCG64(seed)).standard_normal((K, H, 2))
+
+
+# ------------------------------------------------- configs[4]: 64 multi-ego scenes
+FIELDS_NPZ = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                          "obstacle_fields_64.npz")
+N_SCENES_CFG5 = 64
+
+
+def obstacle_field(g):
+    """Circles [n][3] of scene g (0-based): PathPlanning/Scenarios/obstacle_field.mat field g+1 (Julia
+    index), rescaled into the corridor by tests/golden/make_obstacle_fields.py."""
+    d = np.load(FIELDS_NPZ)
+    f = g % N_SCENES_CFG5
+    return d["circles"][f, :int(d["count"][f])]
+
+
+def cfg5_x0(g):
+    """X0 of scene g: the reference start (MPPI/main.jl:7) with the lateral offset y = -0.5 + (g mod 8)/7."""
+    x = np.array(X0_REF)
+    x[1] = -0.5 + (g % 8) / 7.0
+    return x
+
+
+def cfg5_shard(scene_base, S, noise_mode=MP_NOISE_EXTERNAL, seed=20260415):
+    """BASELINE.json configs[4] ("64 independent scenes x K=8192 x H=50"): scenes [scene_base, scene_base+S),
+    each configs[1] (K=8192, H=50, 100x100 occupancy grid) with its own X0 (cfg5_x0) and its own grid,
+    rasterised from obstacle_field.mat field g+1.  params.scene_base = scene_base (Philox counter word)."""
+    c = cfg2(noise_mode=noise_mode, seed=seed)
+    p = c["params"]
+    p.scene_base = scene_base
+    spec = grid_spec()
+    gs = list(range(scene_base, scene_base + S))
+    X0 = np.stack([cfg5_x0(g) for g in gs])
+    grids = np.stack([rasterize_circles(obstacle_field(g), spec) for g in gs])
+    return dict(params=p, X0=X0, goal=np.tile(GOAL_REF, (S, 1)), grid=grids, unom=np.zeros((S, p.H, 2)),
+                fields=[g % N_SCENES_CFG5 + 1 for g in gs])

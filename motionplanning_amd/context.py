@@ -51,6 +51,40 @@ class Context:
             pass
 
 
+class CommGroup:
+    """One host process driving several GPUs: a Context per device joined into one RCCL communicator
+    (mp_comm_init, ncclCommInitAll) — the single-process multi-GPU path of include/mpgpu.h that a Julia
+    host uses (torch.distributed's one-process-per-GPU path is motionplanning_amd/distributed.py)."""
+
+    def __init__(self, devices):
+        self.ctxs = [Context(d) for d in devices]
+        self.lib = self.ctxs[0].lib
+        self.n = len(self.ctxs)
+        self.array = (ctypes.c_void_p * self.n)(*[c.handle.value for c in self.ctxs])
+        st = self.lib.mp_comm_init(self.array, self.n)
+        if st != MP_OK:
+            raise MPGPUError(st, self.lib.mp_last_error(self.ctxs[0].handle).decode())
+        self.live = True
+
+    def check(self, st):
+        if st != MP_OK:
+            raise MPGPUError(st, self.lib.mp_last_error(self.ctxs[0].handle).decode())
+        return st
+
+    def close(self):
+        if getattr(self, "live", False):
+            self.lib.mp_comm_destroy(self.array, self.n)
+            self.live = False
+        for c in getattr(self, "ctxs", []):
+            c.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def default_context(device=None):
     """Per-thread default context on `device` (default: LOCAL_RANK or 0)."""
     import os

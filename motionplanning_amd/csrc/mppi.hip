@@ -88,9 +88,12 @@ struct PlanArgs {
 };
 
 // Snapshot record of one scene for the deferred final rollout (final_stream = 1), in doubles:
-// [0, 2H) MPPICtrl | [2H, 4H) U_nom | X0[7] | goal[2] | obstacles[3 n_obs] | grid bytes
+// [0, 2H) MPPICtrl | [2H, 4H) U_nom | X0[7] | goal[2] | obstacles[3 n_obs] | grid bytes | ran
+// `ran` (1.0 / 0.0) is written by the plan kernel of the same call: whether it planned the scene.
+// The final rollout reads it, not the closed loop's live flags, which the plant kernel on the
+// context stream may already have cleared for a later replan when the side stream gets there.
 struct FinRec {
-  int u, unom, x0, goal, obs, grid, stride;
+  int u, unom, x0, goal, obs, grid, ran, stride;
   __host__ __device__ FinRec(int H, int n_obs, int gbytes) {
     u = 0;
     unom = 2 * H;
@@ -98,7 +101,8 @@ struct FinRec {
     goal = x0 + 7;
     obs = goal + 2;
     grid = obs + 3 * n_obs;
-    stride = (grid + (gbytes + 7) / 8 + 1) & ~1;
+    ran = grid + (gbytes + 7) / 8;
+    stride = (ran + 2) & ~1;
   }
 };
 
@@ -169,7 +173,10 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   const int k = b * RPB + pair;
   const bool active = k < K;
   const int kk = active ? k : K - 1;
-  if (A.live && A.live[s] == 0) return;  // closed loop: this scene has reached its goal (block-uniform)
+  if (A.live && A.live[s] == 0) {  // closed loop: this scene has reached its goal (block-uniform)
+    if (A.fin && b == 0 && tid == 0) A.fin[(size_t)s * A.fin_stride + FinRec(H, P.n_obs, P.gnx * P.gny).ran] = 0.0;
+    return;
+  }
   MP_STAMP(0);
   __builtin_amdgcn_s_setprio(3);
 
@@ -446,6 +453,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       rec[R.unom + t] = unom[t];
     }
     if (tid < 7) rec[R.x0 + tid] = X0[tid];
+    if (tid == 0) rec[R.ran] = 1.0;
     if (tid < 2) rec[R.goal + tid] = goal[tid];
     for (int i = tid; i < 3 * P.n_obs; i += NT) rec[R.obs + i] = obs[i];
     if (grid) {
@@ -481,13 +489,13 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
 // rollouts already occupy the rest of the GPU.
 __global__ __launch_bounds__(64) void final_rollout_kernel(MppiDev P, const double* fin, int fin_stride,
                                                            int grid_lds, double* traj_out, double* cost_out,
-                                                           int* feas_out, int* flags, const int* live) {
+                                                           int* feas_out, int* flags) {
   extern __shared__ double fsh[];
   __shared__ double atab[20];
   const int s = blockIdx.x, tid = threadIdx.x, side = tid & 1, H = P.H;
-  if (live && live[s] == 0) return;  // closed loop: the plan kernel skipped this scene (no snapshot)
   const FinRec R(H, P.n_obs, P.gnx * P.gny);
   const double* rec = fin + (size_t)s * fin_stride;
+  if (rec[R.ran] == 0.0) return;  // closed loop: the plan kernel of this call skipped the scene
   const int nw = grid_lds ? R.stride : R.grid;  // the grid stays in the record when it does not fit
   for (int i = tid; i < nw; i += 64) fsh[i] = rec[i];
   if (tid == 0) mpj_atan_tab_init(atab);
@@ -658,6 +666,28 @@ __global__ __launch_bounds__(64) void loop_plant_kernel(int S, int H, double* st
       if (last >= max_steps) live[vv] = 0;
     }
   }
+}
+
+// ------------------------------------------------------ sharded plan (RCCL)
+// One scene's results packed for the all-gather of mp_mppi_plan_sharded, in doubles:
+// [U_out 2H | traj_out 7(H+1) | cost | feasible | rollout_count | feasible_count]
+__host__ __device__ inline int shard_rec(int H) { return 2 * H + 7 * (H + 1) + 4; }
+
+__global__ __launch_bounds__(256) void shard_pack_kernel(int S, int H, const double* U, const double* traj,
+                                                         const double* cost, const int* feas, const int* rc,
+                                                         const int* fc, double* out) {
+  const int D = shard_rec(H), nu = 2 * H, nt = 7 * (H + 1);
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)S * D) return;
+  const int s = (int)(i / D), j = (int)(i % D);
+  double v;
+  if (j < nu) v = U[(size_t)s * nu + j];
+  else if (j < nu + nt) v = traj[(size_t)s * nt + (j - nu)];
+  else {
+    const int q = j - nu - nt;
+    v = q == 0 ? cost[s] : q == 1 ? (double)feas[s] : q == 2 ? (double)rc[s] : (double)fc[s];
+  }
+  out[i] = v;
 }
 
 // ----------------------------------------------------------------- host
@@ -886,7 +916,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     }
     MP_HIP(ctx, hipStreamWaitEvent(ctx->side, plan_done, 0));
     hipLaunchKernelGGL(final_rollout_kernel, dim3(S), dim3(64), fsh, ctx->side, D, A.fin, A.fin_stride, grid_lds,
-                       traj_out, cost_out, feasible_out, ctx->flags, live);
+                       traj_out, cost_out, feasible_out, ctx->flags);
     MP_HIP(ctx, hipGetLastError());
     MP_HIP(ctx, hipEventRecord(ctx->ev_fin[par], ctx->side));
   }
@@ -1181,6 +1211,95 @@ int mp_mppi_closed_loop(mp_ctx* ctx, const mp_mppi_params* p, const mp_mppi_loop
   if ((st = gather(feas_log, dfeas, 1))) return st;
   if ((st = gather(rc_log, drc, 1))) return st;
   if (flag & 1) return mp_fail(ctx, MP_ERR_NUMERIC, "NaN rollout cost in the closed loop");
+  return MP_OK;
+}
+
+int mp_mppi_plan_sharded(mp_ctx** ctxs, int32_t n, const mp_mppi_params* p, int32_t S, const double* X0,
+                         const double* goal, const double* U_nom, const double* obstacles, const uint8_t* grid,
+                         const double* noise, double* U_out, double* traj_out, double* cost_out,
+                         int32_t* feasible_out, int32_t* rollout_count_out, int32_t* feasible_count_out) {
+  if (!ctxs || n < 1 || !ctxs[0]) return MP_ERR_INVALID;
+  mp_ctx* c0 = ctxs[0];
+  int st = mp_comm_check(ctxs, n);
+  if (st) return st;
+  MppiDev D;
+  if ((st = make_dev_params(c0, p, p ? p->K : 0, &D))) return st;
+  MP_CHECK(c0, S >= 1, "S (%d) must be >= 1", S);
+  MP_CHECK(c0, X0 && goal && U_nom && U_out && traj_out && cost_out && feasible_out && rollout_count_out &&
+               feasible_count_out, "required pointer is NULL");
+  MP_CHECK(c0, p->noise_mode != MP_NOISE_EXTERNAL || noise, "noise is NULL in MP_NOISE_EXTERNAL mode");
+  MP_CHECK(c0, p->n_obs == 0 || obstacles, "obstacles NULL with n_obs > 0");
+  MP_CHECK(c0, p->grid_nx == 0 || grid, "grid NULL with grid_nx > 0");
+  MP_CHECK(c0, p->final_stream == 0 || p->final_stream == 1, "final_stream (%d) must be 0 or 1", p->final_stream);
+  const size_t K = p->K, H = p->H, Dr = shard_rec((int)H), gb = (size_t)p->grid_nx * p->grid_ny;
+  const int base = S / n, rem = S % n, smax = base + (rem > 0);
+  auto lo = [&](int r) { return r * base + (r < rem ? r : rem); };
+  std::vector<void*> send(n), recv(n);
+  // every rank plans its block [a, b) of scenes (Philox counter word scene_base + a: the same noise as
+  // one mp_mppi_plan over all S) and packs its results; all launches are enqueued before any wait
+  for (int r = 0; r < n; r++) {
+    mp_ctx* c = ctxs[r];
+    MP_HIP(c0, hipSetDevice(c->device));
+    const int a = lo(r), cnt = lo(r + 1) - a;
+    const size_t sa = a, sc = cnt;
+    send[r] = mp_ws(c, WS_SHARD_SEND, sizeof(double) * (size_t)smax * Dr);
+    recv[r] = mp_ws(c, WS_SHARD_RECV, sizeof(double) * (size_t)n * smax * Dr);
+    if (!send[r] || !recv[r]) return mp_fail(c0, MP_ERR_NOMEM, "rank %d: %s", r, c->err.c_str());
+    if (cnt == 0) continue;  // more ranks than scenes: this rank only takes part in the gather
+    st = MP_OK;
+    const double* dX0 = mp_upload(c, WS_IO0, X0 + 7 * sa, 7 * sc, &st);
+    const double* dgoal = mp_upload(c, WS_IO1, goal + 2 * sa, 2 * sc, &st);
+    const double* dun = mp_upload(c, WS_IO2, U_nom + 2 * H * sa, 2 * H * sc, &st);
+    const double* dobs = mp_upload(c, WS_IO3, p->n_obs ? obstacles + 3 * (size_t)p->n_obs * sa : nullptr,
+                                   3 * (size_t)p->n_obs * sc, &st);
+    const uint8_t* dgrid = mp_upload(c, WS_IO4, gb ? grid + gb * sa : nullptr, gb * sc, &st);
+    const double* dnoise = mp_upload(c, WS_IO5, p->noise_mode == MP_NOISE_EXTERNAL ? noise + K * H * 2 * sa : nullptr,
+                                     K * H * 2 * sc, &st);
+    double* dU = (double*)mp_ws(c, WS_IO6, sizeof(double) * 2 * H * sc);
+    double* dtraj = (double*)mp_ws(c, WS_IO7, sizeof(double) * (H + 1) * 7 * sc);
+    double* dcost = (double*)mp_ws(c, WS_IO8, sizeof(double) * sc);
+    int32_t* dfe = (int32_t*)mp_ws(c, WS_IO9, sizeof(int32_t) * sc);
+    int32_t* drc = (int32_t*)mp_ws(c, WS_IO10, sizeof(int32_t) * sc);
+    int32_t* dfc = (int32_t*)mp_ws(c, WS_IO11, sizeof(int32_t) * sc);
+    if (st || !dU || !dtraj || !dcost || !dfe || !drc || !dfc)
+      return mp_fail(c0, st ? st : MP_ERR_NOMEM, "rank %d: %s", r, c->err.c_str());
+    MP_HIP(c0, hipMemsetAsync(c->flags, 0, sizeof(int), c->stream));
+    MppiDev Dr_ = D;
+    Dr_.scene_base = p->scene_base + a;
+    if ((st = plan_launch(c, Dr_, cnt, dX0, dgoal, dun, dobs, dgrid, dnoise, dU, dtraj, dcost, dfe, drc, dfc, nullptr,
+                          nullptr, nullptr, nullptr, p->final_stream)))
+      return mp_fail(c0, st, "rank %d: %s", r, c->err.c_str());
+    if (p->final_stream && (st = mp_ctx_join(c))) return mp_fail(c0, st, "rank %d: %s", r, c->err.c_str());
+    const long long tot = (long long)cnt * (long long)Dr;
+    hipLaunchKernelGGL(shard_pack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, cnt, (int)H,
+                       dU, dtraj, dcost, dfe, drc, dfc, (double*)send[r]);
+    MP_HIP(c0, hipGetLastError());
+  }
+  // the exchange step: every GPU ends with every scene's results (RCCL all-gather over xGMI)
+  if ((st = mp_comm_allgather(ctxs, n, send.data(), recv.data(), sizeof(double) * (size_t)smax * Dr))) return st;
+  std::vector<double> all((size_t)n * smax * Dr);
+  MP_HIP(c0, hipSetDevice(c0->device));
+  MP_HIP(c0, hipMemcpyAsync(all.data(), recv[0], all.size() * sizeof(double), hipMemcpyDeviceToHost, c0->stream));
+  int nan = 0;
+  for (int r = 0; r < n; r++) {
+    int f = 0;
+    MP_HIP(c0, hipSetDevice(ctxs[r]->device));
+    MP_HIP(c0, hipMemcpyAsync(&f, ctxs[r]->flags, sizeof(int), hipMemcpyDeviceToHost, ctxs[r]->stream));
+    MP_HIP(c0, hipStreamSynchronize(ctxs[r]->stream));
+    nan |= f & 1;
+  }
+  for (int r = 0; r < n; r++)
+    for (int s = lo(r), j = 0; s < lo(r + 1); s++, j++) {
+      const double* q = all.data() + ((size_t)r * smax + j) * Dr;
+      for (size_t t = 0; t < 2 * H; t++) U_out[(size_t)s * 2 * H + t] = q[t];
+      for (size_t t = 0; t < 7 * (H + 1); t++) traj_out[(size_t)s * 7 * (H + 1) + t] = q[2 * H + t];
+      const double* e = q + 2 * H + 7 * (H + 1);
+      cost_out[s] = e[0];
+      feasible_out[s] = (int32_t)e[1];
+      rollout_count_out[s] = (int32_t)e[2];
+      feasible_count_out[s] = (int32_t)e[3];
+    }
+  if (nan) return mp_fail(c0, MP_ERR_NUMERIC, "NaN rollout cost (Julia would have produced NaN weights)");
   return MP_OK;
 }
 

@@ -15,6 +15,8 @@
 // ahead of the GPU and the context stream never idles between plan kernels.
 #define MP_FIN_RING 4
 
+struct mp_comm_group;  // RCCL communicators of the contexts joined by mp_comm_init (comm.cpp)
+
 struct mp_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -47,6 +49,9 @@ struct mp_ctx {
   // kernel attributes (150 KiB dynamic LDS) are per device: set once per context, on its device
   // (a context is used by one thread at a time, so the flags need no lock)
   bool mppi_lds_attr = false, fin_lds_attr = false;
+  // multi-GPU in one process (mp_comm_init): the group and this context's rank in it
+  mp_comm_group* comm = nullptr;
+  int comm_rank = -1;
 };
 
 // Create the side stream and its events on first use.
@@ -92,10 +97,16 @@ enum {
   WS_HA2,
   WS_FIN0,  // MPPI final-rollout snapshots, MP_FIN_RING slots
   WS_FIN_END = WS_FIN0 + MP_FIN_RING - 1,
+  WS_SHARD_SEND,  // mp_mppi_plan_sharded: this rank's packed per-scene results
+  WS_SHARD_RECV,  // ... and every rank's, after the all-gather
   WS_COUNT
 };
 
 int mp_fail(mp_ctx* ctx, int code, const char* fmt, ...);
+// ctxs[0..n) are ranks 0..n-1 of one mp_comm_init group (error on ctxs[0] otherwise)
+int mp_comm_check(mp_ctx** ctxs, int n);
+// ncclAllGather of `bytes` per rank, ctxs[i]'s send[i] -> recv[i] ([n][bytes]) on each context stream
+int mp_comm_allgather(mp_ctx** ctxs, int n, void* const* send, void* const* recv, size_t bytes);
 void* mp_ws(mp_ctx* ctx, int slot, size_t bytes);  // nullptr on failure (error set)
 // bytes currently held by a workspace slot (0 if none)
 size_t mp_ws_size(mp_ctx* ctx, int slot);

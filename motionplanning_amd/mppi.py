@@ -199,6 +199,36 @@ def mppi_plan_batch(p: MPPIParams, X0, goal, U_nom, obstacles=None, grid=None, n
     return out
 
 
+def mppi_plan_sharded(group, p: MPPIParams, X0, goal, U_nom, obstacles=None, grid=None, noise=None):
+    """mp_mppi_plan_sharded: S scenes split over the GPUs of a CommGroup (balanced blocks, Philox counter
+    word scene_base + block start) and one RCCL all-gather of the per-scene results.  Same shapes and
+    outputs as mppi_plan_batch without the TrajectoryCollection; equal to one mppi_plan_batch over all S
+    scenes."""
+    X0 = f64(X0).reshape(-1, 7)
+    S, K, H = X0.shape[0], p.K, p.H
+    goal = f64(goal, (S, 2))
+    U_nom = f64(U_nom, (S, H, 2))
+    obstacles = None if obstacles is None or p.n_obs == 0 else f64(obstacles, (S, p.n_obs, 3))
+    grid = None if grid is None or p.grid_nx == 0 else np.ascontiguousarray(grid, np.uint8).reshape(
+        S, p.grid_ny, p.grid_nx)
+    if noise is not None:
+        noise = f64(noise, (S, K, H, 2))
+        p.noise_mode = MP_NOISE_EXTERNAL
+    else:
+        p.noise_mode = MP_NOISE_PHILOX
+    out = dict(U=np.zeros((S, H, 2)), traj=np.zeros((S, H + 1, 7)), cost=np.zeros(S),
+               feasible=np.zeros(S, np.int32), rollout_count=np.zeros(S, np.int32),
+               feasible_count=np.zeros(S, np.int32))
+    st = group.lib.mp_mppi_plan_sharded(group.array, group.n, ctypes.byref(p), S, ptr(X0), ptr(goal), ptr(U_nom),
+                                        ptr(obstacles), ptr(grid), ptr(noise), ptr(out["U"]), ptr(out["traj"]),
+                                        ptr(out["cost"]), ptr(out["feasible"]), ptr(out["rollout_count"]),
+                                        ptr(out["feasible_count"]))
+    out["nan"] = st == MP_ERR_NUMERIC
+    if st != MP_ERR_NUMERIC:
+        group.check(st)
+    return out
+
+
 def MPPIPlan(mppi, noise=None, collect=True, ctx=None):
     """MPPIUtils.jl:169-203.  Mutates mppi.r and mppi.p.TrajectoryCollection.
 

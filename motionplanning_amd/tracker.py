@@ -58,9 +58,21 @@ def track_batch(searchers, ctx=None, settings=None, his_stride=0, his_cap=0):
     """Track every planned searcher's reference path from its starting_real (main_Tracker.jl:63-122).
 
     Needs `retrieve_batch` first (r.tol_length, r.interp_values).  Fills r.tracking =
-    dict(status, n_steps, states_his (rows, 3), final_state, err_accumulated, x_ref/y_ref/ψ_ref)."""
+    dict(status, n_steps, states_his (rows, 3), final_state, err_accumulated, x_ref/y_ref/ψ_ref).
+    Without `settings`, each searcher is tracked with its own vehicle length (veh_param[1] =
+    vehicle_size[1], main_Tracker.jl:50): the batch is split into one launch per distinct length."""
     ctx = ctx or default_context()
-    st = settings or settings_for(searchers[0])
+    if settings is not None:
+        return _track_group(searchers, ctx, settings, his_stride, his_cap)
+    groups = {}
+    for h in searchers:
+        groups.setdefault(float(h.s.vehicle_size[0]), []).append(h)
+    for hs in groups.values():
+        _track_group(hs, ctx, settings_for(hs[0]), his_stride, his_cap)
+    return searchers
+
+
+def _track_group(searchers, ctx, st, his_stride, his_cap):
     B = len(searchers)
     start = f64([h.s.starting_real for h in searchers])
     tol = np.array([h.r.tol_length if h.r.found and h.r.interp_values is not None else 0.0 for h in searchers])

@@ -31,8 +31,8 @@ def test_struct_sizes_match_header(tmp_path):
     """ctypes mirrors vs the C compiler's layout of include/mpgpu.h (sizeof + every offsetof)."""
     import subprocess
 
-    structs = {"mp_mppi_params": abi.MPPIParams, "mp_ilqr_params": abi.ILQRParams, "mp_ha_params": abi.HAParams,
-               "mp_track_params": abi.TrackParams}
+    structs = {"mp_mppi_params": abi.MPPIParams, "mp_mppi_loop_params": abi.MPPILoopParams,
+               "mp_ilqr_params": abi.ILQRParams, "mp_ha_params": abi.HAParams, "mp_track_params": abi.TrackParams}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/mpgpu.h"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

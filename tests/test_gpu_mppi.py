@@ -209,29 +209,29 @@ def test_jlmath_bitexact(ctx):
         assert np.array_equal(out.view(np.int64), cpu.view(np.int64)), (fn, names[fn], x[out.view(np.int64) != cpu.view(np.int64)][:5])
 
 
-def test_bench_workload_full_size_bitexact(ctx):
-    """The headline bench workload itself (bench.py run(): configs[4] per-GPU shard = 8 scenes x configs[1],
-    K=8192, H=50, occupancy grid, device Philox noise seeded 20260415, step offset 3, final rollout on
-    the side stream) vs 8 oracle MPPIPlan solves with the same Philox stream (threaded): every rollout's
-    cost, feasibility, controls and states bit for bit, MPPICtrl / final trajectory within the stated
-    tolerance."""
+@pytest.mark.parametrize("base", [0, 56])
+def test_bench_workload_full_size_bitexact(ctx, base):
+    """The headline bench workload itself (bench.py run(): configs[4] per-GPU shard = 8 of the 64 scenes,
+    each configs[1], K=8192, H=50, its own X0 and its own occupancy grid from obstacle_field.mat field g+1
+    (rank 0's fields 1-8 and rank 7's fields 57-64), device Philox noise seeded 20260415, step offset 3,
+    final rollout on the side stream) vs 8 oracle MPPIPlan solves with the same Philox stream (threaded):
+    every rollout's cost, feasibility, controls and states bit for bit, MPPICtrl / final trajectory within
+    the stated tolerance."""
     from concurrent.futures import ThreadPoolExecutor
 
     from motionplanning_amd.abi import MP_NOISE_PHILOX
 
     S = 8
-    c = configs.cfg2(noise_mode=MP_NOISE_PHILOX, seed=20260415)
+    c = configs.cfg5_shard(base, S, noise_mode=MP_NOISE_PHILOX, seed=20260415)
     p = c["params"]
     p.offset = 3
     p.final_stream = 1
-    X0 = np.tile(c["X0"], (S, 1))
-    X0[:, 1] = np.linspace(-0.5, 0.5, S)
-    goal = np.tile(c["goal"], (S, 1))
-    grid = np.tile(c["grid"], (S, 1, 1))
+    X0, goal, grid = c["X0"], c["goal"], c["grid"]
+    assert len({g.tobytes() for g in grid}) == S, "every scene has its own obstacle set"
     gpu = mppi_plan_batch(p, X0, goal, np.zeros((S, p.H, 2)), None, grid, None, collect=True, ctx=ctx)
 
     def ref(s):
-        return oracle.mppi_plan(p, X0[s], goal[s], np.zeros((p.H, 2)), None, c["grid"], None, scene=s, collect=True)
+        return oracle.mppi_plan(p, X0[s], goal[s], np.zeros((p.H, 2)), None, grid[s], None, scene=s, collect=True)
 
     with ThreadPoolExecutor(8) as ex:
         refs = list(ex.map(ref, range(S)))
@@ -265,3 +265,89 @@ def test_scene_batching_invariance(ctx):
         for key in ("cost", "feas", "ctrl", "traj"):
             assert np.array_equal(one["coll"][key][0], whole["coll"][key][s]), (s, key)
         assert np.array_equal(one["U"][0], whole["U"][s]) and one["cost"][0] == whole["cost"][s]
+
+
+def test_cfg2_default_feasibility_count_full_size(ctx):
+    """configs[1] at full size (K=8192, H=50, grid) with the reference's default FeasibilityCount = 1300
+    (types.jl:24, MPPIUtils.jl:175): the prefix stops at the 1301st feasible rollout, so only the first m
+    rollouts enter the weights and RolloutCount = m + 1 -- bit-exact collection, exact counts."""
+    c = configs.cfg2(feasibility_count=configs.FEASIBILITY_COUNT_REF)
+    p = c["params"]
+    assert p.feasibility_count == 1300
+    z = configs.standard_noise(p.K, p.H, seed=8)
+    gpu = mppi_plan_batch(p, c["X0"][None], c["goal"][None], c["unom"][None], None, c["grid"][None], z[None],
+                          collect=True, ctx=ctx)
+    ref = oracle.mppi_plan(p, c["X0"], c["goal"], c["unom"], None, c["grid"], z, collect=True)
+    assert ref["feasible_count"] == 1301 and ref["rollout_count"] - 1 < p.K, (ref["feasible_count"],
+                                                                             ref["rollout_count"])
+    _check_plan(gpu, ref)
+
+
+def test_sharded_plan_one_gpu_equals_plan(ctx):
+    """mp_comm_init + mp_mppi_plan_sharded over a one-GPU communicator (RCCL all-gather with one rank)
+    equals mp_mppi_plan of the same scenes bit for bit (U, final trajectory, cost, flags, counts).
+    n > 1 needs a multi-GPU box (not available to these tests)."""
+    from motionplanning_amd.context import CommGroup
+    from motionplanning_amd.mppi import mppi_plan_sharded
+
+    S = 3
+    c = configs.cfg5_shard(5, S, noise_mode=MP_NOISE_PHILOX, seed=31)
+    p = c["params"]
+    p.K = 2048
+    g = CommGroup([0])
+    try:
+        for fs in (0, 1):
+            p.final_stream = fs
+            sh = mppi_plan_sharded(g, p, c["X0"], c["goal"], c["unom"], None, c["grid"])
+            one = mppi_plan_batch(p, c["X0"], c["goal"], c["unom"], None, c["grid"], None, ctx=ctx)
+            for k in ("U", "traj", "cost", "feasible", "rollout_count", "feasible_count"):
+                assert np.array_equal(sh[k], one[k]), (fs, k)
+    finally:
+        g.close()
+
+
+def test_searcher_object_api(ctx):
+    """The drop-in searcher surface (MPPIUtils.jl:169-203, types.jl:3-8): MPPIPlan(mppi) mutates mppi.r
+    (Control, Traj, Feasibility, cost, RolloutCount, FeasibleTrajCount) and mppi.p.TrajectoryCollection[1:m];
+    TrajectoryRollout(mppi, ctrl) returns (states_his, ctrl, constraint, cost); MPPIClosedLoop(mppi) leaves
+    the last plan in mppi.r -- each checked field by field against the oracle on the same noise."""
+    from motionplanning_amd import mppi
+
+    m = mppi.reference_searcher(K=1500, N=20)
+    m.s.FeasibilityCount = 700  # a prefix that stops early: TrajectoryCollection has m < K holders
+    r = np.random.default_rng(4)
+    un = np.c_[r.uniform(-0.1, 0.1, 20), r.uniform(-0.5, 0.5, 20)]
+    mppi.defineMPPINominalControl_(m, un)
+    z = r.standard_normal((1500, 20, 2))
+    p = mppi.params_of(m, 0)
+    ref = oracle.mppi_plan(p, m.s.X0, m.s.goal, un, np.array(m.s.obstacle_list), None, z, collect=True)
+    assert mppi.MPPIPlan(m, noise=z, ctx=ctx) is None
+    mm = ref["rollout_count"] - 1
+    assert m.r.RolloutCount == ref["rollout_count"] and m.r.FeasibleTrajCount == ref["feasible_count"]
+    assert m.r.Feasibility == ("Feasible" if ref["feasible"] else "InFeasible")
+    np.testing.assert_allclose(m.r.Control, ref["U"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(m.r.Traj, ref["traj"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(m.r.cost, ref["cost"], rtol=1e-9)
+    assert len(m.p.TrajectoryCollection) == mm < 1500
+    for i in (0, 1, mm // 2, mm - 1):
+        h = m.p.TrajectoryCollection[i]
+        assert np.array_equal(h.Trajectory, ref["coll"]["traj"][i])
+        assert np.array_equal(h.Control, ref["coll"]["ctrl"][i])
+        assert h.Feasibility == bool(ref["coll"]["feas"][i]) and h.cost == ref["coll"]["cost"][i]
+    # TrajectoryRollout(mppi, ctrl) of one control list (MPPIUtils.jl:31-57): the collection's holder i
+    i = mm // 3
+    sh, cl, feas, cost = mppi.TrajectoryRollout(m, ref["coll"]["ctrl"][i], ctx=ctx)
+    assert np.array_equal(sh, ref["coll"]["traj"][i]) and np.array_equal(cl, ref["coll"]["ctrl"][i])
+    assert feas == bool(ref["coll"]["feas"][i]) and cost == ref["coll"]["cost"][i]
+    # MPPIClosedLoop(mppi): 0.3 s of main.jl's loop (3 replans) with given noise, last plan in mppi.r
+    m2 = mppi.reference_searcher(K=1500, N=20)
+    zz = r.standard_normal((3, 1500, 20, 2))
+    his = mppi.MPPIClosedLoop(m2, sim_time=0.3, noise=zz, ctx=ctx)
+    upd, hold = configs.mppi_hold_index(3.0, 20)
+    p2 = mppi.params_of(m2, 0)
+    o = oracle.mppi_closed_loop(p2, np.array(configs.X0_REF), np.array(configs.GOAL_REF), np.zeros((20, 2)), hold,
+                                upd, 300, 1e-3, 6.0, obstacles=np.array(configs.OBSTACLES_REF), noise=zz)
+    assert his.shape == (301, 8) and o["n_replans"] == 3
+    np.testing.assert_allclose(his, o["his"], rtol=0, atol=1e-9)
+    assert m2.r.RolloutCount == o["rollout_count"][-1]
+    np.testing.assert_allclose(m2.r.Control, m2.r.log["Control"][-1], rtol=0, atol=0)

@@ -116,3 +116,32 @@ def test_closed_loop_philox_reference_settings(ctx):
     assert int(g["n_rows"][0]) == 501 and int(g["n_replans"][0]) == 5
     np.testing.assert_allclose(g["his"][0], ref["his"], rtol=0, atol=1e-9)
     np.testing.assert_array_equal(g["rollout_count"][0], ref["rollout_count"])
+
+
+def test_closed_loop_final_rollout_of_the_stopping_replan(ctx):
+    """The final rollout of the replan whose period ends a scene runs from that plan's own snapshot (its
+    `ran` flag), not from the live flags the plant kernel clears on the context stream meanwhile: with one
+    plant step per replan (update_steps = 1) every stop happens in the first step of a period, and scene 0
+    starts inside the goal radius (it stops after plant step 1 of replan 0).  Every replan's MPPICtrl,
+    final trajectory, cost and Feasibility, the last one included, must match the oracle."""
+    S, K, H, upd, max_steps = 2, 256, 20, 1, 40
+    p = configs.mppi_params(K=K, H=H, T=3.0, n_obs=3)
+    X0 = np.tile(np.array(configs.X0_REF), (S, 1))
+    goal = np.array([[0.0, 0.0], [0.08, 0.0]])  # scene 1: ~10 steps of 5 mm to come within 0.05 m
+    obs = np.tile(np.array(configs.OBSTACLES_REF), (S, 1, 1))
+    hold = np.zeros(upd, np.int32)
+    z = np.random.default_rng(9).standard_normal((max_steps, S, K, H, 2))
+    U0 = np.zeros((S, H, 2))
+    for poll in (0, 1):
+        g = mppi_closed_loop_batch(p, X0, goal, U0, hold, upd, max_steps, 1e-3, 0.05, obs, None, z, poll_every=poll)
+        assert list(g["n_replans"]) == list(g["n_rows"] - 1)
+        assert int(g["n_replans"][0]) == 1 and 3 < int(g["n_replans"][1]) < max_steps
+        for s in range(S):
+            for r in range(int(g["n_replans"][s])):
+                x0 = g["his"][s, r, 1:]
+                un = U0[s] if r == 0 else g["U"][s, r - 1]
+                ref = oracle.mppi_plan(p, x0, goal[s], un, obs[s], None, z[r, s])
+                np.testing.assert_allclose(g["U"][s, r], ref["U"], rtol=1e-9, atol=1e-12)
+                np.testing.assert_allclose(g["cost"][s, r], ref["cost"], rtol=1e-9)
+                np.testing.assert_allclose(g["traj"][s, r], ref["traj"], rtol=1e-9, atol=1e-9)
+                assert bool(g["feasible"][s, r]) == ref["feasible"], (poll, s, r)
