@@ -18,8 +18,8 @@
  * other operation is a separately rounded IEEE op; no contraction is allowed
  * anywhere else (both builds pass -ffp-contract=off).
  *
- * `exp` and `log` are FDLIBM's e_exp.c / e_log.c (Julia >= 1.6 uses a
- * table-driven exp; results agree to <= 1 ulp, not bit-for-bit).
+ * `exp` is Julia's own table-driven exp (base/special/exp.jl); `log` (only the
+ * Box–Muller of the synthetic Philox noise, not a reference path) is FDLIBM's e_log.c.
  *
  * Accuracy vs glibc is checked in tests/test_jlmath.py (CPU) and the GPU
  * implementation is checked bit-exact against the CPU one in
@@ -473,8 +473,111 @@ MPJ_FN double mpj_acos(double x) {
 }
 
 /* -------------------------------------------------------------- exp / log */
-/* FDLIBM e_exp.c */
+/* Julia >= 1.6 `exp(::Float64)` (base/special/exp.jl, exp_impl with base e): reduction
+ * N = round(x * 256/ln2) by the 1.5*2^52 shift (muladd), r = x - N*ln2/256 in two fused steps
+ * (Cody-Waite hi/lo), 2^(j/256) from the packed 256-entry table (hi part jU rounded down,
+ * lo part jL from 12 packed bits; tools/gen_jl_exp_table.py regenerates it), expm1 on
+ * |r| <= ln2/512 by the degree-4 minimax polynomial (evalpoly = nested muladd), and the result
+ * 2^k * (jU + jU*p(r) + jL) assembled by an integer add into the exponent field.  Julia JITs
+ * `muladd` to a fused multiply-add on FMA hardware (every x86-64 since Haswell, and gfx950),
+ * so every muladd is mpj_fma here.  Max error ~0.52 ulp (tests/test_jlmath.py). */
+static const uint64_t mpj_exp_jtab[256] = {
+    0x0000000000000000ull, 0xaac00b1afa5abcbeull, 0x9b60163da9fb3335ull, 0xab502168143b0280ull,
+    0xadc02c9a3e778060ull, 0x656037d42e11bbccull, 0xa7a04315e86e7f84ull, 0x84c04e5f72f654b1ull,
+    0x8d7059b0d3158574ull, 0xa510650a0e3c1f88ull, 0xa8d0706b29ddf6ddull, 0x83207bd42b72a836ull,
+    0x6180874518759bc8ull, 0xa4b092bdf66607dfull, 0x91409e3ecac6f383ull, 0x85d0a9c79b1f3919ull,
+    0x98a0b5586cf9890full, 0x94f0c0f145e46c85ull, 0x9010cc922b7247f7ull, 0xa210d83b23395debull,
+    0x4030e3ec32d3d1a2ull, 0xa5b0efa55fdfa9c4ull, 0xae40fb66affed31aull, 0x8d41073028d7233eull,
+    0xa4911301d0125b50ull, 0xa1a11edbab5e2ab5ull, 0xaf712abdc06c31cbull, 0xae8136a814f204aaull,
+    0xa661429aaea92ddfull, 0xa9114e95934f312dull, 0x82415a98c8a58e51ull, 0x58f166a45471c3c2ull,
+    0xab9172b83c7d517aull, 0x70917ed48695bbc0ull, 0xa7718af9388c8de9ull, 0x94a1972658375d2full,
+    0x8e51a35beb6fcb75ull, 0x97b1af99f8138a1cull, 0xa351bbe084045cd3ull, 0x9001c82f95281c6bull,
+    0x9e01d4873168b9aaull, 0xa481e0e75eb44026ull, 0xa711ed5022fcd91cull, 0xa201f9c18438ce4cull,
+    0x8dc2063b88628cd6ull, 0x935212be3578a819ull, 0x82a21f49917ddc96ull, 0x8d322bdda27912d1ull,
+    0x99b2387a6e756238ull, 0x8ac2451ffb82140aull, 0x8ac251ce4fb2a63full, 0x93e25e85711ece75ull,
+    0x82b26b4565e27cddull, 0x9e02780e341ddf29ull, 0xa2d284dfe1f56380ull, 0xab4291ba7591bb6full,
+    0x86129e9df51fdee1ull, 0xa352ab8a66d10f12ull, 0xafb2b87fd0dad98full, 0xa572c57e39771b2eull,
+    0x9002d285a6e4030bull, 0x9d12df961f641589ull, 0x71c2ecafa93e2f56ull, 0xaea2f9d24abd886aull,
+    0x86f306fe0a31b715ull, 0x89531432edeeb2fdull, 0x8a932170fc4cd831ull, 0xa1d32eb83ba8ea31ull,
+    0x93233c08b26416ffull, 0xab23496266e3fa2cull, 0xa92356c55f929ff0ull, 0xa8f36431a2de883aull,
+    0xa4e371a7373aa9caull, 0xa3037f26231e7549ull, 0xa0b38cae6d05d865ull, 0xa3239a401b7140eeull,
+    0xad43a7db34e59ff6ull, 0x9543b57fbfec6cf4ull, 0xa083c32dc313a8e4ull, 0x7fe3d0e544ede173ull,
+    0x8ad3dea64c123422ull, 0xa943ec70df1c5174ull, 0xa413fa4504ac801bull, 0x8bd40822c367a024ull,
+    0xaf04160a21f72e29ull, 0xa3d423fb27094689ull, 0xab8431f5d950a896ull, 0x88843ffa3f84b9d4ull,
+    0x48944e086061892dull, 0xae745c2042a7d231ull, 0x9c946a41ed1d0057ull, 0xa1e4786d668b3236ull,
+    0x73c486a2b5c13cd0ull, 0xab1494e1e192aed1ull, 0x99c4a32af0d7d3deull, 0xabb4b17dea6db7d6ull,
+    0x7d44bfdad5362a27ull, 0x9054ce41b817c114ull, 0x98e4dcb299fddd0dull, 0xa564eb2d81d8abfeull,
+    0xa5a4f9b2769d2ca6ull, 0x7a2508417f4531eeull, 0xa82516daa2cf6641ull, 0xac65257de83f4eeeull,
+    0xabe5342b569d4f81ull, 0x879542e2f4f6ad27ull, 0xa8a551a4ca5d920eull, 0xa7856070dde910d1ull,
+    0x99b56f4736b527daull, 0xa7a57e27dbe2c4ceull, 0x82958d12d497c7fdull, 0xa4059c0827ff07cbull,
+    0x9635ab07dd485429ull, 0xa245ba11fba87a02ull, 0x3c45c9268a5946b7ull, 0xa195d84590998b92ull,
+    0x9ba5e76f15ad2148ull, 0xa985f6a320dceb70ull, 0xa60605e1b976dc08ull, 0x9e46152ae6cdf6f4ull,
+    0xa636247eb03a5584ull, 0x984633dd1d1929fdull, 0xa8e6434634ccc31full, 0xa28652b9febc8fb6ull,
+    0xa226623882552224ull, 0xa85671c1c70833f5ull, 0x60368155d44ca973ull, 0x880690f4b19e9538ull,
+    0xa216a09e667f3bccull, 0x7a36b052fa75173eull, 0xada6c012750bdabeull, 0x9c76cfdcddd47645ull,
+    0xae46dfb23c651a2eull, 0xa7a6ef9298593ae4ull, 0xa9f6ff7df9519483ull, 0x59d70f7466f42e87ull,
+    0xaba71f75e8ec5f73ull, 0xa6f72f8286ead089ull, 0xa7a73f9a48a58173ull, 0x90474fbd35d7cbfdull,
+    0xa7e75feb564267c8ull, 0x9b777024b1ab6e09ull, 0x986780694fde5d3full, 0x934790b938ac1cf6ull,
+    0xaaf7a11473eb0186ull, 0xa207b17b0976cfdaull, 0x9f17c1ed0130c132ull, 0x91b7d26a62ff86f0ull,
+    0x7057e2f336cf4e62ull, 0xabe7f3878491c490ull, 0xa6c80427543e1a11ull, 0x946814d2add106d9ull,
+    0xa1582589994cce12ull, 0x9998364c1eb941f7ull, 0xa9c8471a4623c7acull, 0xaf2857f4179f5b20ull,
+    0xa01868d99b4492ecull, 0x85d879cad931a436ull, 0x99988ac7d98a6699ull, 0x9d589bd0a478580full,
+    0x96e8ace5422aa0dbull, 0x9ec8be05bad61778ull, 0xade8cf3216b5448bull, 0xa478e06a5e0866d8ull,
+    0x85c8f1ae99157736ull, 0x959902fed0282c8aull, 0xa119145b0b91ffc5ull, 0xab2925c353aa2fe1ull,
+    0xae893737b0cdc5e4ull, 0xa88948b82b5f98e4ull, 0xad395a44cbc8520eull, 0xaf296bdd9a7670b2ull,
+    0xa1797d829fde4e4full, 0x7ca98f33e47a22a2ull, 0xa749a0f170ca07b9ull, 0xa119b2bb4d53fe0cull,
+    0x7c79c49182a3f090ull, 0xa579d674194bb8d4ull, 0x7829e86319e32323ull, 0xaad9fa5e8d07f29dull,
+    0xa65a0c667b5de564ull, 0x9c6a1e7aed8eb8bbull, 0x963a309bec4a2d33ull, 0xa2aa42c980460ad7ull,
+    0xa16a5503b23e255cull, 0x650a674a8af46052ull, 0x9bca799e1330b358ull, 0xa58a8bfe53c12e58ull,
+    0x90fa9e6b5579fdbfull, 0x889ab0e521356ebaull, 0xa81ac36bbfd3f379ull, 0x97ead5ff3a3c2774ull,
+    0x97aae89f995ad3adull, 0xa5aafb4ce622f2feull, 0xa21b0e07298db665ull, 0x94db20ce6c9a8952ull,
+    0xaedb33a2b84f15faull, 0xac1b468415b749b0ull, 0xa1cb59728de55939ull, 0x92ab6c6e29f1c52aull,
+    0xad5b7f76f2fb5e46ull, 0xa24b928cf22749e3ull, 0xa08ba5b030a10649ull, 0xafcbb8e0b79a6f1eull,
+    0x823bcc1e904bc1d2ull, 0xafcbdf69c3f3a206ull, 0xa08bf2c25bd71e08ull, 0xa89c06286141b33cull,
+    0x811c199bdd85529cull, 0xa48c2d1cd9fa652bull, 0x9b4c40ab5fffd07aull, 0x912c544778fafb22ull,
+    0x928c67f12e57d14bull, 0xa86c7ba88988c932ull, 0x71ac8f6d9406e7b5ull, 0xaa0ca3405751c4daull,
+    0x750cb720dcef9069ull, 0xac5ccb0f2e6d1674ull, 0xa88cdf0b555dc3f9ull, 0xa2fcf3155b5bab73ull,
+    0xa1ad072d4a07897bull, 0x955d1b532b08c968ull, 0xa15d2f87080d89f1ull, 0x93dd43c8eacaa1d6ull,
+    0x82ed5818dcfba487ull, 0x5fed6c76e862e6d3ull, 0xa77d80e316c98397ull, 0x9a0d955d71ff6075ull,
+    0x9c2da9e603db3285ull, 0xa24dbe7cd63a8314ull, 0x92ddd321f301b460ull, 0xa1ade7d5641c0657ull,
+    0xa72dfc97337b9b5eull, 0xadae11676b197d16ull, 0xa42e264614f5a128ull, 0xa30e3b333b16ee11ull,
+    0x839e502ee78b3ff6ull, 0xaa7e653924676d75ull, 0x92de7a51fbc74c83ull, 0xa77e8f7977cdb73full,
+    0xa0bea4afa2a490d9ull, 0x948eb9f4867cca6eull, 0xa1becf482d8e67f0ull, 0x91cee4aaa2188510ull,
+    0x9dcefa1bee615a27ull, 0xa66f0f9c1cb64129ull, 0x93af252b376bba97ull, 0xacdf3ac948dd7273ull,
+    0x99df50765b6e4540ull, 0x9faf6632798844f8ull, 0xa12f7bfdad9cbe13ull, 0xaeef91d802243c88ull,
+    0x874fa7c1819e90d8ull, 0xacdfbdba3692d513ull, 0x62efd3c22b8f71f1ull, 0x74afe9d96b2a23d9ull};
 MPJ_FN double mpj_exp(double x) {
+  const double magic = 6.755399441055744e15; /* 1.5 * 2^52 */
+  double nf = mpj_fma(x, 369.3299304675746, magic);
+  mpj_du nb; nb.d = nf;
+  const int32_t n = (int32_t)(uint32_t)nb.u;
+  nf = nf - magic;
+  double r = mpj_fma(nf, -0.002707606173999011, x);
+  r = mpj_fma(nf, -6.327543041662719e-14, r);
+  const int32_t k = n >> 8;
+  const uint64_t j = mpj_exp_jtab[n & 255];
+  mpj_du ju, jl;
+  ju.u = 0x3FF0000000000000ull | (j & 0x000FFFFFFFFFFFFFull);
+  jl.u = 0x3C00000000000000ull | (j >> 8);
+  const double p = mpj_fma(r, mpj_fma(r, mpj_fma(r, 0.04166666857598777, 0.1666666857598779), 0.4999999999999997),
+                           0.9999999999999912);
+  mpj_du sp;
+  sp.d = mpj_fma(ju.d, r * p, jl.d) + ju.d;
+  if (!(__builtin_fabs(x) <= 708.3964185322641)) {
+    if (x != x) return x;
+    if (x >= 709.782712893384) return __builtin_inf();
+    if (x <= -745.1332191019412) return 0.0;
+    if (k <= -53) {
+      mpj_du o; o.u = ((uint64_t)(int64_t)(k + 53) << 52) + sp.u;
+      return o.d * 1.1102230246251565e-16; /* 0x1p-53 */
+    }
+  }
+  mpj_du o; o.u = ((uint64_t)(int64_t)k << 52) + sp.u; /* Int64(k) << 52, wrapping add */
+  return o.d;
+}
+
+/* FDLIBM e_exp.c (the round-1/2 exp; kept for tools/ilqr_ulp_sources.py and the accuracy tests) */
+MPJ_FN double mpj_exp_fdlibm(double x) {
   const double o_threshold = 7.09782712893383973096e+02, u_threshold = -7.45133219101941108420e+02,
                ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
                invln2 = 1.44269504088896338700e+00,
@@ -877,42 +980,6 @@ MPJ_FN double mpj_log_bl(double x) {
   return MPJ_SEL(i > 0, rp, rn);
 }
 
-/* exp for 2^-28 <= |x| < 704 as one basic block (FDLIBM e_exp.c with every branch a select):
- * the |x| < 1.5 ln2 reduction (hi = x ∓ ln2HI, lo = ±ln2LO, k = ±1) is the general one with
- * t = k = ±1 (x - (-1)·ln2HI == x + ln2HI exactly), and (x·c)/(c-2) == -((x·c)/(2-c)) exactly,
- * so one division serves both the k == 0 and the k != 0 result.  Other arguments (incl. NaN,
- * Inf, overflow/underflow, k <= -1022) take mpj_exp through a wave-uniform branch. */
-MPJ_FN double mpj_exp_fast(double x, int* bad) {
-  const double ln2HI = 6.93147180369123816490e-01, ln2LO = 1.90821492927058770002e-10,
-               invln2 = 1.44269504088896338700e+00,
-               P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03,
-               P3 = 6.61375632143793436117e-05, P4 = -1.65339022054652515390e-06,
-               P5 = 4.13813679705723846039e-08;
-  const uint32_t hx0 = mpj_hi(x);
-  const uint32_t hx = hx0 & 0x7fffffffu;
-  *bad |= hx < 0x3e300000u || hx >= 0x40860000u;
-  const int xsb = (int)(hx0 >> 31);
-  const int red = hx > 0x3fd62e42u;
-  const int kfar = (int)(invln2 * MPJ_SEL(hx >= 0x40860000u, 0.0, x) + (xsb ? -0.5 : 0.5)); /* no UB on bad lanes */
-  const int k = red ? (hx < 0x3FF0A2B2u ? 1 - xsb - xsb : kfar) : 0;
-  const double t = (double)k;
-  const double hi = x - t * ln2HI, lo = t * ln2LO;
-  const double xr = MPJ_SEL(red, hi - lo, x);
-  const double tt = xr * xr;
-  const double c = xr - tt * mpj_fma(tt, mpj_fma(tt, mpj_fma(tt, mpj_fma(tt, P5, P4), P3), P2), P1);
-  const double q = (xr * c) / (2.0 - c);
-  const double r0 = 1.0 - ((-q) - xr);
-  const double y = 1.0 - ((lo - q) - hi);
-  const double twopk = mpj_from_words(0x3ff00000u + ((uint32_t)k << 20), 0);
-  return MPJ_SEL(k == 0, r0, y * twopk);
-}
-MPJ_FN double mpj_exp_bl(double x) {
-  const uint32_t hx = mpj_hi(x) & 0x7fffffffu;
-  if (MPJ_ANY(hx < 0x3e300000u || hx >= 0x40860000u)) return mpj_exp(x);
-  int bad = 0;
-  return mpj_exp_fast(x, &bad);
-}
-
 /* tan for |x| <= π/4 as one basic block (FDLIBM k_tan.c with iy = 1, both the |x| < 0.6744
  * and the reflected |x| >= 0.6744 forms, selected); larger |x|, NaN and Inf take mpj_tan. */
 MPJ_FN double mpj_tan_fast(double x, int* bad) {
@@ -1094,6 +1161,205 @@ MPJ_FN int mpj_isless(double a, double b) {
   if (a < b) return 1;
   if (a == b) return (mpj_hi(a) >> 31) > (mpj_hi(b) >> 31);
   return 0;
+}
+
+/* ------------------------------------------------ LinearAlgebra.pinv (2x2) */
+/* Julia's `pinv(A::Matrix{Float64})` (stdlib LinearAlgebra dense.jl) for a 2x2 A, the path both
+ * `pinv(Quu)` (ILQR.jl:61,63) and cubic_fit's `pinv(A)` (hybrid_astar_utils.jl:107-109) take:
+ *   isdiag(A)  -> B = diag(abs(x) > tol ? inv(x) : 0), tol = 2eps * max|diag|, off-diagonal +0.0;
+ *   otherwise  -> svd(A) = LAPACK dgesdd(JOBZ='S'), tol = 2eps * max(S), Sinv = S > tol ? inv(S) : 0,
+ *                 pinv = Vt' * (Diagonal(Sinv) * U')  (matmul2x2!: a*b + c*d, no FMA).
+ * dgesdd on a 2x2 (M < MNTHR = 3) is its path 5: dgebd2 (one Householder reflector H1 from dlarfg
+ * on column 1, applied to column 2 by dlarf; the row and last-column reflectors are identities,
+ * n = 1), dbdsdc -> dlasdq -> dbdsqr on the 2x2 upper bidiagonal [d1 e1; 0 d2] (split when
+ * |e1| <= thresh, otherwise one dlasv2 and two drot on the identity), singular values made
+ * non-negative and sorted decreasing, then dormbr applies H1 to U.  The BLAS level-1/2 calls inside
+ * (dgemv, dger) round as the OpenBLAS kernels do: dgemv's w = C(1,j)*1 + C(2,j)*v2 rounds the
+ * product and the sum separately, dger's C(2,j) += (-tau*w_j)*v2 is one fused multiply-add.
+ * Pinned bit for bit against numpy's gesdd (OpenBLAS 0.3.29) on >= 1e5 random, near-singular,
+ * triangular, orthogonal-column and scaled 2x2 matrices (tests/test_jlmath.py).
+ * Domain: max|A_ij| in [6.7e-139, 1.5e138] or A == 0 (dgesdd rescales outside it; not restated),
+ * finite entries (Julia's svd throws on NaN/Inf). */
+MPJ_FN double mpj_fsign(double a, double b) { return __builtin_copysign(__builtin_fabs(a), b); } /* Fortran SIGN */
+
+/* LAPACK DLASV2: SVD of the upper triangular [f g; 0 h]. */
+MPJ_FN void mpj_lasv2(double f, double g, double h, double* ssmin, double* ssmax, double* snr, double* csr,
+                      double* snl, double* csl) {
+  const double eps = 1.1102230246251565e-16; /* DLAMCH('EPS') */
+  double ft = f, fa = __builtin_fabs(f), ht = h, ha = __builtin_fabs(h);
+  int pmax = 1;
+  const int swap = ha > fa;
+  if (swap) {
+    pmax = 3;
+    double t = ft; ft = ht; ht = t;
+    t = fa; fa = ha; ha = t;
+  }
+  const double gt = g, ga = __builtin_fabs(g);
+  double clt, crt, slt, srt, smin, smax;
+  if (ga == 0.0) {
+    smin = ha; smax = fa; clt = 1.0; crt = 1.0; slt = 0.0; srt = 0.0;
+  } else {
+    int gasmal = 1;
+    if (ga > fa) {
+      pmax = 2;
+      if (fa / ga < eps) {
+        gasmal = 0;
+        smax = ga;
+        smin = ha > 1.0 ? fa / (ga / ha) : (fa / ga) * ha;
+        clt = 1.0; slt = ht / gt; srt = 1.0; crt = ft / gt;
+      }
+    }
+    if (gasmal) {
+      const double d = fa - ha;
+      double l = d == fa ? 1.0 : d / fa;
+      const double m = gt / ft;
+      double t = 2.0 - l;
+      const double mm = m * m, tt = t * t;
+      const double s = mpj_sqrt(tt + mm);
+      const double r = l == 0.0 ? __builtin_fabs(m) : mpj_sqrt(l * l + mm);
+      const double a = 0.5 * (s + r);
+      smin = ha / a;
+      smax = fa * a;
+      if (mm == 0.0) {
+        if (l == 0.0) t = mpj_fsign(2.0, ft) * mpj_fsign(1.0, gt);
+        else t = gt / mpj_fsign(d, ft) + m / t;
+      } else {
+        t = (m / (s + t) + m / (r + l)) * (1.0 + a);
+      }
+      l = mpj_sqrt(t * t + 4.0);
+      crt = 2.0 / l;
+      srt = t / l;
+      clt = (crt + srt * m) / a;
+      slt = (ht / ft) * srt / a;
+    }
+  }
+  if (swap) { *csl = srt; *snl = crt; *csr = slt; *snr = clt; }
+  else { *csl = clt; *snl = slt; *csr = crt; *snr = srt; }
+  double tsign;
+  if (pmax == 1) tsign = mpj_fsign(1.0, *csr) * mpj_fsign(1.0, *csl) * mpj_fsign(1.0, f);
+  else if (pmax == 2) tsign = mpj_fsign(1.0, *snr) * mpj_fsign(1.0, *csl) * mpj_fsign(1.0, g);
+  else tsign = mpj_fsign(1.0, *snr) * mpj_fsign(1.0, *snl) * mpj_fsign(1.0, h);
+  *ssmax = mpj_fsign(smax, tsign);
+  *ssmin = mpj_fsign(smin, tsign * mpj_fsign(1.0, f) * mpj_fsign(1.0, h));
+}
+
+/* dlarf('Left') of H = I - tau [1; v2][1 v2] on one column [c1; c2] already known to be inside
+ * dlarf's iladlc range: lastv = 1 when v2 == 0 (row 2 untouched), else w = c1*1 + c2*v2
+ * (dgemv('T'), separately rounded), c1 += (-tau*w)*1, c2 = fma(-tau*w, v2, c2) (dger). */
+MPJ_FN void mpj_larf2(double tau, double v2, double* c1, double* c2) {
+  if (v2 != 0.0) {
+    const double tw = -tau * (*c1 + *c2 * v2);
+    *c1 = *c1 + tw;
+    *c2 = mpj_fma(tw, v2, *c2);
+  } else {
+    *c1 = *c1 + (-tau * *c1);
+  }
+}
+
+/* svd(A) of a row-major 2x2 through dgesdd path 5 (above): U, VT row-major, S decreasing. */
+MPJ_FN void mpj_svd2(const double* A, double* U, double* S, double* VT) {
+  const double a11 = A[0], a12 = A[1], a21 = A[2], a22 = A[3];
+  /* dgebd2, i = 1: dlarfg(2, a11, a21) -> beta, tau, v = [1, v2]; dlarf('L') on column 2 */
+  double tau = 0.0, v2 = 0.0, d1 = a11, e1 = a12, d2 = a22;
+  const double xnorm = __builtin_fabs(a21); /* dnrm2 of one entry */
+  if (xnorm != 0.0) {
+    const double aa = __builtin_fabs(a11);
+    const double w = aa > xnorm ? aa : xnorm, z = aa > xnorm ? xnorm : aa; /* dlapy2 */
+    const double q = z / w;
+    const double py = z == 0.0 ? w : w * mpj_sqrt(1.0 + q * q);
+    const double beta = -mpj_fsign(py, a11);
+    tau = (beta - a11) / beta;
+    v2 = a21 * (1.0 / (a11 - beta));
+    d1 = beta;
+    if (a12 != 0.0 || (v2 != 0.0 && a22 != 0.0)) mpj_larf2(tau, v2, &e1, &d2); /* column 2 (iladlc) */
+  }
+  /* dbdsqr on [d1 e1; 0 d2] with VT = U = I */
+  double vt[4] = {1.0, 0.0, 0.0, 1.0}, ub[4] = {1.0, 0.0, 0.0, 1.0}, d[2];
+  const double unfl = 2.2250738585072014e-308, tol = 1.0958066990042004e-14; /* TOLMUL*EPS, TOLMUL = EPS^(-1/8) */
+  double sminoa = __builtin_fabs(d1);
+  if (sminoa != 0.0) {
+    const double mu = __builtin_fabs(d2) * (sminoa / (sminoa + __builtin_fabs(e1)));
+    sminoa = mu < sminoa ? mu : sminoa;
+  }
+  sminoa = sminoa / 1.4142135623730951;
+  const double th0 = tol * sminoa, th1 = 6.0 * (2.0 * (2.0 * unfl));
+  const double thresh = th0 > th1 ? th0 : th1;
+  if (__builtin_fabs(e1) <= thresh) {
+    d[0] = d1; d[1] = d2;
+  } else {
+    double smin, smax, snr, csr, snl, csl;
+    mpj_lasv2(d1, e1, d2, &smin, &smax, &snr, &csr, &snl, &csl);
+    d[0] = smax; d[1] = smin;
+    /* drot(VT rows 1, 2; csr, snr) and drot(U columns 1, 2; csl, snl) on the identity */
+    for (int c = 0; c < 2; c++) {
+      const double x = vt[c], y = vt[2 + c];
+      vt[c] = csr * x + snr * y;
+      vt[2 + c] = csr * y - snr * x;
+    }
+    for (int r = 0; r < 2; r++) {
+      const double x = ub[2 * r], y = ub[2 * r + 1];
+      ub[2 * r] = csl * x + snl * y;
+      ub[2 * r + 1] = csl * y - snl * x;
+    }
+  }
+  for (int i = 0; i < 2; i++)
+    if (d[i] < 0.0) {
+      d[i] = -d[i];
+      vt[2 * i] = vt[2 * i] * -1.0;
+      vt[2 * i + 1] = vt[2 * i + 1] * -1.0;
+    }
+  if (!(d[1] <= d[0])) { /* sort decreasing (ties keep the order) */
+    double t = d[0]; d[0] = d[1]; d[1] = t;
+    t = vt[0]; vt[0] = vt[2]; vt[2] = t;
+    t = vt[1]; vt[1] = vt[3]; vt[3] = t;
+    t = ub[0]; ub[0] = ub[1]; ub[1] = t;
+    t = ub[2]; ub[2] = ub[3]; ub[3] = t;
+  }
+  /* dormbr('Q','L','N'): U = H1 * Ub (dorm2r -> dlarf on both columns) */
+  for (int i = 0; i < 4; i++) U[i] = ub[i];
+  if (tau != 0.0) {
+    const int lastv = v2 != 0.0 ? 2 : 1;
+    /* iladlc: the last column with a non-zero in rows 1..lastv; columns past it are untouched */
+    const int nz1 = U[1] != 0.0 || (lastv == 2 && U[3] != 0.0);
+    const int nz0 = U[0] != 0.0 || (lastv == 2 && U[2] != 0.0);
+    const int lastc = nz1 ? 2 : (nz0 ? 1 : 0);
+    for (int j = 0; j < lastc; j++) mpj_larf2(tau, v2, &U[j], &U[2 + j]);
+  }
+  S[0] = d[0]; S[1] = d[1];
+  for (int i = 0; i < 4; i++) VT[i] = vt[i];
+}
+
+/* Julia `pinv(x::Number)`: inv(x) when finite, else zero. */
+MPJ_FN double mpj_pinv_scalar(double x) {
+  const double xi = 1.0 / x;
+  return (xi - xi == 0.0) ? xi : 0.0;
+}
+
+/* pinv(M) for a row-major 2x2 (see the block comment above); P row-major. */
+MPJ_FN void mpj_pinv2(const double* M, double* P) {
+  const double rtol = 4.440892098500626e-16; /* eps(Float64) * min(size(A)...) */
+  if (M[1] == 0.0 && M[2] == 0.0) { /* isdiag */
+    const double a0 = __builtin_fabs(M[0]), a3 = __builtin_fabs(M[3]);
+    const double mx = a3 > a0 ? a3 : a0; /* maximum(abs, dA) */
+    const double tol = rtol * mx;
+    P[0] = a0 > tol ? mpj_pinv_scalar(M[0]) : 0.0;
+    P[3] = a3 > tol ? mpj_pinv_scalar(M[3]) : 0.0;
+    P[1] = 0.0;
+    P[2] = 0.0;
+    return;
+  }
+  double U[4], S[2], VT[4];
+  mpj_svd2(M, U, S, VT);
+  const double tol = rtol * S[0]; /* maximum(S): S is sorted decreasing */
+  const double i0 = S[0] > tol ? mpj_pinv_scalar(S[0]) : 0.0;
+  const double i1 = S[1] > tol ? mpj_pinv_scalar(S[1]) : 0.0;
+  /* D = Diagonal(Sinv) * U':  D[k][j] = Sinv[k] * U[j][k] */
+  const double D00 = i0 * U[0], D01 = i0 * U[2], D10 = i1 * U[1], D11 = i1 * U[3];
+  /* Vt' * D (matmul2x2!, tA = 'T'): P[i][j] = VT[0][i]*D[0][j] + VT[1][i]*D[1][j] */
+  P[0] = VT[0] * D00 + VT[2] * D10;
+  P[1] = VT[0] * D01 + VT[2] * D11;
+  P[2] = VT[1] * D00 + VT[3] * D10;
+  P[3] = VT[1] * D01 + VT[3] * D11;
 }
 
 #endif /* MP_JLMATH_H */

@@ -420,7 +420,7 @@ int mp_ha_track(mp_ctx* ctx, const mp_track_params* p, int32_t B, const double* 
  * (bit-exactness check against the CPU build).  fn: 0 sin, 1 cos, 2 tan, 3 atan,
  * 4 atan2(x, y), 5 asin, 6 acos, 7 exp, 8 log, 9 modpi, 10 sqrt; the branch-free
  * variants of the hot kernels: 11 modpi_bl, 12 atan_bl, 13 atan_tab, 14 sin (sincos_bl),
- * 15 cos (sincos_bl), 16 exp_bl, 17 tan_bl, 18 atan2_sel(x, y), 19 sin / 20 cos (sincos_wide),
+ * 15 cos (sincos_bl), 16 exp_fdlibm, 17 tan_bl, 18 atan2_sel(x, y), 19 sin / 20 cos (sincos_wide),
  * 21 tan_wide, 22 sin_34 (tyre sin, |x| <= 3π/4 fast path), 23 log_bl — each must equal its exact
  * routine bit for bit. */
 int mp_math_eval(mp_ctx* ctx, int32_t fn, int64_t n, const double* x, const double* y, double* out);

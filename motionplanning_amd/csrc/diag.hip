@@ -29,7 +29,7 @@ __global__ void math_kernel(int fn, long long n, const double* x, const double* 
     case 13: r = mpj_atan_tab(a, atab); break;
     case 14: { double s, c; mpj_sincos_bl(a, &s, &c); r = s; break; }
     case 15: { double s, c; mpj_sincos_bl(a, &s, &c); r = c; break; }
-    case 16: r = mpj_exp_bl(a); break;
+    case 16: r = mpj_exp_fdlibm(a); break;
     case 17: r = mpj_tan_bl(a); break;
     case 18: r = mpj_atan2_sel(a, y[i]); break;
     case 19: { double s, c; int b = 0; mpj_sincos_wide(a, &s, &c, &b); r = b ? mpj_sin(a) : s; break; }

@@ -1273,26 +1273,15 @@ constexpr int RSAMP = 50;  // steps of retrievePath (:167)
 constexpr int RT = 256;
 
 // cubic_fit's coefficients (:101-111): [xg³ xg²; 3xg² 2xg] \ (pinv) [yg; tan ψg] in the frame of `cur`.
-// pinv through the closed-form 2x2 SVD of the iLQR sweep (oracle/or_ilqr.c or_pinv2).
+// pinv: Julia's LinearAlgebra.pinv through LAPACK dgesdd's 2x2 path (mp_jlmath.h mpj_pinv2).
 __device__ __forceinline__ void cubic_params(const double* cur, const double* nxt, double* out) {
   double ns[3];
   change_basis(cur, nxt, 1.0, ns);
   const double xg = ns[0], yg = ns[1], pg = ns[2];
   const double M[4] = {xg * xg * xg, xg * xg, 3 * (xg * xg), 2 * xg};
-  const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
-  const double Q = mpj_sqrt(E * E + H * H), R = mpj_sqrt(F * F + G * G);
-  const double sx = Q + R, sy = Q - R;
-  const double a1 = mpj_atan2(G, F), a2 = mpj_atan2(H, E);
-  const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
-  double st, ct, sp, cp;
-  mpj_sincos(th, &st, &ct);
-  mpj_sincos(ph, &sp, &cp);
-  const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
-  const double tol = 4.440892098500626e-16 * smax;
-  const double i1 = __builtin_fabs(sx) > tol ? 1.0 / sx : 0.0;
-  const double i2 = __builtin_fabs(sy) > tol ? 1.0 / sy : 0.0;
-  const double P0 = ct * i1 * cp - st * i2 * sp, P1 = ct * i1 * sp + st * i2 * cp;
-  const double P2 = -st * i1 * cp - ct * i2 * sp, P3 = -st * i1 * sp + ct * i2 * cp;
+  double Pm[4];
+  mpj_pinv2(M, Pm);
+  const double P0 = Pm[0], P1 = Pm[1], P2 = Pm[2], P3 = Pm[3];
   const double b0 = yg, b1 = mpj_tan(pg);
   out[0] = P0 * b0 + P1 * b1;
   out[1] = P2 * b0 + P3 * b1;

@@ -95,17 +95,14 @@ template <> struct LM<true> {
   static __device__ __forceinline__ double tan(double x, int& b) { return mpj_tan_wide(x, &b); }
   static __device__ __forceinline__ double atan(double x, int&) { return mpj_atan_bl(x); }
   static __device__ __forceinline__ void sincos(double x, double* s, double* c, int& b) { mpj_sincos_wide(x, s, c, &b); }
-#if defined(MP_ILQR_EXPBL)  // A/B: exp with a per-call wave-uniform exact fallback (with FASTFWD: forward 351 vs exact 365 us, roll out 361 vs 277 us)
-  static __device__ __forceinline__ double exp(double x, int&) { return mpj_exp_bl(x); }
-#else
-  static __device__ __forceinline__ double exp(double x, int& b) { return mpj_exp_fast(x, &b); }
-#endif
+  // Julia's table-driven exp is one basic block for |x| <= 708.39 (the far branch is wave-uniform here)
+  static __device__ __forceinline__ double exp(double x, int&) { return mpj_exp(x); }
   static __device__ __forceinline__ double atan2(double y, double x, int& b) { return mpj_atan2_fast(y, x, &b); }
 #else
   static __device__ double tan(double x, int& b) { int t = 0; double r = mpj_tan_wide(x, &t); if (t) { b |= 1; if (atomicAdd(&g_nbad, 1) < 8) printf("tan %.17g\n", x); } return r; }
   static __device__ double atan(double x, int&) { return mpj_atan_bl(x); }
   static __device__ void sincos(double x, double* s, double* c, int& b) { int t = 0; mpj_sincos_wide(x, s, c, &t); if (t) { b |= 2; if (atomicAdd(&g_nbad, 1) < 8) printf("sincos %.17g\n", x); } }
-  static __device__ double exp(double x, int& b) { int t = 0; double r = mpj_exp_fast(x, &t); if (t) { b |= 4; if (atomicAdd(&g_nbad, 1) < 8) printf("exp %.17g\n", x); } return r; }
+  static __device__ double exp(double x, int&) { return mpj_exp(x); }
   static __device__ double atan2(double y, double x, int& b) { int t = 0; double r = mpj_atan2_fast(y, x, &t); if (t) { b |= 8; if (atomicAdd(&g_nbad, 1) < 8) printf("atan2 %.17g %.17g\n", y, x); } return r; }
 #endif
 };
@@ -365,26 +362,10 @@ __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const
   }
 }
 
-// pinv of a 2x2 (closed-form SVD; identical operation sequence to oracle/or_ilqr.c or_pinv2)
+// pinv of a 2x2: Julia's LinearAlgebra.pinv through LAPACK dgesdd's 2x2 path (mp_jlmath.h
+// mpj_pinv2, the oracle's or_pinv2): no libm calls, a few square roots and divisions.
 template <bool FT>
-__device__ __forceinline__ void pinv2(const double* M, double* Pm, int& bad) {
-  const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
-  const double Q = mpj_sqrt(E * E + H * H), R = mpj_sqrt(F * F + G * G);
-  const double sx = Q + R, sy = Q - R;
-  const double a1 = LM<FT>::atan2(G, F, bad), a2 = LM<FT>::atan2(H, E, bad);
-  const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
-  double st, ct, sp, cp;
-  LM<FT>::sincos(th, &st, &ct, bad);
-  LM<FT>::sincos(ph, &sp, &cp, bad);
-  const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
-  const double tol = 4.440892098500626e-16 * smax;
-  const double i1 = __builtin_fabs(sx) > tol ? 1.0 / sx : 0.0;
-  const double i2 = __builtin_fabs(sy) > tol ? 1.0 / sy : 0.0;
-  Pm[0] = ct * i1 * cp - st * i2 * sp;
-  Pm[1] = ct * i1 * sp + st * i2 * cp;
-  Pm[2] = -st * i1 * cp - ct * i2 * sp;
-  Pm[3] = -st * i1 * sp + ct * i2 * cp;
-}
+__device__ __forceinline__ void pinv2(const double* M, double* Pm, int&) { mpj_pinv2(M, Pm); }
 
 // Exchange a double with the other lane of the pair (DPP quad_perm [1,0,3,2]).
 __device__ __forceinline__ double dswap(double v) {
@@ -393,34 +374,9 @@ __device__ __forceinline__ double dswap(double v) {
   return __hiloint2double(hi, lo);
 }
 
-// pinv2 on a lane pair: the two square roots, the two atan2, the two sincos and the two
-// reciprocals of the closed-form SVD are the same operations on lane-selected operands (side 0
-// the first of each, side 1 the second), exchanged with one DPP swap each.  Every value is
-// computed exactly as in pinv2 (same operands, same operation), so Pm is bit-identical.
+// pinv2 on a lane pair: both lanes evaluate the whole (short, libm-free) LAPACK path.
 template <bool FT>
-__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int side, int& bad) {
-  const double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
-  const double a = side ? F : E, c = side ? G : H;
-  const double r0 = mpj_sqrt(a * a + c * c), r1 = dswap(r0);
-  const double Q = side ? r1 : r0, R = side ? r0 : r1;
-  const double sx = Q + R, sy = Q - R;
-  const double t0 = LM<FT>::atan2(side ? H : G, side ? E : F, bad), t1 = dswap(t0);
-  const double a1 = side ? t1 : t0, a2 = side ? t0 : t1;
-  const double th = (a2 - a1) / 2, ph = (a2 + a1) / 2;
-  double sn, cs;
-  LM<FT>::sincos(side ? ph : th, &sn, &cs, bad);
-  const double so = dswap(sn), co = dswap(cs);
-  const double st = side ? so : sn, ct = side ? co : cs, sp = side ? sn : so, cp = side ? cs : co;
-  const double smax = __builtin_fabs(sx) > __builtin_fabs(sy) ? __builtin_fabs(sx) : __builtin_fabs(sy);
-  const double tol = 4.440892098500626e-16 * smax;
-  const double sv = side ? sy : sx;
-  const double i0 = __builtin_fabs(sv) > tol ? 1.0 / sv : 0.0, io = dswap(i0);
-  const double i1 = side ? io : i0, i2 = side ? i0 : io;
-  Pm[0] = ct * i1 * cp - st * i2 * sp;
-  Pm[1] = ct * i1 * sp + st * i2 * cp;
-  Pm[2] = -st * i1 * cp - ct * i2 * sp;
-  Pm[3] = -st * i1 * sp + ct * i2 * cp;
-}
+__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int, int&) { mpj_pinv2(M, Pm); }
 
 // ILQR.jl:46-67 for instance b: one thread per instance (the sweep is a serial chain in j).
 // The derivative record of knot j-1 is loaded while knot j is processed (coalesced: the

@@ -32,7 +32,7 @@ def lib():
         if not os.path.exists(LIB):
             build()
         L = ctypes.CDLL(LIB)
-        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "atan_tab", "modpi_bl", "sin_bl", "cos_bl", "exp_bl", "tan_bl", "sin_wide", "cos_wide", "tan_wide", "sin_34", "log_bl"]:
+        for n in ["sin", "cos", "tan", "atan", "asin", "acos", "exp", "log", "modpi", "atan_bl", "atan_tab", "modpi_bl", "sin_bl", "cos_bl", "exp_fdlibm", "tan_bl", "sin_wide", "cos_wide", "tan_wide", "sin_34", "log_bl"]:
             f = getattr(L, "or_m_" + n)
             f.restype = _D
             f.argtypes = [_D]
@@ -60,6 +60,10 @@ def lib():
         L.or_philox_normal2.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                         ctypes.c_uint32, _V]
         L.or_inv2.argtypes = [_V, _V]
+        L.or_pinv2.argtypes = [_V, _V]
+        L.or_pinv2_closed.argtypes = [_V, _V]
+        L.or_pinv2_batch.argtypes = [ctypes.c_int, _V, _V]
+        L.or_svd2_batch.argtypes = [ctypes.c_int, _V, _V, _V, _V]
         L.or_chol2.argtypes = [_V, _V]
         for name, args in [
             ("or_ilqr_rollout", [ctypes.POINTER(ILQRParams), _V, _V, _V]),
@@ -78,6 +82,36 @@ def lib():
 # ----------------------------------------------------------------- math
 def m(name, *x):
     return getattr(lib(), "or_m_" + name)(*x)
+
+
+def pinv2(M):
+    """Julia LinearAlgebra.pinv of one 2x2 (mp_jlmath.h mpj_pinv2)."""
+    M = np.ascontiguousarray(M, np.float64).reshape(2, 2)
+    P = np.zeros((2, 2))
+    lib().or_pinv2(ptr(M), ptr(P))
+    return P
+
+
+def pinv2_closed(M):
+    M = np.ascontiguousarray(M, np.float64).reshape(2, 2)
+    P = np.zeros((2, 2))
+    lib().or_pinv2_closed(ptr(M), ptr(P))
+    return P
+
+
+def pinv2_batch(M):
+    M = np.ascontiguousarray(M, np.float64).reshape(-1, 2, 2)
+    P = np.zeros_like(M)
+    lib().or_pinv2_batch(len(M), ptr(M), ptr(P))
+    return P
+
+
+def svd2_batch(A):
+    """LAPACK dgesdd(JOBZ='S') of n 2x2 matrices as restated in mpj_svd2: (U, S, VT)."""
+    A = np.ascontiguousarray(A, np.float64).reshape(-1, 2, 2)
+    U, S, VT = np.zeros_like(A), np.zeros((len(A), 2)), np.zeros_like(A)
+    lib().or_svd2_batch(len(A), ptr(A), ptr(U), ptr(S), ptr(VT))
+    return U, S, VT
 
 
 # ----------------------------------------------------------------- MPPI

@@ -160,9 +160,18 @@ static void linearize(const double* s, const double* u, double dT, double e, dou
   }
 }
 
-/* pinv of a 2x2 (LinearAlgebra.pinv: SVD, rtol = eps*2), closed-form SVD:
- * M = R(φ) diag(sx, sy) R(θ);  pinv = R(θ)ᵀ diag(1/s | 0) R(φ)ᵀ. */
-void or_pinv2(const double* M, double* P) {
+/* pinv of a 2x2: Julia's LinearAlgebra.pinv through LAPACK dgesdd (mp_jlmath.h mpj_pinv2). */
+void or_pinv2(const double* M, double* P) { mpj_pinv2(M, P); }
+void or_pinv2_batch(int n, const double* M, double* P) {
+  for (int i = 0; i < n; i++) mpj_pinv2(M + 4 * i, P + 4 * i);
+}
+void or_svd2_batch(int n, const double* A, double* U, double* S, double* VT) {
+  for (int i = 0; i < n; i++) mpj_svd2(A + 4 * i, U + 4 * i, S + 2 * i, VT + 4 * i);
+}
+
+/* The round-1/2 closed-form 2x2 SVD pinv (M = R(φ) diag(sx, sy) R(θ)), kept only for
+ * tools/ilqr_ulp_sources.py's rounding-source table. */
+void or_pinv2_closed(const double* M, double* P) {
   double E = (M[0] + M[3]) / 2, F = (M[0] - M[3]) / 2, G = (M[2] + M[1]) / 2, H = (M[2] - M[1]) / 2;
   double Q = sqrt(E * E + H * H), R = sqrt(F * F + G * G);
   double sx = Q + R, sy = Q - R;

@@ -413,7 +413,7 @@ double or_m_atan_bl(double x) { return mpj_atan_bl(x); }
 double or_m_modpi_bl(double x) { return mpj_modpi_bl(x); }
 double or_m_atan2_bl(double y, double x) { return mpj_atan2_bl(y, x); }
 double or_m_atan2_sel(double y, double x) { return mpj_atan2_sel(y, x); }
-double or_m_exp_bl(double x) { return mpj_exp_bl(x); }
+double or_m_exp_fdlibm(double x) { return mpj_exp_fdlibm(x); }
 double or_m_sin_wide(double x) { double s, c; int b = 0; mpj_sincos_wide(x, &s, &c, &b); return b ? mpj_sin(x) : s; }
 double or_m_cos_wide(double x) { double s, c; int b = 0; mpj_sincos_wide(x, &s, &c, &b); return b ? mpj_cos(x) : c; }
 double or_m_tan_bl(double x) { return mpj_tan_bl(x); }
