@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--rotate", type=int, default=3, help="output buffer sets rotated (>256 MB MALL at S=8)")
     ap.add_argument("--no-single", action="store_true", help="skip the single-scene (configs[1]) line")
+    ap.add_argument("--roofline", default=os.path.join(ROOT, "profiles", "roofline_latest.json"),
+                    help="per-kernel VALU counts + durations (tools/pmc_roofline.py) for the iLQR / HA* rooflines")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                     help="rocprofv3 PMC summary (tools/pmc_traffic.py) for roofline.traffic")
     ap.add_argument("--final-inline", action="store_true",
@@ -279,6 +281,13 @@ def main():
     if not a.no_extras:
         out["ilqr"] = bench_ilqr(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
         out["hybrid_astar"] = bench_hastar(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
+        rl = load_roofline(a.roofline)
+        if rl:
+            out["ilqr"]["roofline"] = valu_roofline(rl, ["ilqr_backward_staged_kernel<2>", "ilqr_forward_quad_kernel",
+                                                         "ilqr_deriv_kernel", "ilqr_search_kernel<16, 4>",
+                                                         "ilqr_search_rest_kernel<16, 4>"])
+            out["hybrid_astar"]["roofline"] = valu_roofline(rl, ["ha_iter_kernel<4, 16>", "ha_book_kernel",
+                                                                 "ha_iter_kernel<12, 4>"])
         out["closed_loop"] = bench_closed_loop(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
@@ -302,6 +311,30 @@ def load_traffic(path, S, K, H):
     return {"traffic_bytes": e["traffic_bytes"], "valu_insts": e.get("SQ_INSTS_VALU"),
             "valu_active": e.get("SQ_ACTIVE_INST_VALU"), "wave_cycles": e.get("SQ_WAVE_CYCLES"),
             "waves": e.get("SQ_WAVES"), "source": os.path.relpath(path, ROOT)}
+
+
+def load_roofline(path):
+    try:
+        return json.load(open(path)) | {"path": os.path.relpath(path, ROOT)}
+    except (OSError, ValueError):
+        return None
+
+
+def valu_roofline(rl, names):
+    """roofline of a latency/VALU-bound leg: per kernel SQ_INSTS_VALU per launch / kernel-trace average
+    duration vs the fp64 VALU issue peak (tools/pmc_roofline.py, a PMC pass of this tree); the first
+    listed kernel present is the headline ("kernel"), the others follow under "kernels"."""
+    ks = {n: rl["kernels"][n] for n in names if n in rl["kernels"] and "valu_frac" in rl["kernels"][n]}
+    if not ks:
+        return None
+    head = next(iter(ks))
+    e = ks[head]
+    return {"bound": "valu", "kernel": head, "achieved": e["valu_achieved"], "peak": rl["peak_wave_insts_per_s"],
+            "unit": "wave-insts/s", "frac": e["valu_frac"], "traffic": None,
+            "kernels": {n: {"insts_per_launch": k["SQ_INSTS_VALU"], "avg_us": k["avg_ns"] / 1e3,
+                            "frac": k["valu_frac"], "wave_valu_busy": k.get("wave_valu_busy")}
+                        for n, k in ks.items()},
+            "source": rl["path"] + " (from " + str(rl.get("source")) + ")"}
 
 
 def _sync_max(x, world, dev):
