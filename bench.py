@@ -283,7 +283,7 @@ def main():
         out["hybrid_astar"] = bench_hastar(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
         rl = load_roofline(a.roofline)
         if rl:
-            out["ilqr"]["roofline"] = valu_roofline(rl, ["ilqr_backward_staged_kernel<2>", "ilqr_forward_quad_kernel",
+            out["ilqr"]["roofline"] = valu_roofline(rl, ["ilqr_backward_quad_kernel", "ilqr_forward_quad_kernel",
                                                          "ilqr_deriv_kernel", "ilqr_search_kernel<16, 4>",
                                                          "ilqr_search_rest_kernel<16, 4>"])
             out["hybrid_astar"]["roofline"] = valu_roofline(rl, ["ha_iter_kernel<4, 16>", "ha_book_kernel",

@@ -1362,4 +1362,103 @@ MPJ_FN void mpj_pinv2(const double* M, double* P) {
   P[3] = VT[1] * D01 + VT[3] * D11;
 }
 
+#ifndef MPJ_PSEL /* the selects of mpj_pinv2_fast (A/B: plain ternaries) */
+#define MPJ_PSEL(c, t, f) MPJ_SEL(c, t, f)
+#endif
+/* mpj_pinv2's general path as one basic block (the device's Riccati sweep, where the branchy
+ * routine's ~20 uniform branches cost more than its divisions): every operation of mpj_pinv2 on the
+ * path that a generic Quu takes -- not diagonal, a21 != 0 (a real reflector, v2 != 0), a12 != 0,
+ * |e1| above dbdsqr's split threshold, dlasv2's gasmal branch with m*m != 0 -- with the swap, pmax,
+ * sign-fix and cutoff decisions as selects.  Any lane off that path sets *rare; the caller then runs
+ * mpj_pinv2 for it (mpj_pinv2_bl: wave-uniform on the device).  Same operations on the same
+ * operands, so the same bits (tests/test_jlmath.py). */
+MPJ_FN void mpj_pinv2_fast(const double* M, double* P, int* rare) {
+  const double eps = 1.1102230246251565e-16, rtol = 4.440892098500626e-16;
+  const double a11 = M[0], a12 = M[1], a21 = M[2], a22 = M[3];
+  /* dgebd2: dlarfg(2, a11, a21) + dlarf on column 2 */
+  const double xnorm = __builtin_fabs(a21), aa = __builtin_fabs(a11);
+  const int big = aa > xnorm;
+  const double w = MPJ_PSEL(big, aa, xnorm), z = MPJ_PSEL(big, xnorm, aa);
+  const double q = z / w;
+  const double py = MPJ_PSEL(z == 0.0, w, w * mpj_sqrt(1.0 + q * q));
+  const double beta = -mpj_fsign(py, a11);
+  const double tau = (beta - a11) / beta;
+  const double v2 = a21 * (1.0 / (a11 - beta));
+  const double d1 = beta;
+  const double tw0 = -tau * (a12 + a22 * v2);
+  const double e1 = a12 + tw0, d2 = mpj_fma(tw0, v2, a22);
+  /* dbdsqr split test */
+  const double unfl = 2.2250738585072014e-308, tol = 1.0958066990042004e-14;
+  const double s0 = __builtin_fabs(d1);
+  const double mu = __builtin_fabs(d2) * (s0 / (s0 + __builtin_fabs(e1)));
+  const double sminoa = MPJ_PSEL(mu < s0, mu, s0) / 1.4142135623730951;
+  const double th0 = tol * sminoa, th1 = 6.0 * (2.0 * (2.0 * unfl));
+  const double thresh = MPJ_PSEL(th0 > th1, th0, th1);
+  /* dlasv2(d1, e1, d2) */
+  const double f = d1, g = e1, h = d2;
+  const double fa0 = __builtin_fabs(f), ha0 = __builtin_fabs(h);
+  const int swap = ha0 > fa0;
+  const double ft = MPJ_PSEL(swap, h, f), ht = MPJ_PSEL(swap, f, h);
+  const double fa = MPJ_PSEL(swap, ha0, fa0), ha = MPJ_PSEL(swap, fa0, ha0);
+  const double gt = g, ga = __builtin_fabs(g);
+  const int gbig = ga > fa;
+  const double d = fa - ha;
+  const double l0 = MPJ_PSEL(d == fa, 1.0, d / fa);
+  const double m = gt / ft;
+  const double t0 = 2.0 - l0;
+  const double mm = m * m, tt = t0 * t0;
+  const double s = mpj_sqrt(tt + mm);
+  const double r = MPJ_PSEL(l0 == 0.0, __builtin_fabs(m), mpj_sqrt(l0 * l0 + mm));
+  const double a = 0.5 * (s + r);
+  const double smin = ha / a, smax = fa * a;
+  const double t = (m / (s + t0) + m / (r + l0)) * (1.0 + a);
+  const double l = mpj_sqrt(t * t + 4.0);
+  const double crt = 2.0 / l, srt = t / l;
+  const double clt = (crt + srt * m) / a;
+  const double slt = (ht / ft) * srt / a;
+  const double csl = MPJ_PSEL(swap, srt, clt), snl = MPJ_PSEL(swap, crt, slt);
+  const double csr = MPJ_PSEL(swap, slt, crt), snr = MPJ_PSEL(swap, clt, srt);
+  const double ts1 = mpj_fsign(1.0, csr) * mpj_fsign(1.0, csl) * mpj_fsign(1.0, f);
+  const double ts2 = mpj_fsign(1.0, snr) * mpj_fsign(1.0, csl) * mpj_fsign(1.0, g);
+  const double ts3 = mpj_fsign(1.0, snr) * mpj_fsign(1.0, snl) * mpj_fsign(1.0, h);
+  const double tsign = MPJ_PSEL(gbig, ts2, MPJ_PSEL(swap, ts3, ts1));
+  const double dd0 = mpj_fsign(smax, tsign);
+  const double dd1 = mpj_fsign(smin, tsign * mpj_fsign(1.0, f) * mpj_fsign(1.0, h));
+  *rare |= (a12 == 0.0) | (a21 == 0.0) | (v2 == 0.0) | !(__builtin_fabs(e1) > thresh) | (gbig && fa / ga < eps) |
+           (mm == 0.0);
+  /* drot on the identity */
+  const double vt0 = csr * 1.0 + snr * 0.0, vt1 = csr * 0.0 + snr * 1.0;
+  const double vt2 = csr * 0.0 - snr * 1.0, vt3 = csr * 1.0 - snr * 0.0;
+  const double ub0 = csl * 1.0 + snl * 0.0, ub1 = csl * 0.0 - snl * 1.0;
+  const double ub2 = csl * 0.0 + snl * 1.0, ub3 = csl * 1.0 - snl * 0.0;
+  *rare |= (ub1 == 0.0) & (ub3 == 0.0);
+  /* sign fix (d >= 0) and the sort (never swaps here: |ssmin| <= |ssmax|).  The fixed values are
+   * |dd0| = smax and |dd1| = smin exactly (both >= 0), so the reciprocals below start from smax and
+   * smin without waiting for the sign decision. */
+  const int n0 = dd0 < 0.0, n1 = dd1 < 0.0;
+  const double S0 = smax, S1 = smin;
+  *rare |= !(S1 <= S0) | !(S0 > 0.0);
+  const double V0 = MPJ_PSEL(n0, vt0 * -1.0, vt0), V1 = MPJ_PSEL(n0, vt1 * -1.0, vt1);
+  const double V2 = MPJ_PSEL(n1, vt2 * -1.0, vt2), V3 = MPJ_PSEL(n1, vt3 * -1.0, vt3);
+  /* dormbr: U = H1 * Ub on both columns (lastv = 2, lastc = 2: column 2 of Ub is never zero) */
+  const double twa = -tau * (ub0 + ub2 * v2), twb = -tau * (ub1 + ub3 * v2);
+  const double U0 = ub0 + twa, U2 = mpj_fma(twa, v2, ub2);
+  const double U1 = ub1 + twb, U3 = mpj_fma(twb, v2, ub3);
+  /* pinv composition */
+  const double ctol = rtol * S0;
+  const double x0 = 1.0 / S0, x1 = 1.0 / S1;
+  const double i0 = MPJ_PSEL(S0 > ctol && x0 - x0 == 0.0, x0, 0.0);
+  const double i1 = MPJ_PSEL(S1 > ctol && x1 - x1 == 0.0, x1, 0.0);
+  const double D00 = i0 * U0, D01 = i0 * U2, D10 = i1 * U1, D11 = i1 * U3;
+  P[0] = V0 * D00 + V2 * D10;
+  P[1] = V0 * D01 + V2 * D11;
+  P[2] = V1 * D00 + V3 * D10;
+  P[3] = V1 * D01 + V3 * D11;
+}
+MPJ_FN void mpj_pinv2_bl(const double* M, double* P) {
+  int rare = 0;
+  mpj_pinv2_fast(M, P, &rare);
+  if (MPJ_ANY(rare)) mpj_pinv2(M, P);
+}
+
 #endif /* MP_JLMATH_H */

@@ -363,9 +363,15 @@ __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const
 }
 
 // pinv of a 2x2: Julia's LinearAlgebra.pinv through LAPACK dgesdd's 2x2 path (mp_jlmath.h
-// mpj_pinv2, the oracle's or_pinv2): no libm calls, a few square roots and divisions.
+// mpj_pinv2, the oracle's or_pinv2): no libm calls, a few square roots and divisions.  FT: the
+// straight-line general path (mpj_pinv2_fast) with a wave-uniform exact fallback for the rare lanes
+// (diagonal / triangular Quu, dbdsqr splits): the branchy routine's uniform branches cost a lone wave
+// ~4,300 cycles per call vs ~2,000 straight-line (tools/ubench/pinvlat.hip).
 template <bool FT>
-__device__ __forceinline__ void pinv2(const double* M, double* Pm, int&) { mpj_pinv2(M, Pm); }
+__device__ __forceinline__ void pinv2(const double* M, double* Pm, int&) {
+  if (FT) mpj_pinv2_bl(M, Pm);
+  else mpj_pinv2(M, Pm);
+}
 
 // Exchange a double with the other lane of the pair (DPP quad_perm [1,0,3,2]).
 __device__ __forceinline__ double dswap(double v) {
@@ -376,7 +382,7 @@ __device__ __forceinline__ double dswap(double v) {
 
 // pinv2 on a lane pair: both lanes evaluate the whole (short, libm-free) LAPACK path.
 template <bool FT>
-__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int, int&) { mpj_pinv2(M, Pm); }
+__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int, int& bad) { pinv2<FT>(M, Pm, bad); }
 
 // ILQR.jl:46-67 for instance b: one thread per instance (the sweep is a serial chain in j).
 // The derivative record of knot j-1 is loaded while knot j is processed (coalesced: the
@@ -803,14 +809,280 @@ __global__ __launch_bounds__(64 * (LANES + 1)) void ilqr_backward_staged_kernel(
   }
 }
 
-// Two compute lanes per instance: the whole sweep runs on both (the matrix products need no
-// exchange) except the closed-form pinv, whose sqrt / atan2 / sincos / reciprocal pairs are
-// split over the pair (pinv2_pair).  Measured: 247 us vs 294 us for one lane (the pinv's libm
-// chains dominate a lone wave's issue), vs 566 us when the matrix rows were split as well.
-#if defined(MP_ILQR_SINGLEPINV)
-constexpr int kBwdStagedLanes = 1;
-#else
+// Broadcast lane k of each lane quad to the quad (DPP quad_perm [k,k,k,k], one VALU op per half).
+template <int K>
+__device__ __forceinline__ double qbcast(double v) {
+  constexpr int ctl = K | (K << 2) | (K << 4) | (K << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ void qgather(double v, double* out) {  // out[k] = lane k's v
+  out[0] = qbcast<0>(v);
+  out[1] = qbcast<1>(v);
+  out[2] = qbcast<2>(v);
+  out[3] = qbcast<3>(v);
+}
+
+// ILQR.jl:46-67 on a LANE QUAD per instance (lane q = 0..3), records from the LDS stage
+// [2][ND][IPB].  Every product entry is computed by exactly the operations (and summation order)
+// of backward_sweep / the oracle, only on the lane that owns it: lane q owns row q of T44, Qxx, Vxx
+// and KQ, entry q of Qx and Vx, column q of T24, Qux and KK; the 2x2 Quu, the pinv, Qu, kk and qk
+// are evaluated on all four lanes (the pinv is the chain every lane waits on anyway).  Quad
+// broadcasts (DPP) assemble T24, KK, Vx and Vxx where a full copy is needed.  The lone wave issues
+// ~40 % of the one-lane sweep's instructions per knot, leaving the pinv chain as the bound.
+template <int IPB>
+__device__ __forceinline__ void backward_sweep_quad(const IlqrDev& P, int b, bool live, const double* X,
+                                                    double* kout, double* Kout, const double* lds, int inst, int q) {
+  const int N = P.N;
+  const double e = P.eps;
+  const int V = P.variant;
+  double Vx[4], Vxx[16];
+  {  // CalculateMatrix(StatesList[:, end], [0 0], TerminalCost): lx, lxx (every lane, once per sweep)
+    const double* xs = X + ((size_t)b * N + N - 1) * 4;
+    const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
+    double sp[4], sm[4], t1[4], t2[4], t3[4], t4[4];
+    const double c12 = 1 / (12 * (e * e)), c4 = 1 / (4 * (e * e));
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
+      sp[i] = s[i] + e;
+      sm[i] = s[i] - e;
+      Vx[i] = (terminal(V, sp) - terminal(V, sm)) / (2 * e);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) { t1[r] = s[r]; t2[r] = s[r]; t3[r] = s[r]; t4[r] = s[r]; }
+        if (i == j) {
+          t1[i] = s[i] + 2 * e; t2[i] = s[i] + e; t3[i] = s[i] - e; t4[i] = s[i] - 2 * e;
+          Vxx[4 * i + j] = c12 * (-terminal(V, t1) + 16 * terminal(V, t2) - 30 * terminal(V, s) +
+                                  16 * terminal(V, t3) - terminal(V, t4));
+        } else {
+          t1[i] = s[i] + e; t1[j] = s[j] + e;
+          t2[i] = s[i] - e; t2[j] = s[j] - e;
+          t3[i] = s[i] + e; t3[j] = s[j] - e;
+          t4[i] = s[i] - e; t4[j] = s[j] + e;
+          Vxx[4 * i + j] = c4 * (terminal(V, t1) + terminal(V, t2) - terminal(V, t3) - terminal(V, t4));
+        }
+      }
+  }
+  for (int j = N - 2, t = 0; j >= 0; j--, t++) {
+    lds_barrier();  // knot j's records staged by the loader wave before barrier t
+    const double* bf = lds + (size_t)(t & 1) * ND * IPB + inst;
+    // no run-time index into a register array (q is per lane): column q of A comes from LDS, column
+    // q of Vxx from the selects below
+    double A[16], Bm[8], Acol[4], Vcol[4];
+#pragma unroll
+    for (int r = 0; r < 16; r++) A[r] = bf[r * IPB];
+#pragma unroll
+    for (int k = 0; k < 4; k++) Acol[k] = bf[(4 * k + q) * IPB];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      Vcol[k] = q < 2 ? (q == 0 ? Vxx[4 * k + 0] : Vxx[4 * k + 1]) : (q == 2 ? Vxx[4 * k + 2] : Vxx[4 * k + 3]);
+#pragma unroll
+    for (int r = 0; r < 8; r++) Bm[r] = bf[(16 + r) * IPB];
+    const double lxq = bf[(24 + q) * IPB];
+    const double lu0 = bf[28 * IPB], lu1 = bf[29 * IPB];
+    double lxxq[4], luu[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) lxxq[c] = bf[(30 + 4 * q + c) * IPB];
+#pragma unroll
+    for (int c = 0; c < 4; c++) luu[c] = bf[(46 + c) * IPB];
+    const double lux0q = bf[(50 + q) * IPB], lux1q = bf[(54 + q) * IPB];
+    // Qx[q] = lx[q] + fx' * Vx  (own entry)
+    double Qxq;
+    {
+      double acc = Acol[0] * Vx[0];
+#pragma unroll
+      for (int k = 1; k < 4; k++) acc = acc + Acol[k] * Vx[k];
+      Qxq = lxq + acc;
+    }
+    double Qu[2];  // every lane
+    {
+      double a0 = Bm[0 * 2 + 0] * Vx[0], a1 = Bm[0 * 2 + 1] * Vx[0];
+#pragma unroll
+      for (int k = 1; k < 4; k++) {
+        a0 = a0 + Bm[k * 2 + 0] * Vx[k];
+        a1 = a1 + Bm[k * 2 + 1] * Vx[k];
+      }
+      Qu[0] = lu0 + a0;
+      Qu[1] = lu1 + a1;
+    }
+    // T24 column q = (fu' Vxx)[:, q], gathered to the full 2x4
+    double T24[8];
+    {
+      double c0 = Bm[0 * 2 + 0] * Vcol[0], c1 = Bm[0 * 2 + 1] * Vcol[0];
+#pragma unroll
+      for (int k = 1; k < 4; k++) {
+        c0 = c0 + Bm[k * 2 + 0] * Vcol[k];
+        c1 = c1 + Bm[k * 2 + 1] * Vcol[k];
+      }
+      qgather(c0, T24);
+      qgather(c1, T24 + 4);
+    }
+    // T44 row q = (fx' Vxx)[q, :], Qxx row q = lxx[q, :] + T44[q, :] fx  (own)
+    double T44q[4], Qxxq[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      double acc = Acol[0] * Vxx[0 * 4 + c];
+#pragma unroll
+      for (int k = 1; k < 4; k++) acc = acc + Acol[k] * Vxx[k * 4 + c];
+      T44q[c] = acc;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      double acc = T44q[0] * A[0 * 4 + c];
+#pragma unroll
+      for (int k = 1; k < 4; k++) acc = acc + T44q[k] * A[k * 4 + c];
+      Qxxq[c] = lxxq[c] + acc;
+    }
+    // Quu (every lane), Qux column q (own)
+    double Quu[4];
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+#pragma unroll
+      for (int c = 0; c < 2; c++) {
+        double acc = T24[4 * i + 0] * Bm[0 * 2 + c];
+#pragma unroll
+        for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * Bm[k * 2 + c];
+        Quu[2 * i + c] = luu[2 * i + c] + acc;
+      }
+    double Quxq[2];
+    {
+      double a0 = T24[0] * Acol[0], a1 = T24[4] * Acol[0];
+#pragma unroll
+      for (int k = 1; k < 4; k++) {
+        a0 = a0 + T24[k] * Acol[k];
+        a1 = a1 + T24[4 + k] * Acol[k];
+      }
+      Quxq[0] = lux0q + a0;
+      Quxq[1] = lux1q + a1;
+    }
+    double Pm[4];
+    int bad = 0;
+    pinv2<true>(Quu, Pm, bad);
+    double kk[2], KKq[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) kk[i] = (-Pm[2 * i + 0]) * Qu[0] + (-Pm[2 * i + 1]) * Qu[1];
+#pragma unroll
+    for (int i = 0; i < 2; i++) KKq[i] = (-Pm[2 * i + 0]) * Quxq[0] + (-Pm[2 * i + 1]) * Quxq[1];
+    if (live) {
+      if (q < 2) kout[((size_t)b * (N - 1) + j) * 2 + q] = q == 0 ? kk[0] : kk[1];
+      double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8 + 2 * q;  // Klist[:, :, j] column q = (KK[0][q], KK[1][q])
+      Ko[0] = KKq[0];
+      Ko[1] = KKq[1];
+    }
+    double qk[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) qk[i] = Quu[2 * i + 0] * kk[0] + Quu[2 * i + 1] * kk[1];
+    const double vxq = Qxq - (KKq[0] * qk[0] + KKq[1] * qk[1]);
+    double KQ[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) KQ[c] = KKq[0] * Quu[0 * 2 + c] + KKq[1] * Quu[1 * 2 + c];
+    double KK0[4], KK1[4];
+    qgather(KKq[0], KK0);
+    qgather(KKq[1], KK1);
+    double vxxq[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) vxxq[c] = Qxxq[c] - (KQ[0] * KK0[c] + KQ[1] * KK1[c]);
+    qgather(vxq, Vx);
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      double col[4];
+      qgather(vxxq[c], col);
+#pragma unroll
+      for (int k = 0; k < 4; k++) Vxx[4 * k + c] = col[k];
+    }
+  }
+}
+
+#ifndef ILQR_LOADER_DEPTH
+#define ILQR_LOADER_DEPTH 2
+#endif
+constexpr int kLoaderDepth = ILQR_LOADER_DEPTH;  // knots of records in flight in the loader wave
+
+// The loader wave of a quad-sweep block: knot j's records of the block's IPB instances into LDS
+// buffer t&1 ([ND][IPB]) before barrier t; lane l loads components l/IPB, l/IPB + 64/IPB, ... of
+// instance column l % IPB (IPB consecutive columns per component: coalesced 8*IPB-byte rows).
+template <int IPB>
+__device__ __forceinline__ void record_loader_quad(const IlqrDev& P, int B, int col0, int ncol, const double* D,
+                                                   double* lds, int lane) {
+  constexpr int CPL = 64 / IPB;                      // components per pass
+  constexpr int NP = (ND + CPL - 1) / CPL;           // passes
+  const int N = P.N;
+  const size_t ks = (size_t)ND * B;
+  const int ci = lane % IPB, c0 = lane / IPB;
+  const int col = col0 + (ci < ncol ? ci : ncol - 1);  // columns past the list end repeat the last one
+  const double* Db = D + col;
+  // kLoaderDepth knots in flight: the loads of knot j-PD are issued while knot j is handed over, so
+  // the global-load latency overlaps PD compute steps.  Measured at configs[2]: depth 1 388 us per
+  // sweep (the loads' latency, not the compute, set the pace), 2: 180 us, 3 / 4 / 6: 181 / 183 / 182 us.
+  constexpr int PD = kLoaderDepth;
+  double v[PD][NP];
+#pragma unroll
+  for (int d = 0; d < PD; d++)
+#pragma unroll
+    for (int pq = 0; pq < NP; pq++) {
+      const int qq = c0 + pq * CPL;
+      v[d][pq] = qq < ND && N - 2 - d >= 0 ? Db[(size_t)(N - 2 - d) * ks + (size_t)qq * B] : 0.0;
+    }
+  for (int j = N - 2, t = 0; j >= 0; j--, t++) {
+    double* bf = lds + (size_t)(t & 1) * ND * IPB + ci;
+#pragma unroll
+    for (int pq = 0; pq < NP; pq++) {
+      const int qq = c0 + pq * CPL;
+      if (qq < ND) bf[qq * IPB] = v[0][pq];
+    }
+#pragma unroll
+    for (int d = 0; d + 1 < PD; d++)
+#pragma unroll
+      for (int pq = 0; pq < NP; pq++) v[d][pq] = v[d + 1][pq];
+    if (j - PD >= 0) {
+#pragma unroll
+      for (int pq = 0; pq < NP; pq++) {
+        const int qq = c0 + pq * CPL;
+        if (qq < ND) v[PD - 1][pq] = Db[(size_t)(j - PD) * ks + (size_t)qq * B];
+      }
+    }
+    lds_barrier();
+  }
+}
+
+// Riccati sweep, quad mapping (default): block = one compute wave (IPB = 16 instances x 4 lanes)
+// + one loader wave; 4,096 instances -> 256 blocks, one per CU.
+constexpr int kQuadIPB = 16;
+__global__ __launch_bounds__(128) void ilqr_backward_quad_kernel(IlqrDev P, int B, const double* X, const double* D,
+                                                                 const int* list, const int* n_dev, int nmax,
+                                                                 double* kout, double* Kout) {
+  extern __shared__ double recs[];  // [2][ND][kQuadIPB]
+  const int tid = threadIdx.x;
+  const int n = n_dev ? *n_dev : nmax;
+  const int col0 = blockIdx.x * kQuadIPB;
+  if (col0 >= n) return;  // block-uniform: the grid covers nmax >= n
+  if (tid >= 64) {
+    record_loader_quad<kQuadIPB>(P, B, col0, n - col0, D, recs, tid - 64);
+    return;
+  }
+  const int inst = tid >> 2, q = tid & 3;
+  const int i0 = col0 + inst;
+  const bool live = i0 < n;
+  const int i = live ? i0 : n - 1;  // dead quads recompute the last column and store nothing
+  const int b = list ? list[i] : i;
+  backward_sweep_quad<kQuadIPB>(P, b, live, X, kout, Kout, recs, live ? inst : (n - 1 - col0), q);
+}
+
+// Compute lanes per instance.  Round 2 ran two (the whole sweep on both, the closed-form pinv's
+// sqrt / atan2 / sincos / reciprocal pairs split over the pair: 247 vs 294 us for one lane); the
+// LAPACK pinv has no libm pairs to split, so one lane per instance is the default now and
+// -DMP_ILQR_PAIRPINV builds the pair (both lanes then run the identical pinv).
+#if defined(MP_ILQR_PAIRPINV)
 constexpr int kBwdStagedLanes = 2;
+#else
+constexpr int kBwdStagedLanes = 1;
 #endif
 
 #if defined(MP_ILQR_PAIR)  // A/B build: a lane pair per instance (measured slower: 391 vs 354 us)
@@ -1342,7 +1614,10 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
   hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
                      list, n_dev, na, dD);
   MP_HIP(ctx, hipGetLastError());
-#if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR)
+#if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR) && !defined(MP_ILQR_STAGED)
+  hipLaunchKernelGGL(ilqr_backward_quad_kernel, dim3((na + kQuadIPB - 1) / kQuadIPB), dim3(128),
+                     sizeof(double) * 2 * ND * kQuadIPB, ctx->stream, D, B, dX, dD, list, n_dev, na, dk, dK);
+#elif !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR)
   hipLaunchKernelGGL(ilqr_backward_staged_kernel<kBwdStagedLanes>, dim3((na + 63) / 64),
                      dim3(64 * (kBwdStagedLanes + 1)), sizeof(double) * 2 * ND * 64, ctx->stream, D, B, dX, dD,
                      list, n_dev, na, dk, dK);

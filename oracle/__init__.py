@@ -64,6 +64,7 @@ def lib():
         L.or_pinv2_closed.argtypes = [_V, _V]
         L.or_pinv2_batch.argtypes = [ctypes.c_int, _V, _V]
         L.or_svd2_batch.argtypes = [ctypes.c_int, _V, _V, _V, _V]
+        L.or_pinv2_fast_batch.argtypes = [ctypes.c_int, _V, _V, _V]
         L.or_chol2.argtypes = [_V, _V]
         for name, args in [
             ("or_ilqr_rollout", [ctypes.POINTER(ILQRParams), _V, _V, _V]),
@@ -104,6 +105,14 @@ def pinv2_batch(M):
     P = np.zeros_like(M)
     lib().or_pinv2_batch(len(M), ptr(M), ptr(P))
     return P
+
+
+def pinv2_fast_batch(M):
+    """mpj_pinv2_fast (the straight-line general path): (P, rare)."""
+    M = np.ascontiguousarray(M, np.float64).reshape(-1, 2, 2)
+    P, rare = np.zeros_like(M), np.zeros(len(M), np.int32)
+    lib().or_pinv2_fast_batch(len(M), ptr(M), ptr(P), ptr(rare))
+    return P, rare
 
 
 def svd2_batch(A):

@@ -165,6 +165,13 @@ void or_pinv2(const double* M, double* P) { mpj_pinv2(M, P); }
 void or_pinv2_batch(int n, const double* M, double* P) {
   for (int i = 0; i < n; i++) mpj_pinv2(M + 4 * i, P + 4 * i);
 }
+/* the device sweep's straight-line variant (mpj_pinv2_fast); rare[i] = 1 where it defers to mpj_pinv2 */
+void or_pinv2_fast_batch(int n, const double* M, double* P, int* rare) {
+  for (int i = 0; i < n; i++) {
+    rare[i] = 0;
+    mpj_pinv2_fast(M + 4 * i, P + 4 * i, rare + i);
+  }
+}
 void or_svd2_batch(int n, const double* A, double* U, double* S, double* VT) {
   for (int i = 0; i < n; i++) mpj_svd2(A + 4 * i, U + 4 * i, S + 2 * i, VT + 4 * i);
 }

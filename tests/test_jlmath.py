@@ -321,3 +321,18 @@ def test_pinv2_is_julia_pinv():
     M = r.standard_normal((200, 2, 2))
     P = oracle.pinv2_batch(M)
     np.testing.assert_allclose(np.einsum("nij,njk,nkl->nil", M, P, M), M, rtol=1e-9, atol=1e-9)
+
+
+def test_pinv2_fast_path_bitexact():
+    """mpj_pinv2_fast (the device sweep's one-basic-block general path) == mpj_pinv2 bit for bit on every
+    matrix it does not flag rare; the flagged ones (diagonal, triangular, zero entries, splits, ...)
+    take mpj_pinv2 itself.  Random Quu-like symmetric matrices are never rare."""
+    r = np.random.default_rng(21)
+    A = _families(r, 3000)
+    Q = r.standard_normal((20000, 2, 2)) * 10.0 ** r.integers(-3, 5, (20000, 1, 1))
+    A = np.concatenate([A, Q + np.swapaxes(Q, 1, 2)])
+    P, rare = oracle.pinv2_fast_batch(A)
+    ref = oracle.pinv2_batch(A)
+    ok = rare == 0
+    assert np.array_equal(P[ok].view(np.int64), ref[ok].view(np.int64))
+    assert rare[-20000:].sum() == 0 and 0 < rare.sum() < len(A)

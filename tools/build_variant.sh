@@ -20,7 +20,9 @@ for f in *.hip; do
 done
 $HIPCC $FLAGS $EXTRA -x hip -c runtime.cpp -o $B/runtime.o &
 pids+=($!)
+$HIPCC $FLAGS $EXTRA -x hip -c comm.cpp -o $B/comm.o &
+pids+=($!)
 for p in "${pids[@]}"; do wait $p; done
-$HIPCC --offload-arch=gfx950 -shared -fPIC -pthread -o ../lib/libmpgpu_$SUF.so $B/*.o
+$HIPCC --offload-arch=gfx950 -shared -fPIC -pthread -o ../lib/libmpgpu_$SUF.so $B/*.o -ldl
 rm -rf $B
 echo "built motionplanning_amd/lib/libmpgpu_$SUF.so"

@@ -55,13 +55,20 @@ def main():
     ap.add_argument("--extra", action="append", default=[])
     ap.add_argument("--top", type=int, default=0)
     ap.add_argument("--inst", default="ILi512E", help="substring selecting the template instance")
+    ap.add_argument("--lines", type=int, default=0, help="attribute the loop's VALU instructions to source lines "
+                                                         "(-g .loc directives) and print the top N")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         asm = os.path.join(td, "k.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                        "--cuda-device-only", "-S", "-DMPJ_COUNT_HOT_PATH", "-I" + os.path.join(ROOT, "include"),
+                        "--cuda-device-only", "-S", "-DMPJ_COUNT_HOT_PATH", *(["-g"] if a.lines else []), "-I" + os.path.join(ROOT, "include"),
                         *a.extra, "-o", asm, a.src], check=True, capture_output=True)
         lines = open(asm).read().split("\n")
+    files = {}
+    for l in lines:
+        m = re.match(r'\s*\.file\s+(\d+)\s+"([^"]*)"(?:\s+"([^"]*)")?', l)
+        if m:
+            files[m.group(1)] = os.path.basename(m.group(3) or m.group(2))
     # kernels: every symbol containing the name; take the one with the biggest body
     starts = [i for i, l in enumerate(lines) if re.match(r"^_Z\S*" + a.kernel + r"\S*:", l) and a.inst in l]
     best = None
@@ -73,23 +80,41 @@ def main():
             lab = body[h].split(":")[0]  # .LBBk_n
             tag = lab[2:]  # BBk_n as in the "in Loop: Header=BBk_n" / "Parent Loop BBk_n" block notes
             # every basic block of the loop nest: the header and each block the assembler notes as in it
-            ins, inside = [], False
+            ins, locs, inside, loc = [], [], False, None
             for l in body:
                 if l.startswith(".LBB") or l.startswith("; %bb."):
                     inside = l.startswith(lab + ":") or ("Header=" + tag + " ") in l or ("Parent Loop " + tag + " ") in l
                     continue
                 t = l.strip()
+                if t.startswith(".loc"):
+                    f = t.split()
+                    loc = (files.get(f[1], f[1]), int(f[2]))
+                    continue
                 if inside and t and not t.startswith((";", ".")):
                     ins.append(t.split()[0])
+                    locs.append(loc)
             if best is None or len(ins) > len(best[1]):
-                best = (lines[s0].split(":")[0], ins)
-    name, ins = best
+                best = (lines[s0].split(":")[0], ins, locs)
+    name, ins, locs = best
     c = collections.Counter(classify(op) for op in ins)
     valu = sum(v for k, v in c.items() if k.startswith(("f64", "v_", "other VALU")))
     nbr = sum(1 for op in ins if op.startswith("s_cbranch"))
     print(f"{name[:60]}: largest loop body {len(ins)} instructions, VALU {valu}, conditional branches {nbr}")
     for k, v in c.most_common():
         print(f"  {k:20s} {v:6d}")
+    if a.lines:
+        byline = collections.Counter()
+        for op, lc in zip(ins, locs):
+            if classify(op).startswith(("f64", "v_", "other VALU")):
+                byline[lc] += 1
+        for lc, v in byline.most_common(a.lines):
+            src = ""
+            if lc and lc[0]:
+                for d in (os.path.join(ROOT, "include"), os.path.join(ROOT, "motionplanning_amd", "csrc")):
+                    fp = os.path.join(d, lc[0])
+                    if os.path.exists(fp):
+                        src = open(fp).read().split("\n")[lc[1] - 1].strip()[:90]
+            print(f"    {v:5d}  {lc[0] if lc else '?'}:{lc[1] if lc else 0}  {src}")
     if a.top:
         for op, v in collections.Counter(ins).most_common(a.top):
             print(f"    {op:28s} {v}")

@@ -20,7 +20,7 @@ import sys
 from collections import defaultdict
 
 VALU_PEAK = 1024 * 2.4e9 / 4
-KERNELS = ("ilqr_deriv_kernel", "ilqr_backward_staged_kernel", "ilqr_backward_kernel", "ilqr_forward_quad_kernel",
+KERNELS = ("ilqr_deriv_kernel", "ilqr_backward_quad_kernel", "ilqr_backward_staged_kernel", "ilqr_backward_kernel", "ilqr_forward_quad_kernel",
            "ilqr_search_kernel", "ilqr_search_rest_kernel", "ilqr_search_finish_kernel", "ilqr_rollout_kernel",
            "ha_iter_kernel", "ha_book_kernel", "ha_retrieve_kernel", "mppi_plan_kernel", "final_rollout_kernel")
 
