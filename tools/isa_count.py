@@ -55,13 +55,15 @@ def main():
     ap.add_argument("--extra", action="append", default=[])
     ap.add_argument("--top", type=int, default=0)
     ap.add_argument("--inst", default="ILi512E", help="substring selecting the template instance")
+    ap.add_argument("--funcs", action="store_true", help="group the loop's VALU instructions by enclosing "
+                                                          "source function (-g)")
     ap.add_argument("--lines", type=int, default=0, help="attribute the loop's VALU instructions to source lines "
                                                          "(-g .loc directives) and print the top N")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as td:
         asm = os.path.join(td, "k.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                        "--cuda-device-only", "-S", "-DMPJ_COUNT_HOT_PATH", *(["-g"] if a.lines else []), "-I" + os.path.join(ROOT, "include"),
+                        "--cuda-device-only", "-S", "-DMPJ_COUNT_HOT_PATH", *(["-g"] if (a.lines or a.funcs) else []), "-I" + os.path.join(ROOT, "include"),
                         *a.extra, "-o", asm, a.src], check=True, capture_output=True)
         lines = open(asm).read().split("\n")
     files = {}
@@ -102,6 +104,33 @@ def main():
     print(f"{name[:60]}: largest loop body {len(ins)} instructions, VALU {valu}, conditional branches {nbr}")
     for k, v in c.most_common():
         print(f"  {k:20s} {v:6d}")
+    if a.funcs:
+        srcs = {}
+
+        def func_of(lc):
+            if not lc or not lc[0]:
+                return "?"
+            if lc[0] not in srcs:
+                txt = None
+                for d in (os.path.join(ROOT, "include"), os.path.join(ROOT, "motionplanning_amd", "csrc")):
+                    fp = os.path.join(d, lc[0])
+                    if os.path.exists(fp):
+                        txt = open(fp).read().split("\n")
+                srcs[lc[0]] = txt
+            txt = srcs[lc[0]]
+            if txt is None:
+                return lc[0]
+            for i in range(min(lc[1] - 1, len(txt) - 1), -1, -1):
+                m = re.search(r"(?:MPJ_FN|__device__)[^(]*?\b(\w+)\s*\(", txt[i])
+                if m:
+                    return f"{lc[0]}:{m.group(1)}"
+            return lc[0]
+        byf = collections.Counter()
+        for op, lc in zip(ins, locs):
+            if classify(op).startswith(("f64", "v_", "other VALU")):
+                byf[func_of(lc)] += 1
+        for f, v in byf.most_common():
+            print(f"    {v:5d}  {f}")
     if a.lines:
         byline = collections.Counter()
         for op, lc in zip(ins, locs):
