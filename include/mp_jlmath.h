@@ -23,7 +23,7 @@
  *
  * Accuracy vs glibc is checked in tests/test_jlmath.py (CPU) and the GPU
  * implementation is checked bit-exact against the CPU one in
- * tests/test_gpu_parity.py::test_jlmath_bitexact.
+ * tests/test_gpu_mppi.py::test_jlmath_bitexact.
  *
  * This header holds pure functions only; it is NOT the oracle (oracle/ is the
  * reference restatement, and it includes this header for its libm).

@@ -2,9 +2,10 @@
 over the libmpgpu C-ABI (mp_ha_*).
 
 ``defineHybridAstar`` / ``defineHybridAstarobs_`` / ``planHybridAstar_`` keep the reference's
-names and argument meaning.  The search loop runs in the library (C++ host bookkeeping,
-one fused device launch per iteration for the whole batch of scenes: RS_connected +
-the 62-neighbour FindNewNode expansion); ``plan_batch`` runs B scenes in lockstep.
+names and argument meaning.  The search loop runs in the library and is device-resident: per
+iteration one fused launch for the whole batch of scenes (RS_connected + the 62-neighbour
+FindNewNode expansion) and one bookkeeping launch (Dict / open-list updates, popfirst!),
+enqueued without host round trips; ``plan_batch`` runs B scenes in lockstep.
 Setup-time lattice arithmetic (regulate_states, Encode bounds) is exact IEEE
 (round-half-even, fmod), computed here.
 """

@@ -1,8 +1,8 @@
 """Per-kernel VALU rooflines of the iLQR and Hybrid A* legs from a rocprofv3 pass directory.
 
 usage: python tools/pmc_roofline.py DIR > roofline.json
-  DIR/pmc1/run_counter_collection.csv  SQ_INSTS_VALU, SQ_WAVES, SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, ...
-                                       (rocprofv3 --pmc over the bench command with its extras)
+  DIR/pmc4/run_counter_collection.csv  SQ_INSTS_VALU, SQ_WAVES, SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, ...
+                                       (rocprofv3 --pmc over the bench command with its extras; pmc1 if absent)
   DIR/prof/run_kernel_stats.csv        average launch durations (rocprofv3 --kernel-trace --stats of
                                        the same bench command, a separate run)
 
@@ -57,7 +57,8 @@ def durations(path):
 
 
 def main(d):
-    cnt = counters(os.path.join(d, "pmc1", "run_counter_collection.csv"))
+    pm = os.path.join(d, "pmc4", "run_counter_collection.csv")  # gpu_pass3.sh: the bench with its extras
+    cnt = counters(pm if os.path.exists(pm) else os.path.join(d, "pmc1", "run_counter_collection.csv"))
     dur = durations(os.path.join(d, "prof", "run_kernel_stats.csv"))
     out = {"source": d, "peak_wave_insts_per_s": VALU_PEAK, "kernels": {}}
     for k in sorted(set(cnt) | set(dur)):
