@@ -403,17 +403,6 @@ struct IterArgs {
   long long* idx;        // [B][n_prim]
   unsigned char* fr;     // [B][n_prim]
   double* h;             // [B][n_prim]
-  // device-resident search (mp_ha_plan): the Dict lookups of FindNewNode done here, off the
-  // bookkeeping launch's dependent-load chain.  Per neighbour k: hrec[B][n_prim][8] = the existing
-  // node's g, f, seq, Encode index, state (3), and (pos | node id << 32) -- id -1 when the cell has no
-  // node.  The search state cannot change between this launch and the bookkeeping that reads it.
-  const int* nid;        // [B][C] cell -> node id
-  const double *ng, *nf;  // [B][C]
-  const long long *nseq, *nindex;
-  const double* nst;     // [B][C][3]
-  const int* npos;       // [B][C]
-  int C;
-  double* hrec;          // nullptr: no prefetch (the other entry points)
 };
 
 // output addressing: per scene
@@ -585,27 +574,6 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     R.nb[3 * k + 1] = nb[1];
     R.nb[3 * k + 2] = nb[2];
     R.idx[k] = ix;
-    if (A.hrec) {  // FindNewNode's Dict lookup for this neighbour (ha_book reads the record)
-      const size_t sb = (size_t)s * A.C;
-      const int hit = (ix >= 0 && ix < A.C) ? A.nid[sb + ix] : -1;
-      double rec[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-      int pos = -1;
-      if (hit >= 0) {
-        const size_t q = sb + hit;
-        rec[0] = A.ng[q];
-        rec[1] = A.nf[q];
-        rec[2] = __longlong_as_double(A.nseq[q]);
-        rec[3] = __longlong_as_double(A.nindex[q]);
-        rec[4] = A.nst[q * 3];
-        rec[5] = A.nst[q * 3 + 1];
-        rec[6] = A.nst[q * 3 + 2];
-        pos = A.npos[q];
-      }
-      rec[7] = __longlong_as_double((long long)(unsigned)pos | ((long long)hit << 32));
-      double* o = A.hrec + ((size_t)s * P.n_prim + k) * 8;
-#pragma unroll
-      for (int e = 0; e < 8; e++) o[e] = rec[e];
-    }
     g_nb[tid][0] = nb[0];
     g_nb[tid][1] = nb[1];
     g_nb[tid][2] = nb[2];
@@ -980,24 +948,6 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   double bf = __builtin_inf();
   long long bs = 0x7fffffffffffffffLL;
   int bp = -1;
-  // up to 16 entries per thread: every load of the scan in flight at once (one memory round trip),
-  // consumed in position order per thread as the strided loop below does
-  constexpr int SU = 16;
-  if (n_open <= SU * BKT) {
-    double fv[SU];
-    long long sv[SU];
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-      const int p = tid + u * BKT;
-      fv[u] = p < n_open ? Q.of[base + p] : 0.0;
-      sv[u] = p < n_open ? Q.oseq[base + p] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < SU; u++) {
-      const int p = tid + u * BKT;
-      if (p < n_open && (bp < 0 || key_before(fv[u], sv[u], bf, bs))) { bf = fv[u]; bs = sv[u]; bp = p; }
-    }
-  } else
   for (int p0 = tid; p0 < n_open; p0 += 4 * BKT) {
     double fv[4];
     long long sv[4];
@@ -1146,13 +1096,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   long long ix = 0;
   int frk = 0;
   double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
-  double hr[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   if (tid < np) {
-    if (A.hrec) {
-      const double* r = A.hrec + ((size_t)b * np + tid) * 8;
-#pragma unroll
-      for (int e = 0; e < 8; e++) hr[e] = r[e];
-    }
     ix = A.idx[(size_t)b * np + tid];
     frk = A.fr[(size_t)b * np + tid];
     hk = A.h[(size_t)b * np + tid];
@@ -1216,20 +1160,16 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
       th = __builtin_fmax(hk, 0.0);
       if (hk != hk) th = hk;
       tf = tg + th;
-      // the Dict lookup: prefetched by ha_iter_kernel (hrec), else here (two dependent loads)
-      const long long pk = __double_as_longlong(hr[7]);
-      const int hit = A.hrec ? (int)(pk >> 32) : ((ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1);
+      const int hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
       if (hit >= 0) {
         id = hit;
-        const bool pre = A.hrec != nullptr;
-        const double go = pre ? hr[0] : Q.g[base + id];
-        const int po = pre ? (int)(unsigned)(pk & 0xffffffffLL) : Q.pos[base + id];
-        const double fo_ = pre ? hr[1] : Q.f[base + id];
-        const long long so0 = pre ? __double_as_longlong(hr[2]) : Q.seq[base + id];
-        const long long io = pre ? __double_as_longlong(hr[3]) : Q.index[base + id];
-        nst0 = pre ? hr[4] : Q.st[(base + id) * 3];
-        nst1 = pre ? hr[5] : Q.st[(base + id) * 3 + 1];
-        nst2 = pre ? hr[6] : Q.st[(base + id) * 3 + 2];
+        const double go = Q.g[base + id];
+        const int po = Q.pos[base + id];
+        const double fo_ = Q.f[base + id];
+        const long long so0 = Q.seq[base + id], io = Q.index[base + id];
+        nst0 = Q.st[(base + id) * 3];
+        nst1 = Q.st[(base + id) * 3 + 1];
+        nst2 = Q.st[(base + id) * 3 + 2];
         nix = io;
         if (tg < go) {
           if (po >= 0) {
@@ -1727,16 +1667,6 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     A.wtab = wt;
   }
   A.node = Q.node;
-  A.nid = Q.nid;
-  A.ng = Q.g;
-  A.nf = Q.f;
-  A.nseq = Q.seq;
-  A.nindex = Q.index;
-  A.nst = Q.st;
-  A.npos = Q.pos;
-  A.C = Q.C;
-  A.hrec = (double*)mp_ws(ctx, WS_IO9, sizeof(double) * nB * np * 8);
-  if (!A.hrec) return MP_ERR_NOMEM;
   A.scene_of = nullptr;  // slot = scene
   A.active = Q.sc_i + SI_ACTIVE * B;
   A.sc = ctx->ha_states_candi;
