@@ -440,7 +440,10 @@ static_assert(12 % HW == 0, "HA_WAVES must divide the 12 Reeds-Shepp words");
 // plan): 12 waves per block (one Reeds-Shepp word per wave) and 4 neighbours per expansion block
 // (16 blocks per scene: the collision sweep is one pose per thread), so a lone scene's iteration
 // spreads over 17 CUs instead of 5.
-constexpr int HW_TAIL = 12, NBG_TAIL = 4;
+#ifndef HA_NBG_TAIL
+#define HA_NBG_TAIL 4
+#endif
+constexpr int HW_TAIL = 12, NBG_TAIL = HA_NBG_TAIL;
 
 // allpath + findmin split over the block's HW waves: wave w evaluates words WPW·w+1..WPW·(w+1) for
 // its lanes' candidates (lane&3 = variant of the state in `s`), the per-wave winners are
@@ -1697,7 +1700,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // bookkeeping launch, count on the device); the host sizes the grids by the last live count it has
   // seen (an upper bound: it only decreases) and switches to the tail shape once that many scenes
   // fit in about two blocks per CU
-  const int tail_blocks = 512;
+#ifndef HA_TAIL_BLOCKS
+#define HA_TAIL_BLOCKS 512
+#endif
+  const int tail_blocks = HA_TAIL_BLOCKS;
   int known = B;
   int chunk = 0, checked = 0;
   bool finished = false;
