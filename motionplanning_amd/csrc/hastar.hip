@@ -40,10 +40,14 @@ __device__ int* g_ha_dbg;
     if (threadIdx.x == 0)                                                                          \
       reinterpret_cast<unsigned long long*>(g_ha_dbg + 64 * 64)[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
-// bookkeeping-kernel stamps of scene b at [b][16] after the iteration kernel's 4096 blocks
+// bookkeeping-kernel stamps of scene b at [b][16] after the iteration kernel's 4096 blocks, at
+// iteration HA_DBG_IT
+#ifndef HA_DBG_IT
+#define HA_DBG_IT 20
+#endif
 #define BTIME(i)                                                                                   \
   do {                                                                                             \
-    if (threadIdx.x == 0 && it == 20)                                                              \
+    if (threadIdx.x == 0 && it == HA_DBG_IT)                                                       \
       reinterpret_cast<unsigned long long*>(g_ha_dbg + 64 * 64)[(4096 + b) * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else

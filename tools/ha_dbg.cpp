@@ -85,6 +85,15 @@ int main() {
     printf("book stamps (cycles from [0]):");
     for (int i = 1; i < 16; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
     printf("\npops %d\n", pops);
+    // the same after 600 pops (an open list of ~2,000 entries, as late in configs[3]'s longest searches)
+    memset(buf, 0, 1 << 20);
+    p.max_pops = 600;
+    static int64_t seq6[600];
+    static double st6[600 * 3];
+    printf("plan %d\n", mp_ha_plan(ctx, &p, 1, start, goal, walls, &found, &pops, &nn, seq6, &ns, st6, &rl, rs));
+    printf("book stamps at pop %d, %d nodes (cycles from [0]):", pops, nn);
+    for (int i = 1; i < 16; i++) printf(" [%d]%lld", i, t[i] ? (long long)(t[i] - t[0]) : -1LL);
+    printf("\n");
   }
   mp_ctx_destroy(ctx);
   return 0;
