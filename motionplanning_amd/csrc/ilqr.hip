@@ -67,6 +67,10 @@ constexpr int kSearchL = ILQR_SEARCH_L;  // lanes per line-search trial in mp_il
 #define ILQR_ONEPASS_MAX 512
 #endif
 constexpr int kOnePassMax = ILQR_ONEPASS_MAX;  // active instances up to which the search is one pass
+#ifndef ILQR_PIPE
+#define ILQR_PIPE 1
+#endif
+constexpr bool kPipe = ILQR_PIPE;  // overlap each rest pass with the next iteration's round 0
 #ifndef ILQR_SEARCH_G
 #define ILQR_SEARCH_G 16
 #endif
@@ -1375,17 +1379,19 @@ __device__ __forceinline__ void search_accept(const IlqrDev& P, size_t b, double
 // trials G..ls_cap then run all at once in ilqr_search_rest_kernel).
 // L = lanes per trial: 1 (forward_trial on one lane) or 4 (forward_trial_quad: the trial's
 // exponentials and stage sincos spread over a lane quad, ~2.5x shorter chain per trial).
+// skip (pipelined search, may be nullptr): instances whose previous line search is still in its
+// rest pass (they sit this iteration out); n_pend (may be nullptr) counts the instances marked pending.
 template <int G, int L = 1>
-__global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
-                                                         const double* Kg, double* Xs, double* Us, double* Jcur,
-                                                         int* active, int* iters, int* flags, int* n_active,
-                                                         int one_round, int* pending, int* mstar) {
+__device__ __forceinline__ void search_round0(const IlqrDev& P, int B, double* X, double* U, const double* k,
+                                              const double* Kg, double* Xs, double* Us, double* Jcur, int* active,
+                                              int* iters, int* flags, int* n_active, int one_round, int* pending,
+                                              int* mstar, const int* skip, int* n_pend, int bx) {
   constexpr int GL = G * L;     // lanes per instance
   constexpr int IPW = 64 / GL;  // instances per wave
   static_assert(GL <= 64 && 64 % GL == 0, "G*L must divide 64");
   const int lane = threadIdx.x, g = (lane % GL) / L, sub = lane % L, inst = lane / GL;
-  const int b0 = blockIdx.x * IPW + inst;
-  const bool live = b0 < B && active[b0];
+  const int b0 = bx * IPW + inst;
+  const bool live = b0 < B && active[b0] && !(skip && skip[b0]);
   if (__all(!live)) return;
   const size_t b = b0 < B ? b0 : B - 1;
   const size_t N = P.N;
@@ -1454,9 +1460,18 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
   if (searching) {  // one_round only: trials G..ls_cap follow in ilqr_search_rest_kernel
     pending[b] = 1;
     mstar[b] = ms;
+    if (n_pend) atomicAdd(n_pend, 1);
     return;
   }
   search_accept(P, b, J, Jn, mw, Jcur, active, iters, flags, n_active);
+}
+template <int G, int L = 1>
+__global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
+                                                         const double* Kg, double* Xs, double* Us, double* Jcur,
+                                                         int* active, int* iters, int* flags, int* n_active,
+                                                         int one_round, int* pending, int* mstar) {
+  search_round0<G, L>(P, B, X, U, k, Kg, Xs, Us, Jcur, active, iters, flags, n_active, one_round, pending, mstar,
+                      nullptr, nullptr, blockIdx.x);
 }
 
 // Trials first..min(m*, ls_cap) of the pending instances, all at once: block (b, w) runs trials
@@ -1466,19 +1481,18 @@ __global__ __launch_bounds__(64) void ilqr_search_kernel(IlqrDev P, int B, doubl
 // (m* from it in mstar[]); first = 0 is the one-pass search of every active instance (pending =
 // active), each block computing m* itself and block w = 0 publishing it.
 template <int G, int L = 1>
-__global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, const double* X, const double* U,
-                                                              const double* k, const double* Kg, const double* Jcur,
-                                                              const int* pending, int* mstar, double* Xs2,
-                                                              double* Us2, double* Jt, int* winm, int first,
-                                                              size_t T2) {
-  const int b = blockIdx.x, sub = (int)threadIdx.x % L, m = first + (64 / L) * (int)blockIdx.y + (int)threadIdx.x / L;
+__device__ __forceinline__ void search_rest(const IlqrDev& P, int B, const double* X, const double* U,
+                                            const double* k, const double* Kg, const double* Jcur, const int* pending,
+                                            int* mstar, double* Xs2, double* Us2, double* Jt, int* winm, int first,
+                                            size_t T2, int b, int by) {
+  const int sub = (int)threadIdx.x % L, m = first + (64 / L) * by + (int)threadIdx.x / L;
   if (!pending[b]) return;
   const size_t N = P.N, t = (size_t)(m - first);
   int ms;
   if (first == 0) {
     if (m - (int)threadIdx.x / L > P.ls_cap) return;  // the block's first trial (uniform)
     ms = trial_fixpoint<64>(P, U + b * N * 2, k + b * (N - 1) * 2, threadIdx.x);
-    if (blockIdx.y == 0 && threadIdx.x == 0) mstar[b] = ms;
+    if (by == 0 && threadIdx.x == 0) mstar[b] = ms;
   } else {
     ms = mstar[b];
   }
@@ -1497,6 +1511,37 @@ __global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, 
   if (sub != 0) return;
   Jt[(size_t)b * T2 + t] = jt;
   if (!(jt >= Jcur[b]) || m == P.ls_cap || m == ms) atomicMin(winm + b, m);
+}
+template <int G, int L = 1>
+__global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, const double* X, const double* U,
+                                                              const double* k, const double* Kg, const double* Jcur,
+                                                              const int* pending, int* mstar, double* Xs2,
+                                                              double* Us2, double* Jt, int* winm, int first,
+                                                              size_t T2) {
+  search_rest<G, L>(P, B, X, U, k, Kg, Jcur, pending, mstar, Xs2, Us2, Jt, winm, first, T2, blockIdx.x, blockIdx.y);
+}
+
+// The pipelined two-pass search (mp_ilqr_solve): one launch runs round 0 of this iteration for the
+// instances not in a rest pass (blocks [0, n0)) and the rest pass of the instances the previous
+// iteration's round 0 left pending (blocks n0.., instance-major within each 16-trial column), so
+// the rest pass's latency hides under round 0 instead of following it.  An instance's own sequence
+// of operations is unchanged (its next backward pass simply comes one launch later).
+template <int G, int L>
+__global__ __launch_bounds__(64) void ilqr_search_pipe_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
+                                                              const double* Kg, double* Xs, double* Us, double* Jcur,
+                                                              int* active, int* iters, int* flags, int* n_active,
+                                                              int* pend_new, int* mstar_new, int* npend_new,
+                                                              const int* pend_old, int* mstar_old, double* Xs2,
+                                                              double* Us2, double* Jt, int* winm_old, size_t T2,
+                                                              int n0) {
+  const int bx = blockIdx.x;
+  if (bx < n0) {
+    search_round0<G, L>(P, B, X, U, k, Kg, Xs, Us, Jcur, active, iters, flags, n_active, 1, pend_new, mstar_new,
+                        pend_old, npend_new, bx);
+  } else {
+    const int r = bx - n0;
+    search_rest<G, L>(P, B, X, U, k, Kg, Jcur, pend_old, mstar_old, Xs2, Us2, Jt, winm_old, G, T2, r % B, r / B);
+  }
 }
 
 // Accept the winning trial of each pending instance: 64 lanes copy its slot into X/U.
@@ -1766,12 +1811,13 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   double* dXn = (double*)mp_ws(ctx, WS_IO4, sizeof(double) * 4 * N * B * G);
   double* dUn = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 2 * N * B * G);
   double* dJ = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * B);
-  int* dint = (int*)mp_ws(ctx, WS_IO7, sizeof(int) * (4 * (size_t)B + 1));
+  int* dint = (int*)mp_ws(ctx, WS_IO7, sizeof(int) * (4 * (size_t)B + 2));
   if (st || !dk || !dK || !dXn || !dUn || !dJ || !dint) return st ? st : MP_ERR_NOMEM;
   int* dact = dint;
   int* dit = dint + B;
   int* dfl = dint + 2 * B;
-  int* dn = dint + 3 * B;    // [0] active count, [1..B] their compact list (search_accept)
+  int* dnp = dint + 3 * B;   // instances the last pipelined round 0 left pending (host poll, with dn[0])
+  int* dn = dnp + 1;         // [0] active count, [1..B] their compact list (search_accept)
   // trials G..ls_cap in one pass for the instances still searching after round 0 (G = kSearchG only),
   // while their slots fit in 8 GiB, in half of the free device memory and in the context's
   // workspace cap.  Otherwise -- or when allocating them fails -- the G-wide kernel runs its
@@ -1782,12 +1828,12 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
               mp_ws_affordable(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2, 0.5) &&
               mp_ws_affordable(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2, 0.25);
   double *dXs2 = nullptr, *dUs2 = nullptr, *dJt = nullptr;
-  int* dpw = nullptr;  // pending[B], winm[B], mstar[B]
+  int* dpw = nullptr;  // pending[B], winm[B], mstar[B]; pipelined: pend[2][B], winm[2][B], mstar[2][B]
   if (rest) {
     dXs2 = (double*)mp_ws(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2);
     dUs2 = dXs2 ? (double*)mp_ws(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2) : nullptr;
     dJt = dUs2 ? (double*)mp_ws(ctx, WS_IO12, sizeof(double) * B * T2) : nullptr;
-    dpw = dJt ? (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 3 * (size_t)B) : nullptr;
+    dpw = dJt ? (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 6 * (size_t)B) : nullptr;
     if (!dXs2 || !dUs2 || !dJt || !dpw) {
       rest = false;      // fall back to the multi-round 16-wide search
       ctx->err.clear();  // (the failed allocation left a message; mp_ws already cleared the HIP error)
@@ -1796,7 +1842,7 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   const dim3 g1((B + 63) / 64), b1(64);
   hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl, dn + 1);
   MP_HIP(ctx, hipGetLastError());
-  int* hn = (int*)mp_pinned(ctx, 2 * sizeof(int));
+  int* hn = (int*)mp_pinned(ctx, 4 * sizeof(int));
   if (!hn) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
   // One-pass search: once at most kOnePassMax instances are active (the host's last poll), every
   // active instance's trials 0..min(m*, ls_cap) run in one launch (m* = 51..75 measured, so ~4
@@ -1812,21 +1858,30 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   } evp;
   for (int q = 0; q < 2; q++) MP_HIP(ctx, hipEventCreateWithFlags(&evp.e[q], hipEventDisableTiming));
   int n_act = B;  // upper bound on the active count of the iteration being enqueued
+  // hn[2q] = instances left pending by the pipelined round 0 (their rest pass runs in the next
+  // launch, then they rejoin the list), hn[2q + 1] = the list count: their sum bounds the next list
   auto poll = [&](int outer, bool* stop) -> int {
-    MP_HIP(ctx, hipMemcpyAsync(hn + (outer & 1), dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    MP_HIP(ctx, hipMemcpyAsync(hn + 2 * (outer & 1), dnp, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipEventRecord(evp.e[outer & 1], ctx->stream));
     *stop = false;
     if (outer == 0) return MP_OK;
     MP_HIP(ctx, hipEventSynchronize(evp.e[(outer - 1) & 1]));
-    const int nprev = hn[(outer - 1) & 1];
+    const int nprev = hn[2 * ((outer - 1) & 1)] + hn[2 * ((outer - 1) & 1) + 1];
     if (nprev == 0) *stop = true;
     else n_act = nprev;
     return MP_OK;
   };
-  for (int outer = 0; outer <= D.max_iter + 1; outer++) {
+  // pipelined two-pass search (ilqr_search_pipe_kernel): launch q marks pend[q & 1] and runs the rest
+  // pass of pend[(q - 1) & 1]; pend[1] starts empty
+  const bool pipe = rest && kPipe;
+  int q2 = 0;  // two-pass launches so far
+  if (pipe) MP_HIP(ctx, hipMemsetAsync(dpw + B, 0, sizeof(int) * B, ctx->stream));
+  // (an instance in a rest pass sits one launch out, so the pipelined loop may take more launches
+  // than max_iter + 2; each instance still stops at its own max_iter)
+  for (int outer = 0; outer <= 2 * (D.max_iter + 2); outer++) {
     // the derivative and sweep launches cover the active instances only (compact list dn[1..])
     if ((st = run_backward(ctx, D, B, dX, dU, dn + 1, dn, n_act, dk, dK))) return st;
-    MP_HIP(ctx, hipMemsetAsync(dn, 0, sizeof(int), ctx->stream));
+    MP_HIP(ctx, hipMemsetAsync(dnp, 0, 2 * sizeof(int), ctx->stream));
     mp_time_begin(ctx);
     if (rest && n_act <= kOnePassMax) {
       MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));  // winm = 0x7f7f7f7f
@@ -1846,6 +1901,28 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     // G = 16: a lane quad per trial (4 waves per SIMD at B = 4096); the narrower fallbacks one lane
     const int ipw = G == kSearchG ? 64 / (kSearchG * kSearchL) : 64 / G;
     const dim3 gs((unsigned)((B + ipw - 1) / ipw));
+    if (pipe) {
+      const int cur = q2 & 1, old = cur ^ 1;
+      q2++;
+      int *pend_n = dpw + cur * B, *pend_o = dpw + old * B;
+      int *winm_n = dpw + (2 + cur) * B, *winm_o = dpw + (2 + old) * B;
+      int *ms_n = dpw + (4 + cur) * B, *ms_o = dpw + (4 + old) * B;
+      MP_HIP(ctx, hipMemsetAsync(pend_n, 0, sizeof(int) * B, ctx->stream));
+      MP_HIP(ctx, hipMemsetAsync(winm_n, 0x7f, sizeof(int) * B, ctx->stream));  // 0x7f7f7f7f
+      const unsigned ncol = (unsigned)((T2 + 64 / kSearchL - 1) / (64 / kSearchL));
+      hipLaunchKernelGGL((ilqr_search_pipe_kernel<kSearchG, kSearchL>), dim3(gs.x + (unsigned)B * ncol), b1, 0,
+                         ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn, pend_n, ms_n, dnp,
+                         pend_o, ms_o, dXs2, dUs2, dJt, winm_o, T2, (int)gs.x);
+      MP_HIP(ctx, hipGetLastError());
+      hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, pend_o,
+                         ms_o, dXs2, dUs2, dJt, winm_o, dJ, dact, dit, dfl, dn, kSearchG, T2);
+      MP_HIP(ctx, hipGetLastError());
+      mp_time_end(ctx);
+      bool stop;
+      if ((st = poll(outer, &stop))) return st;
+      if (stop) break;
+      continue;
+    }
     if (rest) {
       MP_HIP(ctx, hipMemsetAsync(dpw, 0, sizeof(int) * B, ctx->stream));             // pending
       MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));      // winm = 0x7f7f7f7f
