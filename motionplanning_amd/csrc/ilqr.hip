@@ -1545,24 +1545,31 @@ __global__ __launch_bounds__(64) void ilqr_search_pipe_kernel(IlqrDev P, int B, 
 }
 
 // Accept the winning trial of each pending instance: 64 lanes copy its slot into X/U.
+// reset: after use, clear pending[b] (reset & 1; the pipelined pend arrays, not the active flags of
+// the one-pass search) and set winm[b] back to 0x7f7f7f7f (reset & 2), so that the next launch that
+// uses these arrays needs no memset.
 template <int G>
 __global__ __launch_bounds__(64) void ilqr_search_finish_kernel(IlqrDev P, int B, double* X, double* U,
-                                                                const int* pending, const int* mstar,
+                                                                int* pending, const int* mstar,
                                                                 const double* Xs2, const double* Us2, const double* Jt,
-                                                                const int* winm, double* Jcur, int* active, int* iters,
-                                                                int* flags, int* n_active, int first, size_t T2) {
+                                                                int* winm, double* Jcur, int* active, int* iters,
+                                                                int* flags, int* n_active, int first, size_t T2,
+                                                                int reset = 0) {
   const size_t b = blockIdx.x;
-  if (!pending[b]) return;
-  const size_t N = P.N;
-  const int mw = winm[b];
-  const size_t t = (size_t)(mw - first);
-  const double* Xw = Xs2 + ((size_t)b * T2 + t) * N * 4;
-  const double* Uw = Us2 + ((size_t)b * T2 + t) * N * 2;
-  for (size_t i = threadIdx.x; i < N * 4; i += 64) X[b * N * 4 + i] = Xw[i];
-  for (size_t i = threadIdx.x; i < N * 2; i += 64) U[b * N * 2 + i] = Uw[i];
-  if (threadIdx.x == 0) {
-    const double J = Jcur[b], Jn = Jt[(size_t)b * T2 + t];
-    search_accept(P, b, J, Jn, mw == mstar[b] && Jn >= J ? P.ls_cap : mw, Jcur, active, iters, flags, n_active);
+  if (pending[b]) {
+    const size_t N = P.N;
+    const int mw = winm[b];
+    const size_t t = (size_t)(mw - first);
+    const double* Xw = Xs2 + ((size_t)b * T2 + t) * N * 4;
+    const double* Uw = Us2 + ((size_t)b * T2 + t) * N * 2;
+    for (size_t i = threadIdx.x; i < N * 4; i += 64) X[b * N * 4 + i] = Xw[i];
+    for (size_t i = threadIdx.x; i < N * 2; i += 64) U[b * N * 2 + i] = Uw[i];
+    if (threadIdx.x == 0) {
+      const double J = Jcur[b], Jn = Jt[(size_t)b * T2 + t];
+      search_accept(P, b, J, Jn, mw == mstar[b] && Jn >= J ? P.ls_cap : mw, Jcur, active, iters, flags, n_active);
+      if (reset & 1) pending[b] = 0;
+      if (reset & 2) winm[b] = 0x7f7f7f7f;
+    }
   }
 }
 
@@ -1875,7 +1882,11 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   // pass of pend[(q - 1) & 1]; pend[1] starts empty
   const bool pipe = rest && kPipe;
   int q2 = 0;  // two-pass launches so far
-  if (pipe) MP_HIP(ctx, hipMemsetAsync(dpw + B, 0, sizeof(int) * B, ctx->stream));
+  if (pipe) {  // pend[2][B] = 0, winm[2][B] = 0x7f7f7f7f; afterwards the finish kernels reset what they use
+    MP_HIP(ctx, hipMemsetAsync(dpw, 0, sizeof(int) * 2 * B, ctx->stream));
+    MP_HIP(ctx, hipMemsetAsync(dpw + 2 * B, 0x7f, sizeof(int) * 2 * B, ctx->stream));
+  }
+  bool onepass_armed = false;  // winm of the one-pass search set (then reset by its finish kernels)
   // (an instance in a rest pass sits one launch out, so the pipelined loop may take more launches
   // than max_iter + 2; each instance still stops at its own max_iter)
   for (int outer = 0; outer <= 2 * (D.max_iter + 2); outer++) {
@@ -1884,13 +1895,14 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     MP_HIP(ctx, hipMemsetAsync(dnp, 0, 2 * sizeof(int), ctx->stream));
     mp_time_begin(ctx);
     if (rest && n_act <= kOnePassMax) {
-      MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));  // winm = 0x7f7f7f7f
+      if (!onepass_armed) MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));  // winm
+      onepass_armed = true;
       hipLaunchKernelGGL((ilqr_search_rest_kernel<kSearchG, kSearchL>),
                          dim3((unsigned)B, (unsigned)((T2 + 64 / kSearchL - 1) / (64 / kSearchL))), b1, 0, ctx->stream, D,
                          B, dX, dU, dk, dK, dJ, dact, dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, 0, T2);
       MP_HIP(ctx, hipGetLastError());
       hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dact,
-                         dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, 0, T2);
+                         dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, 0, T2, 2);
       MP_HIP(ctx, hipGetLastError());
       mp_time_end(ctx);
       bool stop;
@@ -1905,17 +1917,15 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
       const int cur = q2 & 1, old = cur ^ 1;
       q2++;
       int *pend_n = dpw + cur * B, *pend_o = dpw + old * B;
-      int *winm_n = dpw + (2 + cur) * B, *winm_o = dpw + (2 + old) * B;
-      int *ms_n = dpw + (4 + cur) * B, *ms_o = dpw + (4 + old) * B;
-      MP_HIP(ctx, hipMemsetAsync(pend_n, 0, sizeof(int) * B, ctx->stream));
-      MP_HIP(ctx, hipMemsetAsync(winm_n, 0x7f, sizeof(int) * B, ctx->stream));  // 0x7f7f7f7f
+      int* winm_o = dpw + (2 + old) * B;  // pend_n is 0 and winm[cur] 0x7f7f7f7f: reset by the finish
+      int *ms_n = dpw + (4 + cur) * B, *ms_o = dpw + (4 + old) * B;  // kernel that last used them
       const unsigned ncol = (unsigned)((T2 + 64 / kSearchL - 1) / (64 / kSearchL));
       hipLaunchKernelGGL((ilqr_search_pipe_kernel<kSearchG, kSearchL>), dim3(gs.x + (unsigned)B * ncol), b1, 0,
                          ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn, pend_n, ms_n, dnp,
                          pend_o, ms_o, dXs2, dUs2, dJt, winm_o, T2, (int)gs.x);
       MP_HIP(ctx, hipGetLastError());
       hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, pend_o,
-                         ms_o, dXs2, dUs2, dJt, winm_o, dJ, dact, dit, dfl, dn, kSearchG, T2);
+                         ms_o, dXs2, dUs2, dJt, winm_o, dJ, dact, dit, dfl, dn, kSearchG, T2, 3);
       MP_HIP(ctx, hipGetLastError());
       mp_time_end(ctx);
       bool stop;
