@@ -157,3 +157,30 @@ def test_solve_configs2_horizon_bitexact(ctx):
         assert np.array_equal(X[b], Xo) and np.array_equal(U[b], Uo)
         stalled += bool(flags & 1)
     assert stalled > 0  # the rest pass (trials 16..max_ls) was exercised
+
+
+def test_solve_pipelined_search_bitexact(ctx):
+    """mp_ilqr_solve's pipelined line search on a batch large enough to stay in it for many
+    iterations (2048 instances: > 512 active): each iteration's rest pass runs in the next launch
+    beside round 0, the instances it holds sit one backward pass out, and the switch to the one-pass
+    search happens while some are still pending.  Every instance's iteration count, cost, states and
+    controls must equal the oracle's sequential loop."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    B, N = 2048, 20
+    p = ilqr.params(N=N, max_iter=60)
+    x0, U0 = ilqr.cfg3_instances(B, N, seed=11)
+    X0, _ = ilqr.ilqr_rollout(p, x0, U0, ctx=ctx)
+    X, U, J, it, ok = ilqr.ilqr_solve(p, X0, U0, ctx=ctx)
+
+    def ref(b):
+        return oracle.ilqr_solve(p, X0[b], U0[b])
+
+    with ThreadPoolExecutor(16) as ex:
+        refs = list(ex.map(ref, range(B)))
+    stalled = 0
+    for b, (Xo, Uo, Jo, ito, flags) in enumerate(refs):
+        assert it[b] == ito and (J[b] == Jo or (J[b] != J[b] and Jo != Jo)), (b, it[b], ito)
+        assert np.array_equal(X[b], Xo) and np.array_equal(U[b], Uo)
+        stalled += bool(flags & 1)
+    assert stalled > 0 and int(it.max()) > 10
