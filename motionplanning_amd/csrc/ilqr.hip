@@ -71,6 +71,10 @@ constexpr int kOnePassMax = ILQR_ONEPASS_MAX;  // active instances up to which t
 #define ILQR_PIPE 1
 #endif
 constexpr bool kPipe = ILQR_PIPE;  // overlap each rest pass with the next iteration's round 0
+#ifndef ILQR_DERIV4_MAX
+#define ILQR_DERIV4_MAX 2048
+#endif
+constexpr int kDeriv4Max = ILQR_DERIV4_MAX;  // derivative launches for at most this many instances: 4 lanes each
 #ifndef ILQR_SEARCH_G
 #define ILQR_SEARCH_G 16
 #endif
@@ -246,6 +250,9 @@ __device__ __forceinline__ double cst(int variant, const double* s, const SigCac
 // consecutive threads store consecutive doubles); every loop is unrolled so the perturbed
 // states stay in registers (no scratch).
 template <bool F>
+__device__ __forceinline__ void knot_cost_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
+                                                 size_t stride, int& bad);
+template <bool F>
 __device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
                                             size_t stride, int& bad) {
   const double e = P.eps;
@@ -275,7 +282,17 @@ __device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, c
 #pragma unroll
     for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 1) = (fp[r] - fm[r]) / (2 * e);
   }
-  // ---- cost derivatives: lx 24, lu 28, lxx 30, luu 46, lux 50
+  knot_cost_derivs<F>(P, s, u, out, stride, bad);
+#undef DOUT
+}
+
+// the cost derivatives of knot_derivs (GetMatrix.jl CalculateMatrix): lx 24, lu 28, lxx 30, luu 46, lux 50
+template <bool F>
+__device__ __forceinline__ void knot_cost_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
+                                                 size_t stride, int& bad) {
+  const double e = P.eps;
+#define DOUT(q) out[(size_t)(q) * stride]
+  double sp[4], sm[4];
   SigCache C;
   C.a[0] = u[0] - 2 * e; C.a[1] = u[0] - e; C.a[2] = u[0]; C.a[3] = u[0] + e; C.a[4] = u[0] + 2 * e;
   C.d[0] = u[1] - 2 * e; C.d[1] = u[1] - e; C.d[2] = u[1]; C.d[3] = u[1] + e; C.d[4] = u[1] + 2 * e;
@@ -364,6 +381,72 @@ __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const
     int d = 0;
     knot_derivs<false>(P, s, u, out, (size_t)B, d);
   }
+}
+
+// knot_derivs split four ways for the latency-bound launches (few active instances): part 0 / 1
+// the dynamics Jacobian's state columns 0-1 / 2-3, part 2 its control columns, part 3 the cost
+// derivatives -- the same operations on the same operands per output as knot_derivs (exact libm),
+// so the same bits, on four lanes instead of one.
+template <int PART>
+__device__ __forceinline__ void knot_derivs_part(const IlqrDev& P, const double* s, const double* u, double* out,
+                                                 size_t stride) {
+  const double e = P.eps;
+  int bad = 0;
+#define DOUT(q) out[(size_t)(q) * stride]
+  if (PART <= 1) {
+    const UPre q0 = upre<false>(u[1], bad);
+    double sp[4], sm[4], fp[4], fm[4];
+#pragma unroll
+    for (int i = 2 * PART; i < 2 * PART + 2; i++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
+      sp[i] = s[i] + e;
+      sm[i] = s[i] - e;
+      rk4<false>(sp, u[0], q0, P.dT, fp, bad);
+      rk4<false>(sm, u[0], q0, P.dT, fm, bad);
+#pragma unroll
+      for (int r = 0; r < 4; r++) DOUT(4 * r + i) = (fp[r] - fm[r]) / (2 * e);
+    }
+  } else if (PART == 2) {
+    const UPre q0 = upre<false>(u[1], bad);
+    double fp[4], fm[4];
+    rk4<false>(s, u[0] + e, q0, P.dT, fp, bad);
+    rk4<false>(s, u[0] - e, q0, P.dT, fm, bad);
+#pragma unroll
+    for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 0) = (fp[r] - fm[r]) / (2 * e);
+    const UPre qp = upre<false>(u[1] + e, bad), qm = upre<false>(u[1] - e, bad);
+    rk4<false>(s, u[0], qp, P.dT, fp, bad);
+    rk4<false>(s, u[0], qm, P.dT, fm, bad);
+#pragma unroll
+    for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 1) = (fp[r] - fm[r]) / (2 * e);
+  } else {
+    knot_cost_derivs<false>(P, s, u, out, stride, bad);
+  }
+#undef DOUT
+}
+
+// ilqr_deriv_kernel with four waves per 64 records (knot_derivs_part: wave w of a block evaluates
+// part w of records 64·blockIdx.x + lane, a wave-uniform role), for launches whose active count
+// leaves most of the chip idle.
+__global__ __launch_bounds__(256) void ilqr_deriv4_kernel(IlqrDev P, int B, const double* X, const double* U,
+                                                          const int* list, const int* n_dev, int nmax, double* D) {
+  const int n = n_dev ? *n_dev : nmax;
+  const long long Bn = (long long)n * (P.N - 1);
+  if ((long long)blockIdx.x * 64 >= Bn) return;  // block-uniform: past the live records
+  long long t = (long long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const int part = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (t >= Bn) t = Bn - 1;  // tail lanes recompute the last knot (identical values)
+  const int j = (int)(t / n), i = (int)(t % n);
+  const int b = list ? list[i] : i;
+  const double* xs = X + ((size_t)b * P.N + j) * 4;
+  const double* us = U + ((size_t)b * P.N + j) * 2;
+  const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
+  const double u[2] = {us[0], us[1]};
+  double* out = D + (size_t)j * ND * B + i;
+  if (part == 0) knot_derivs_part<0>(P, s, u, out, (size_t)B);
+  else if (part == 1) knot_derivs_part<1>(P, s, u, out, (size_t)B);
+  else if (part == 2) knot_derivs_part<2>(P, s, u, out, (size_t)B);
+  else knot_derivs_part<3>(P, s, u, out, (size_t)B);
 }
 
 // pinv of a 2x2: Julia's LinearAlgebra.pinv through LAPACK dgesdd's 2x2 path (mp_jlmath.h
@@ -1663,8 +1746,12 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
   double* dD = (double*)mp_ws(ctx, WS_ILQR0, sizeof(double) * (size_t)B * (D.N - 1) * ND);  // knot stride ND*B
   if (!dD) return MP_ERR_NOMEM;
   mp_time_begin(ctx);  // the timed region covers both kernels of the backward pass
-  hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
-                     list, n_dev, na, dD);
+  if (na <= kDeriv4Max)  // few active instances: four lanes per record (latency-bound launch)
+    hipLaunchKernelGGL(ilqr_deriv4_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, ctx->stream, D, B, dX,
+                       dU, list, n_dev, na, dD);
+  else
+    hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
+                       list, n_dev, na, dD);
   MP_HIP(ctx, hipGetLastError());
 #if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR) && !defined(MP_ILQR_STAGED)
   hipLaunchKernelGGL(ilqr_backward_quad_kernel, dim3((na + kQuadIPB - 1) / kQuadIPB), dim3(128),
