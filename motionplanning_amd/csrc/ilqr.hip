@@ -1,17 +1,23 @@
 // ilqr.hip — batched iLQR (OptimalControl/ILQR/{Dynamics,Cost,GetMatrix,ILQR}.jl and
 // the PathPlanning/Parking_ILQR variant) for gfx950 + C-ABI entry points.
 //
-// Per outer iteration (ILQR.jl:44-88) for B instances:
-//   ilqr_deriv_kernel     one thread per (instance, knot j): LocallyLinearizeDynamics
-//                         (12 RK4) and CalculateMatrix (130 StageCost evaluations) by
-//                         finite differences.  Control-only sub-expressions (tan δ, β,
-//                         cos β, the two sigmoid barriers) are evaluated once per distinct
-//                         perturbed control and reused: the same function of the same bits,
-//                         so every derivative is bit-identical to the scalar restatement.
-//                         405,504 independent threads at configs[2] (B=4096, N=100).
-//   ilqr_backward_kernel  one thread per instance: the Riccati sweep j = N-2..0 (ILQR.jl:46-67).
-//   ilqr_search_kernel    one thread per instance: halving line search + accept (ILQR.jl:70-86).
-// The host loops until every instance has met |ΔJ/J| <= tol.
+// Per outer iteration (ILQR.jl:44-88) for the active instances of a batch:
+//   ilqr_deriv_kernel / ilqr_deriv4_kernel   LocallyLinearizeDynamics (12 RK4) and CalculateMatrix
+//                         (130 StageCost evaluations) by finite differences for every (instance,
+//                         knot): one thread per record, or -- launches with few active instances --
+//                         four waves per 64 records, one part of the derivatives each.  Control-only
+//                         sub-expressions (tan δ, β, cos β, the sigmoid barriers) are evaluated once
+//                         per distinct perturbed control and reused: the same function of the same
+//                         bits, so every derivative is bit-identical to the scalar restatement.
+//   ilqr_backward_quad_kernel   the Riccati sweep j = N-2..0 (ILQR.jl:46-67) on a lane quad per
+//                         instance, fed from LDS by a loader wave; Julia's pinv (LAPACK's 2x2 path).
+//   line search (ILQR.jl:70-86), trial m at α = 2^-m on a lane quad: round 0 (16 trials per
+//                         instance at once), then the trials 16..m* of the instances still searching
+//                         all at once in the next launch (ilqr_search_pipe_kernel: beside the next
+//                         iteration's round 0) and ilqr_search_finish_kernel (accept); with few
+//                         instances left, every trial 0..m* in one pass.  The accepted trial is the
+//                         first that would end the sequential loop, so the results are the loop's.
+// The host loops until every instance has met |ΔJ/J| <= tol (or its max_iter).
 #include "../../include/mp_jlmath.h"
 #include "runtime.hpp"
 
