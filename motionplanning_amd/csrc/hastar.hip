@@ -1134,25 +1134,53 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
     return;
   }
   BTIME(2);
+  // ---- FindNewNode (:391-447): only the first valid occurrence of an Encode index in this
+  // expansion can change anything (every neighbour has the same tentative g).  Lane k of wave 0 is
+  // neighbour k; it is a duplicate when an earlier valid lane holds the same Encode index.  The 64
+  // comparisons per lane are split over the block's four waves (wave w: earlier lanes 16w..16w+15,
+  // broadcast LDS reads), while wave 0 already loads the Dict entries of its valid lanes (loads
+  // only: the Dict changes after the check), so their latency overlaps the check.
+  __shared__ long long s_vix[64];
+  __shared__ int s_dup[BKT / 64][64];
+  static_assert(BKT == 256, "the duplicate check below ORs four wave partials");
+  const bool valid = tid < np && ix != 0 && frk;
+  if (tid < 64) s_vix[tid] = valid ? ix : 0;
+  __syncthreads();
+  {
+    const int w = tid >> 6;
+    const long long key = s_vix[lane];  // lane's own index if valid, else 0 (never a duplicate then)
+    bool d = false;
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) {  // unconditional reads: no exec-masked branch per j
+      const int j = 16 * w + jj;
+      const long long oj = s_vix[j];
+      d = d | ((oj == key) & (j < lane) & (key != 0));
+    }
+    s_dup[w][lane] = d;
+  }
+  int hit = -1;
+  double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
+  int po = 0;
+  long long so0 = 0, io = 0;
+  if (valid) {  // wave 0: the Dict entry of every valid lane (used by the first occurrences below)
+    hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
+    if (hit >= 0) {
+      gd = Q.g[base + hit];
+      po = Q.pos[base + hit];
+      fo_ = Q.f[base + hit];
+      so0 = Q.seq[base + hit];
+      io = Q.index[base + hit];
+      dst0 = Q.st[(base + hit) * 3];
+      dst1 = Q.st[(base + hit) * 3 + 1];
+      dst2 = Q.st[(base + hit) * 3 + 2];
+    }
+  }
+  BTIME(8);
+  __syncthreads();
   if (tid < 64) {
-    // ---- FindNewNode (:391-447): only the first valid occurrence of an Encode index in this
-    // expansion can change anything (every neighbour has the same tentative g)
     int n_open = n_open0;
     const int k = lane;
-    const bool valid = k < np && ix != 0 && frk;
-    const long long vix = valid ? ix : 0;
-    BTIME(8);
-    // lane k is a duplicate when an earlier valid lane holds the same Encode index: every lane reads
-    // the 64 indices from LDS (uniform addresses: broadcast reads, all independent)
-    __shared__ long long s_vix[64];
-    s_vix[k] = vix;
-    __builtin_amdgcn_wave_barrier();
-    bool dup = false;
-#pragma unroll 16
-    for (int j = 0; j < 64; j++) {  // unconditional reads: no exec-masked branch per j
-      const long long oj = s_vix[j];
-      dup = dup | ((oj == ix) & (j < k));
-    }
+    const bool dup = s_dup[0][k] | s_dup[1][k] | s_dup[2][k] | s_dup[3][k];
     const bool first = valid && !dup;
     BTIME(3);
     const double tg = cur_g + P.expand_time;
@@ -1167,18 +1195,13 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
       th = __builtin_fmax(hk, 0.0);
       if (hk != hk) th = hk;
       tf = tg + th;
-      const int hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
       if (hit >= 0) {
         id = hit;
-        const double go = Q.g[base + id];
-        const int po = Q.pos[base + id];
-        const double fo_ = Q.f[base + id];
-        const long long so0 = Q.seq[base + id], io = Q.index[base + id];
-        nst0 = Q.st[(base + id) * 3];
-        nst1 = Q.st[(base + id) * 3 + 1];
-        nst2 = Q.st[(base + id) * 3 + 2];
+        nst0 = dst0;
+        nst1 = dst1;
+        nst2 = dst2;
         nix = io;
-        if (tg < go) {
+        if (tg < gd) {
           if (po >= 0) {
             chg = true;
             fo = fo_;
