@@ -536,12 +536,16 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   __shared__ int sh_n;
   const int per = 1 + (P.n_prim + NBG - 1) / NBG;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
-  if (slot >= (A.n_live ? *A.n_live : A.n_active)) return false;  // past the live-scene list
+  // the live count and the slot's scene are independent loads (slot < the grid's bound <= B keeps the
+  // list read in bounds); a scene on the bookkeeping's list (n_live set) is live, so its flag is not
+  // read: the node and goal loads then follow one round trip instead of three
+  const int n_live = A.n_live ? *A.n_live : A.n_active;
+  const int s = A.scene_of ? A.scene_of[slot] : slot;
+  if (slot >= n_live) return false;  // past the live-scene list
   if (item == 0 && !A.do_rs) return false;
   if (item > 0 && !A.do_exp) return false;
   const bool rs = item == 0;  // block-uniform role: RS_connected, else a 16-neighbour group
-  const int s = A.scene_of ? A.scene_of[slot] : slot;
-  if (A.active && !A.active[s]) return false;  // scene finished (device-resident search)
+  if (!A.n_live && A.active && !A.active[s]) return false;  // scene finished (device-resident search)
   const int tid = threadIdx.x, lane = tid & 63;
   HMARK(1);
   HTIME(0);
