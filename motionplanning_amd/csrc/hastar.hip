@@ -628,10 +628,11 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     HTIME(2);
     cb = rs_best_split<true, HWt>(ns, tid, &best, red_c, red_i, cmd);
     HTIME(3);
-    // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment, all segments
-    // at once -- the heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt over every step (one lane),
-    // the per-step increments (all lanes), then the x and y running sums (one lane each, two
-    // waves): the same operations in the same order as segment by segment
+    // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment -- per segment the
+    // heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt, the per-step increments, then the x and y
+    // running sums -- software-pipelined over the segments: stage k runs segment k's heading, segment
+    // k-1's increments and segment k-2's running sums, each on its own threads, so the serial chains
+    // of different segments overlap.  The same operations in the same order per value.
     __syncthreads();  // cmd (written by the winning lane) visible
     int nseg = 0;
     for (int i = 0; i < 5; i++) {
@@ -639,73 +640,83 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       nseg++;
     }
     const int nst = 100 * nseg;
-    // the heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt, segment by segment: all 100 steps at once when
-    // the closed form of repeated addition applies (mpj_rep_add_ok: same bits), else on one lane
-    if (tid == 0) psi_s[0] = node[2];
-    __syncthreads();
-    for (int seg = 0; seg < nseg; seg++) {
-      const double q0 = psi_s[seg * 100];
-      const double dt = __builtin_fabs(cmd[seg * 3]) / 100;
-      const double c = (cmd[seg * 3 + 2] * cmd[seg * 3 + 1]) * dt;
-      double d;
-      if (mpj_rep_add_ok(q0, c, 100, &d)) {
-        for (int k = tid; k < 100; k += HT) psi_s[seg * 100 + k + 1] = c == 0.0 ? q0 + c : mpj_fma(k + 1, d, q0);
-      } else if (tid == 0) {
-        double q = q0;
-        for (int k = 0; k < 100; k++) {
-          q = q + c;
-          psi_s[seg * 100 + k + 1] = q;
-        }
-      }
-      __syncthreads();
-    }
-    HTIME(6);
-    for (int t = tid; t < nst; t += HT) {  // per-step increments
-      const int seg = t / 100;
-      const double dt = __builtin_fabs(cmd[seg * 3]) / 100, v = cmd[seg * 3 + 1];
-      double sn, cs;
-      mpj_sincos_bl(psi_s[t], &sn, &cs);
-      double d0 = v * cs, d1 = v * sn;
-      d0 = d0 * P.minR;
-      d1 = d1 * P.minR;
-      ix_s[t] = d0 * dt;
-      iy_s[t] = d1 * dt;
-      path_s[3 * (t + 1) + 2] = psi_s[t + 1];
-    }
+    constexpr int TP = 128, TW = 192;  // the serial heading's thread; the first increment thread
+    static_assert(HT > TW, "the pipelined createActPath needs four waves");
     if (tid == 0) {
+      psi_s[0] = node[2];
       path_s[0] = node[0];
       path_s[1] = node[1];
     }
     __syncthreads();
-    HTIME(7);
-    // running sums in order, segment by segment: a straight segment (every increment the same bits)
-    // in closed form, else x on wave 0's first lane and y on wave 1's
-    for (int seg = 0; seg < nseg; seg++) {
-      const int t0 = seg * 100;
-      const double x0 = path_s[3 * t0], y0 = path_s[3 * t0 + 1];
-      const double ix = ix_s[t0], iy = iy_s[t0];
-      const bool same = __double_as_longlong(psi_s[t0]) == __double_as_longlong(psi_s[t0 + 1]) &&
-                        cmd[seg * 3 + 2] * cmd[seg * 3 + 1] == 0.0;  // ψ constant over the segment
-      double dx, dy;
-      const bool cx = same && mpj_rep_add_ok(x0, ix, 100, &dx), cy = same && mpj_rep_add_ok(y0, iy, 100, &dy);
-      for (int k = tid; k < 100; k += HT) {
-        if (cx) path_s[3 * (t0 + k + 1)] = ix == 0.0 ? x0 + ix : mpj_fma(k + 1, dx, x0);
-        if (cy) path_s[3 * (t0 + k + 1) + 1] = iy == 0.0 ? y0 + iy : mpj_fma(k + 1, dy, y0);
+    for (int st = 0; st < nseg + 2; st++) {
+      {  // segment st: the heading recurrence, all 100 steps at once when the closed form of repeated
+         // addition applies (mpj_rep_add_ok: same bits, block-uniform), else on thread TP
+        const int seg = st;
+        if (seg < nseg) {
+          const double q0 = psi_s[seg * 100];
+          const double dt = __builtin_fabs(cmd[seg * 3]) / 100;
+          const double c = (cmd[seg * 3 + 2] * cmd[seg * 3 + 1]) * dt;
+          double d;
+          if (mpj_rep_add_ok(q0, c, 100, &d)) {
+            for (int k = tid - TW; k >= 0 && k < 100; k += HT - TW)
+              psi_s[seg * 100 + k + 1] = c == 0.0 ? q0 + c : mpj_fma(k + 1, d, q0);
+          } else if (tid == TP) {
+            double q = q0;
+            for (int k = 0; k < 100; k++) {
+              q = q + c;
+              psi_s[seg * 100 + k + 1] = q;
+            }
+          }
+        }
       }
-      if ((tid == 0 && !cx) || (tid == 64 && !cy)) {
-        const int c = tid == 0 ? 0 : 1;
-        const double* inc = c == 0 ? ix_s : iy_s;
-        double acc = c == 0 ? x0 : y0;
-        // batches of 20 increments into registers first: the LDS reads then pipeline instead of
-        // each waiting behind the previous path store (the compiler cannot disprove aliasing)
-        for (int u0 = t0; u0 < t0 + 100; u0 += 20) {
-          double v[20];
+      {  // segment st-1: the per-step increments
+        const int seg = st - 1;
+        if (seg >= 0 && seg < nseg) {
+          const double dt = __builtin_fabs(cmd[seg * 3]) / 100, v = cmd[seg * 3 + 1];
+          for (int k = tid - TW; k >= 0 && k < 100; k += HT - TW) {
+            const int t = seg * 100 + k;
+            double sn, cs;
+            mpj_sincos_bl(psi_s[t], &sn, &cs);
+            double d0 = v * cs, d1 = v * sn;
+            d0 = d0 * P.minR;
+            d1 = d1 * P.minR;
+            ix_s[t] = d0 * dt;
+            iy_s[t] = d1 * dt;
+            path_s[3 * (t + 1) + 2] = psi_s[t + 1];
+          }
+        }
+      }
+      {  // segment st-2: the running sums in order, a straight segment (every increment the same bits)
+         // in closed form, else x on thread 0 and y on thread 64
+        const int seg = st - 2;
+        if (seg >= 0 && seg < nseg) {
+          const int t0 = seg * 100;
+          const double x0 = path_s[3 * t0], y0 = path_s[3 * t0 + 1];
+          const double ix = ix_s[t0], iy = iy_s[t0];
+          const bool same = __double_as_longlong(psi_s[t0]) == __double_as_longlong(psi_s[t0 + 1]) &&
+                            cmd[seg * 3 + 2] * cmd[seg * 3 + 1] == 0.0;  // ψ constant over the segment
+          double dx, dy;
+          const bool cx = same && mpj_rep_add_ok(x0, ix, 100, &dx), cy = same && mpj_rep_add_ok(y0, iy, 100, &dy);
+          for (int k = tid - TW; k >= 0 && k < 100; k += HT - TW) {
+            if (cx) path_s[3 * (t0 + k + 1)] = ix == 0.0 ? x0 + ix : mpj_fma(k + 1, dx, x0);
+            if (cy) path_s[3 * (t0 + k + 1) + 1] = iy == 0.0 ? y0 + iy : mpj_fma(k + 1, dy, y0);
+          }
+          if ((tid == 0 && !cx) || (tid == 64 && !cy)) {
+            const int c = tid == 0 ? 0 : 1;
+            const double* inc = c == 0 ? ix_s : iy_s;
+            double acc = c == 0 ? x0 : y0;
+            // batches of 20 increments into registers first: the LDS reads then pipeline instead of
+            // each waiting behind the previous path store (the compiler cannot disprove aliasing)
+            for (int u0 = t0; u0 < t0 + 100; u0 += 20) {
+              double v[20];
 #pragma unroll
-          for (int u = 0; u < 20; u++) v[u] = inc[u0 + u];
+              for (int u = 0; u < 20; u++) v[u] = inc[u0 + u];
 #pragma unroll
-          for (int u = 0; u < 20; u++) {
-            acc = acc + v[u];
-            path_s[3 * (u0 + u + 1) + c] = acc;
+              for (int u = 0; u < 20; u++) {
+                acc = acc + v[u];
+                path_s[3 * (u0 + u + 1) + c] = acc;
+              }
+            }
           }
         }
       }
