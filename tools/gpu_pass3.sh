@@ -25,7 +25,7 @@ rc=$?
 echo "chain exit $rc"; tail -c 3000 $O/bench.log
 [ $rc -ne 0 ] && exit $rc
 # N>1 rehearsal of the driver's launch (bench.py --gpus 2 spawns two ranks; both on cuda:0, gloo)
-timeout -k 10 300 python bench.py --gpus 2 --share-device --steps 10 --warmup 2 --no-cpu --no-extras > $O/bench_n2.log 2>&1
+timeout -k 10 400 python bench.py --gpus 2 --share-device --steps 10 --warmup 2 --no-cpu > $O/bench_n2.log 2>&1
 rc=$?
 echo "n2 exit $rc"; tail -c 1500 $O/bench_n2.log
 exit $rc
