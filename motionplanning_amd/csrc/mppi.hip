@@ -87,6 +87,10 @@ struct PlanArgs {
   const int* live;                  // closed loop: scenes with live[s] == 0 are skipped (null: all run)
 };
 
+#ifndef MPPI_NT_CTRL
+#define MPPI_NT_CTRL 0
+#endif
+
 // Snapshot record of one scene for the deferred final rollout (final_stream = 1), in doubles:
 // [0, 2H) MPPICtrl | [2H, 4H) U_nom | X0[7] | goal[2] | obstacles[3 n_obs] | grid bytes | ran
 // `ran` (1.0 / 0.0) is written by the plan kernel of the same call: whether it planned the scene.
@@ -262,7 +266,13 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     auto store = [&](int j, const double* u) {
       if (LPR == 2) {
         if (ush) ush[pair * ustr + 2 * j + side] = u[side];
-        if (ctrl_g) ctrl_g[(size_t)j * K * 2] = u[side];
+        if (ctrl_g) {
+#if MPPI_NT_CTRL
+          __builtin_nontemporal_store(u[side], ctrl_g + (size_t)j * K * 2);
+#else
+          ctrl_g[(size_t)j * K * 2] = u[side];
+#endif
+        }
       } else {
         if (ush) {
           ush[pair * ustr + 2 * j] = u[0];

@@ -261,18 +261,27 @@ struct TrajOut {
 };
 
 // The even lane of the pair stores x[0..3], the odd lane x[4..6] (LPR 1: the lane all 7).
+// TrajectoryCollection states are written once and read only by the caller: non-temporal stores
+// (streaming, no L2 residency) -- 1.5-2 % off the 8-scene plan kernel (profiles/r03nt2_mppi_nt_ab.txt).
+#ifndef MPPI_NT_STATE
+#define MPPI_NT_STATE 1
+#endif
+__device__ __forceinline__ void st_state(double* a, double v) {
+  if (MPPI_NT_STATE) __builtin_nontemporal_store(v, a);
+  else *a = v;
+}
 template <int LPR = 2>
 __device__ __forceinline__ void store_state(const TrajOut& T, int j, const double* x, int side) {
   double* q = T.p + (long long)j * T.rs;
   if (LPR == 1) {
 #pragma unroll
-    for (int i = 0; i < 7; i++) q[(long long)i * T.cs] = x[i];
+    for (int i = 0; i < 7; i++) st_state(q + (long long)i * T.cs, x[i]);
     return;
   }
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double v = MPJ_SEL(side, x[4 + i < 7 ? 4 + i : 6], x[i]);
-    if (!side || i < 3) q[(long long)(side ? 4 + i : i) * T.cs] = v;
+    if (!side || i < 3) st_state(q + (long long)(side ? 4 + i : i) * T.cs, v);
   }
 }
 
