@@ -398,6 +398,8 @@ struct IterArgs {
   const int* n_live;     // device count of the scene_of list (nullptr: n_active)
   int n_active;
   int do_rs, do_exp;
+  int rs_path_free_only;  // RS_connected writes its path only when it is collision-free (the planner
+                          // reads it only then); the standalone entry point writes every path
   // RS_connected outputs (per scene)
   unsigned char* rs_ok;  // [B]
   double* rs_path;       // [B][501][3]
@@ -726,7 +728,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     if (tid == 0) path_s[2] = node[2];
     __syncthreads();
     const int n = nst + 1;
-    for (int i = tid; i < 3 * n; i += HT) R.path[i] = path_s[i];
+    if (!A.rs_path_free_only)
+      for (int i = tid; i < 3 * n; i += HT) R.path[i] = path_s[i];
     if (tid == 0) sh_n = n;
     HTIME(4);
     sweep(n > 5 ? (n - 1) / 5 + 1 : 1);  // block_collision_check on poses 1:5:end
@@ -756,6 +759,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       *R.ok = (unsigned char)g_free[0];
       *R.len = sh_n;
     }
+    if (A.rs_path_free_only && g_free[0])  // block-uniform (after the barrier above)
+      for (int i = tid; i < 3 * sh_n; i += HT) R.path[i] = path_s[i];
   } else if (tid < 64 && (lane & 3) == 0 && j < nk) {
     const int fr = g_ix[j] != 0 && g_free[j];
     R.fr[k0 + j] = (unsigned char)fr;
@@ -1718,6 +1723,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.pc = ctx->ha_paths_candi;
   A.do_rs = 1;
   A.do_exp = 1;
+  A.rs_path_free_only = 1;
   A.n_active = B;
   MP_HIP(ctx, hipMemsetAsync(Q.pop_seq, 0xff, nB * mp * 8, ctx->stream));  // -1 past each scene's pops
   MP_HIP(ctx, hipMemsetAsync(Q.live, 0, sizeof(int) * (mp + 2), ctx->stream));
