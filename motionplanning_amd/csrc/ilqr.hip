@@ -1270,6 +1270,9 @@ __device__ double forward_trial(const IlqrDev& P, const double* X, const double*
   return J + terminal(P.variant, x);
 }
 
+#ifndef ILQR_FWD_NOSTORE
+#define ILQR_FWD_NOSTORE 0  // timing probe only: the forward kernel's trajectory stores off
+#endif
 // Broadcast lane j of each quad to the quad (DPP quad_perm [j,j,j,j]).
 template <int J>
 __device__ __forceinline__ double quad_bcast(double v) {
@@ -1292,9 +1295,11 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
   const double la = 1.56, lb = 1.64, dT = P.dT;
   int bad = 0;
   double x[4] = {X[0], X[1], X[2], X[3]};
-  if (wr && sub == 0)
-#pragma unroll
-    for (int r = 0; r < 4; r++) Xn[r] = x[r];
+  // the trajectory is written a knot group at a time: every lane holds the whole state, lane sub
+  // keeps knot j of X and knot i of U with j, i = sub (mod 4), and after each 4th knot the quad
+  // writes the group's 128 B of X / 64 B of U as 16 B stores (one 8 B store per lane per knot put
+  // 20-25 % on the kernel at 1-4 waves/SIMD, profiles/r03fs_ilqr_fwd_store.log)
+  double sx[4] = {x[0], x[1], x[2], x[3]}, su[2] = {0.0, 0.0};
   double J = 0.0;
   // knot i's inputs were loaded during knot i-1 (the loads are off the x chain; loading them at the
   // top of the knot put an L2 round trip on it)
@@ -1324,7 +1329,12 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
       for (int c = 1; c < 4; c++) acc = acc + Kr[2 * c + r] * dx[c];
       u[r] = (ur[r] + alpha * kr[r]) + acc;
     }
-    if (wr && sub < 2) Un[2 * i + sub] = u[sub];
+    if ((i & 3) == sub) {
+      su[0] = u[0];
+      su[1] = u[1];
+    }
+    if (wr && (i & 3) == 3)
+      *reinterpret_cast<double2*>(Un + 2 * (i - 3 + sub)) = make_double2(su[0], su[1]);
     // StageCost: sigmoid_boundary(ax; -2, 2) on subs 0/1, sigmoid_boundary(δ; -π/6, π/6) on 2/3
     {
       const double slope = 10, mag = 100;
@@ -1359,7 +1369,15 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
     for (int r = 0; r < 4; r++) xn[r] = 1.0 / 6 * (k1[r] + 2 * k2[r] + 2 * k3[r] + k4[r]) * dT + x[r];
 #pragma unroll
     for (int r = 0; r < 4; r++) x[r] = xn[r];
-    if (wr) Xn[4 * (i + 1) + sub] = xn[sub];
+    if (((i + 1) & 3) == sub) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) sx[r] = xn[r];
+    }
+    if (wr && ((i + 1) & 3) == 3) {
+      double2* d = reinterpret_cast<double2*>(Xn + 4 * (i - 2 + sub));
+      d[0] = make_double2(sx[0], sx[1]);
+      d[1] = make_double2(sx[2], sx[3]);
+    }
 #pragma unroll
     for (int r = 0; r < 4; r++) xr[r] = nxr[r];
 #pragma unroll
@@ -1367,7 +1385,18 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
     kr[0] = nk[0]; kr[1] = nk[1];
     ur[0] = nu[0]; ur[1] = nu[1];
   }
-  if (wr && sub < 2) Un[2 * (N - 1) + sub] = 0.0;
+  // the last group (partial, or U's knot N-1 alone): U's knot N-1 is zero (ILQR.jl never
+  // writes U[:, end]); X's group went out in the loop when N-1 = 3 (mod 4)
+  const int gl = (N - 1) & 3, g0 = N - 1 - gl;
+  if (gl == sub) su[0] = su[1] = 0.0;
+  if (wr && sub <= gl) {
+    *reinterpret_cast<double2*>(Un + 2 * (g0 + sub)) = make_double2(su[0], su[1]);
+    if (gl != 3) {
+      double2* d = reinterpret_cast<double2*>(Xn + 4 * (g0 + sub));
+      d[0] = make_double2(sx[0], sx[1]);
+      d[1] = make_double2(sx[2], sx[3]);
+    }
+  }
   return J + terminal(P.variant, x);
 }
 
@@ -1379,7 +1408,7 @@ __global__ __launch_bounds__(64) void ilqr_forward_quad_kernel(IlqrDev P, int B,
   const size_t b = live ? b0 : B - 1;  // all lanes active (DPP quads); tail quads store nothing
   const size_t N = P.N;
   const double J = forward_trial_quad(P, X + b * N * 4, U + b * N * 2, k + b * (N - 1) * 2, Kg + b * (N - 1) * 8,
-                                      alpha[b], Xn + b * N * 4, Un + b * N * 2, live, sub);
+                                      alpha[b], Xn + b * N * 4, Un + b * N * 2, live && !ILQR_FWD_NOSTORE, sub);
   if (live && sub == 0) Jn[b] = J;
 }
 
