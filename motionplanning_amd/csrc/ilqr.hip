@@ -151,9 +151,11 @@ __device__ __forceinline__ void dyn(const double* s, double ax, const UPre& q, d
   d[3] = s[2] * q.cb * q.tdl / (la + lb);
 }
 
-// RK4Integration, Dynamics.jl:18-28
+// RK4Integration, Dynamics.jl:18-28, as its increment: o[i] = inc[i] + s[i] with
+// inc[i] = 1/6·(k1 + 2k2 + 2k3 + k4)·dT.  dyn reads only s[2] (speed) and s[3] (heading), so the
+// stage slopes -- and inc -- do not depend on s[0] / s[1] at all (knot_derivs uses that).
 template <bool F>
-__device__ __forceinline__ void rk4(const double* s, double ax, const UPre& q, double dT, double* o, int& bad) {
+__device__ __forceinline__ void rk4_inc(const double* s, double ax, const UPre& q, double dT, double* inc, int& bad) {
   double k1[4], k2[4], k3[4], k4[4], x2[4], x3[4], x4[4];
   dyn<F>(s, ax, q, k1, bad);
 #pragma unroll
@@ -166,7 +168,34 @@ __device__ __forceinline__ void rk4(const double* s, double ax, const UPre& q, d
   for (int i = 0; i < 4; i++) x4[i] = s[i] + dT * k3[i];
   dyn<F>(x4, ax, q, k4, bad);
 #pragma unroll
-  for (int i = 0; i < 4; i++) o[i] = 1.0 / 6 * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]) * dT + s[i];
+  for (int i = 0; i < 4; i++) inc[i] = 1.0 / 6 * (k1[i] + 2 * k2[i] + 2 * k3[i] + k4[i]) * dT;
+}
+template <bool F>
+__device__ __forceinline__ void rk4(const double* s, double ax, const UPre& q, double dT, double* o, int& bad) {
+  double inc[4];
+  rk4_inc<F>(s, ax, q, dT, inc, bad);
+#pragma unroll
+  for (int i = 0; i < 4; i++) o[i] = inc[i] + s[i];
+}
+// The x / y columns of the dynamics Jacobian (GetMatrix.jl:3-25, states ± eps): RK4 of the
+// perturbed state is the unperturbed increment plus the perturbed state (rk4_inc), so one RK4 of
+// the knot's own state gives all four perturbed evaluations -- the same operations on the same
+// operands as four rk4 calls, so the same bits.
+template <bool F>
+__device__ __forceinline__ void dyn_jac_xy(const double* s, double ax, const UPre& q, double dT, double e, double* out,
+                                           size_t stride, int& bad) {
+  double inc[4];
+  rk4_inc<F>(s, ax, q, dT, inc, bad);
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    double sp[4], sm[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
+    sp[i] = s[i] + e;
+    sm[i] = s[i] - e;
+#pragma unroll
+    for (int r = 0; r < 4; r++) out[(size_t)(4 * r + i) * stride] = ((inc[r] + sp[r]) - (inc[r] + sm[r])) / (2 * e);
+  }
 }
 
 // RK4Integration with the four stage headings computed first.  The stage speed and heading
@@ -266,8 +295,9 @@ __device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, c
   // ---- dynamics Jacobians: A (row-major 4x4) at 0, B (4x2) at 16
   const UPre q0 = upre<F>(u[1], bad);
   double sp[4], sm[4], fp[4], fm[4];
+  dyn_jac_xy<F>(s, u[0], q0, P.dT, e, out, stride, bad);
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
+  for (int i = 2; i < 4; i++) {
 #pragma unroll
     for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
     sp[i] = s[i] + e;
@@ -389,9 +419,9 @@ __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const
   }
 }
 
-// knot_derivs split four ways for the latency-bound launches (few active instances): part 0 / 1
-// the dynamics Jacobian's state columns 0-1 / 2-3, part 2 its control columns, part 3 the cost
-// derivatives -- the same operations on the same operands per output as knot_derivs (exact libm),
+// knot_derivs split four ways for the latency-bound launches (few active instances): parts 0-2
+// the dynamics Jacobian (state columns x, y, v / heading + the ax column / the δ column), part 3
+// the cost derivatives -- the same operations on the same operands per output as knot_derivs (exact libm),
 // so the same bits, on four lanes instead of one.
 template <int PART>
 __device__ __forceinline__ void knot_derivs_part(const IlqrDev& P, const double* s, const double* u, double* out,
@@ -399,27 +429,32 @@ __device__ __forceinline__ void knot_derivs_part(const IlqrDev& P, const double*
   const double e = P.eps;
   int bad = 0;
 #define DOUT(q) out[(size_t)(q) * stride]
-  if (PART <= 1) {
-    const UPre q0 = upre<false>(u[1], bad);
+  // the dynamics Jacobian over three waves (RK4 counts 3 / 4 / 2 + the two perturbed upre)
+  auto state_col = [&](int i, const UPre& q0) {  // column i of A: state i ± eps
     double sp[4], sm[4], fp[4], fm[4];
 #pragma unroll
-    for (int i = 2 * PART; i < 2 * PART + 2; i++) {
+    for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
+    sp[i] = s[i] + e;
+    sm[i] = s[i] - e;
+    rk4<false>(sp, u[0], q0, P.dT, fp, bad);
+    rk4<false>(sm, u[0], q0, P.dT, fm, bad);
 #pragma unroll
-      for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
-      sp[i] = s[i] + e;
-      sm[i] = s[i] - e;
-      rk4<false>(sp, u[0], q0, P.dT, fp, bad);
-      rk4<false>(sm, u[0], q0, P.dT, fm, bad);
-#pragma unroll
-      for (int r = 0; r < 4; r++) DOUT(4 * r + i) = (fp[r] - fm[r]) / (2 * e);
-    }
-  } else if (PART == 2) {
+    for (int r = 0; r < 4; r++) DOUT(4 * r + i) = (fp[r] - fm[r]) / (2 * e);
+  };
+  if (PART == 0) {  // x, y (one RK4, dyn_jac_xy) and speed columns
     const UPre q0 = upre<false>(u[1], bad);
+    dyn_jac_xy<false>(s, u[0], q0, P.dT, e, out, stride, bad);
+    state_col(2, q0);
+  } else if (PART == 1) {  // heading column and the ax column of B
+    const UPre q0 = upre<false>(u[1], bad);
+    state_col(3, q0);
     double fp[4], fm[4];
     rk4<false>(s, u[0] + e, q0, P.dT, fp, bad);
     rk4<false>(s, u[0] - e, q0, P.dT, fm, bad);
 #pragma unroll
     for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 0) = (fp[r] - fm[r]) / (2 * e);
+  } else if (PART == 2) {  // the δ column of B
+    double fp[4], fm[4];
     const UPre qp = upre<false>(u[1] + e, bad), qm = upre<false>(u[1] - e, bad);
     rk4<false>(s, u[0], qp, P.dT, fp, bad);
     rk4<false>(s, u[0], qm, P.dT, fm, bad);
