@@ -177,15 +177,50 @@ __device__ __forceinline__ void rk4(const double* s, double ax, const UPre& q, d
 #pragma unroll
   for (int i = 0; i < 4; i++) o[i] = inc[i] + s[i];
 }
+// rk4_inc with the (sin, cos) of the first NS stage headings supplied in sc (NS = 0: all computed,
+// stages 1-2 written to sc).  knot_derivs' RK4s of the knot's own state, of its speed ± eps and of
+// ax ± eps have bit-identical stage-1 headings s[3] + β, and the ax pair also the stage-2 heading
+// (ax enters only the speed slope k[2]): the same sincos on the same argument, evaluated once.
+template <bool F, int NS>
+__device__ __forceinline__ void rk4_inc_sh(const double* s, double ax, const UPre& q, double dT, double* inc,
+                                           int& bad, double (&sc)[2][2]) {
+  const double la = 1.56, lb = 1.64;
+  double k[4][4], xs[4];
+#pragma unroll
+  for (int st = 0; st < 4; st++) {
+    const double* xi = st == 0 ? s : xs;
+    double sn, cs;
+    if (st < NS) {
+      sn = sc[st][0];
+      cs = sc[st][1];
+    } else {
+      LM<F>::sincos(xi[3] + q.beta, &sn, &cs, bad);
+      if (NS == 0 && st < 2) {
+        sc[st][0] = sn;
+        sc[st][1] = cs;
+      }
+    }
+    k[st][0] = xi[2] * cs;  // dyn (Dynamics.jl:1-16)
+    k[st][1] = xi[2] * sn;
+    k[st][2] = ax;
+    k[st][3] = xi[2] * q.cb * q.tdl / (la + lb);
+    if (st < 3) {
+      double nx[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) nx[i] = s[i] + (st < 2 ? dT / 2 : dT) * k[st][i];
+#pragma unroll
+      for (int i = 0; i < 4; i++) xs[i] = nx[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) inc[i] = 1.0 / 6 * (k[0][i] + 2 * k[1][i] + 2 * k[2][i] + k[3][i]) * dT;
+}
+
 // The x / y columns of the dynamics Jacobian (GetMatrix.jl:3-25, states ± eps): RK4 of the
 // perturbed state is the unperturbed increment plus the perturbed state (rk4_inc), so one RK4 of
 // the knot's own state gives all four perturbed evaluations -- the same operations on the same
 // operands as four rk4 calls, so the same bits.
-template <bool F>
-__device__ __forceinline__ void dyn_jac_xy(const double* s, double ax, const UPre& q, double dT, double e, double* out,
-                                           size_t stride, int& bad) {
-  double inc[4];
-  rk4_inc<F>(s, ax, q, dT, inc, bad);
+__device__ __forceinline__ void dyn_jac_xy_inc(const double* s, const double* inc, double e, double* out, size_t stride) {
 #pragma unroll
   for (int i = 0; i < 2; i++) {
     double sp[4], sm[4];
@@ -196,6 +231,13 @@ __device__ __forceinline__ void dyn_jac_xy(const double* s, double ax, const UPr
 #pragma unroll
     for (int r = 0; r < 4; r++) out[(size_t)(4 * r + i) * stride] = ((inc[r] + sp[r]) - (inc[r] + sm[r])) / (2 * e);
   }
+}
+template <bool F>
+__device__ __forceinline__ void dyn_jac_xy(const double* s, double ax, const UPre& q, double dT, double e, double* out,
+                                           size_t stride, int& bad) {
+  double inc[4];
+  rk4_inc<F>(s, ax, q, dT, inc, bad);
+  dyn_jac_xy_inc(s, inc, e, out, stride);
 }
 
 // RK4Integration with the four stage headings computed first.  The stage speed and heading
@@ -294,24 +336,34 @@ __device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, c
 #define DOUT(q) out[(size_t)(q) * stride]
   // ---- dynamics Jacobians: A (row-major 4x4) at 0, B (4x2) at 16
   const UPre q0 = upre<F>(u[1], bad);
-  double sp[4], sm[4], fp[4], fm[4];
-  dyn_jac_xy<F>(s, u[0], q0, P.dT, e, out, stride, bad);
-#pragma unroll
-  for (int i = 2; i < 4; i++) {
+  double sp[4], sm[4], fp[4], fm[4], inc[4], incm[4], sc[2][2];
+  rk4_inc_sh<F, 0>(s, u[0], q0, P.dT, inc, bad, sc);  // the knot's own state: stage 1-2 sincos kept
+  dyn_jac_xy_inc(s, inc, e, out, stride);
+  {  // speed ± eps: stage 1's heading is s[3]
 #pragma unroll
     for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
-    sp[i] = s[i] + e;
-    sm[i] = s[i] - e;
+    sp[2] = s[2] + e;
+    sm[2] = s[2] - e;
+    rk4_inc_sh<F, 1>(sp, u[0], q0, P.dT, inc, bad, sc);
+    rk4_inc_sh<F, 1>(sm, u[0], q0, P.dT, incm, bad, sc);
+#pragma unroll
+    for (int r = 0; r < 4; r++) DOUT(4 * r + 2) = ((inc[r] + sp[r]) - (incm[r] + sm[r])) / (2 * e);
+  }
+  {  // heading ± eps
+#pragma unroll
+    for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
+    sp[3] = s[3] + e;
+    sm[3] = s[3] - e;
     rk4<F>(sp, u[0], q0, P.dT, fp, bad);
     rk4<F>(sm, u[0], q0, P.dT, fm, bad);
 #pragma unroll
-    for (int r = 0; r < 4; r++) DOUT(4 * r + i) = (fp[r] - fm[r]) / (2 * e);
+    for (int r = 0; r < 4; r++) DOUT(4 * r + 3) = (fp[r] - fm[r]) / (2 * e);
   }
-  {  // ax perturbation leaves the δ-only terms unchanged
-    rk4<F>(s, u[0] + e, q0, P.dT, fp, bad);
-    rk4<F>(s, u[0] - e, q0, P.dT, fm, bad);
+  {  // ax perturbation leaves the δ-only terms unchanged (and stage 1-2 headings: rk4_inc_sh)
+    rk4_inc_sh<F, 2>(s, u[0] + e, q0, P.dT, inc, bad, sc);
+    rk4_inc_sh<F, 2>(s, u[0] - e, q0, P.dT, incm, bad, sc);
 #pragma unroll
-    for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 0) = (fp[r] - fm[r]) / (2 * e);
+    for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 0) = ((inc[r] + s[r]) - (incm[r] + s[r])) / (2 * e);
     const UPre qp = upre<F>(u[1] + e, bad), qm = upre<F>(u[1] - e, bad);
     rk4<F>(s, u[0], qp, P.dT, fp, bad);
     rk4<F>(s, u[0], qm, P.dT, fm, bad);
