@@ -11,7 +11,8 @@
 //                         bits, so every derivative is bit-identical to the scalar restatement.
 //   ilqr_backward_quad_kernel   the Riccati sweep j = N-2..0 (ILQR.jl:46-67) on a lane quad per
 //                         instance, fed from LDS by a loader wave; Julia's pinv (LAPACK's 2x2 path).
-//   line search (ILQR.jl:70-86), trial m at α = 2^-m on a lane quad: round 0 (16 trials per
+//   line search (ILQR.jl:70-86), trial m at α = 2^-m on a lane quad (a lane pair in the pipelined
+//                         launch's round 0, throughput-bound there): round 0 (16 trials per
 //                         instance at once), then the trials 16..m* of the instances still searching
 //                         all at once in the next launch (ilqr_search_pipe_kernel: beside the next
 //                         iteration's round 0) and ilqr_search_finish_kernel (accept); with few
@@ -69,6 +70,14 @@ constexpr bool kFwdQuad = true;  // ilqr_forward_quad_kernel: a lane quad per in
 #define ILQR_SEARCH_L 4
 #endif
 constexpr int kSearchL = ILQR_SEARCH_L;  // lanes per line-search trial in mp_ilqr_solve (1 or 4)
+#ifndef ILQR_ROUND0_L
+#define ILQR_ROUND0_L 2
+#endif
+constexpr int kRound0L = ILQR_ROUND0_L;  // lanes per trial in the pipelined launch's round 0 (2 or 4) ...
+#ifndef ILQR_PAIR_MIN
+#define ILQR_PAIR_MIN 0
+#endif
+constexpr int kPairMin = ILQR_PAIR_MIN;  // ... while at least this many instances are active (else 4)
 #ifndef ILQR_ONEPASS_MAX
 #define ILQR_ONEPASS_MAX 512
 #endif
@@ -1487,6 +1496,141 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
   return J + terminal(P.variant, x);
 }
 
+// Broadcast lane J (0 / 1) of each lane pair to the pair (DPP quad_perm [J, J, J+2, J+2]).
+template <int J>
+__device__ __forceinline__ double pair_bcast(double v) {
+  constexpr int c = J | (J << 2) | ((J + 2) << 4) | ((J + 2) << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), c, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), c, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// forward_trial_quad on a lane PAIR (sub = lane & 1): lane 0 evaluates StageCost's two ax sigmoid
+// exponentials and the RK4 stage-1 / stage-3 sincos, lane 1 the two δ exponentials and stages 2 / 4;
+// pair broadcasts share them.  Half the lanes of the quad trial per trial, two independent libm
+// calls per lane instead of one: fewer instructions per trial where the search is throughput-bound
+// (round 0 at full activity).  Same operations on the same operands: bit-identical.
+// The trajectory goes out in 4-knot groups: knot j of a group is held by lane (j & 3) >> 1, slot
+// j & 1, and each lane writes its two consecutive knots (64 B of X, 32 B of U).
+__device__ double forward_trial_pair(const IlqrDev& P, const double* X, const double* U, const double* k,
+                                     const double* Kg, double alpha, double* Xn, double* Un, bool wr, int sub) {
+  const int N = P.N;
+  const double la = 1.56, lb = 1.64, dT = P.dT;
+  int bad = 0;
+  double x[4] = {X[0], X[1], X[2], X[3]};
+  double sx[2][4], su[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+#pragma unroll
+  for (int r = 0; r < 4; r++) sx[0][r] = sx[1][r] = x[r];
+  double J = 0.0;
+  double xr[4], Kr[8], kr[2], ur[2];
+#pragma unroll
+  for (int r = 0; r < 4; r++) xr[r] = X[r];
+#pragma unroll
+  for (int r = 0; r < 8; r++) Kr[r] = Kg[r];
+  kr[0] = k[0]; kr[1] = k[1];
+  ur[0] = U[0]; ur[1] = U[1];
+  for (int i = 0; i < N - 1; i++) {
+    const int in = i + 2 < N ? i + 1 : i;  // knot i+1 (clamped)
+    double nxr[4], nK[8], nk[2], nu[2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) nxr[r] = X[4 * in + r];
+#pragma unroll
+    for (int r = 0; r < 8; r++) nK[r] = Kg[8 * in + r];
+    nk[0] = k[2 * in]; nk[1] = k[2 * in + 1];
+    nu[0] = U[2 * in]; nu[1] = U[2 * in + 1];
+    double dx[4], u[2];
+#pragma unroll
+    for (int r = 0; r < 4; r++) dx[r] = x[r] - xr[r];
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      double acc = Kr[2 * 0 + r] * dx[0];
+#pragma unroll
+      for (int c = 1; c < 4; c++) acc = acc + Kr[2 * c + r] * dx[c];
+      u[r] = (ur[r] + alpha * kr[r]) + acc;
+    }
+    if (((i & 3) >> 1) == sub) {
+      su[i & 1][0] = u[0];
+      su[i & 1][1] = u[1];
+    }
+    if (wr && (i & 3) == 3) {
+      double2* d = reinterpret_cast<double2*>(Un + 2 * (i - 3 + 2 * sub));
+      d[0] = make_double2(su[0][0], su[0][1]);
+      d[1] = make_double2(su[1][0], su[1][1]);
+    }
+    {  // StageCost: sigmoid_boundary(ax; -2, 2) on lane 0, sigmoid_boundary(δ; -π/6, π/6) on lane 1
+      const double slope = 10, mag = 100;
+      const double st = sub ? u[1] : u[0];
+      const double mn = sub ? -MPJ_PI / 6 : -2.0, mx = sub ? MPJ_PI / 6 : 2.0;
+      const double cA = 1 / (1 + mpj_exp(-slope * (st - mx)));
+      const double cB = 1 / (1 + mpj_exp(slope * (st - mn)));
+      const double a1 = pair_bcast<0>(cA), a2 = pair_bcast<0>(cB), d1 = pair_bcast<1>(cA), d2 = pair_bcast<1>(cB);
+      const double sa = mag * (a1 + a2), sd = mag * (d1 + d2);
+      J = J + stage_pre(P.variant, x, u[0], u[1], sd, sa);
+    }
+    const UPre q = upre<false>(u[1], bad);
+    const double ax = u[0];
+    const double k1_3 = x[2] * q.cb * q.tdl / (la + lb);
+    const double x2_2 = x[2] + dT / 2 * ax, x2_3 = x[3] + dT / 2 * k1_3;
+    const double k2_3 = x2_2 * q.cb * q.tdl / (la + lb);
+    const double x3_2 = x[2] + dT / 2 * ax, x3_3 = x[3] + dT / 2 * k2_3;
+    const double k3_3 = x3_2 * q.cb * q.tdl / (la + lb);
+    const double x4_2 = x[2] + dT * ax, x4_3 = x[3] + dT * k3_3;
+    const double k4_3 = x4_2 * q.cb * q.tdl / (la + lb);
+    double snA, csA, snB, csB;
+    mpj_sincos((sub ? x2_3 : x[3]) + q.beta, &snA, &csA);  // stage 1 / 2
+    mpj_sincos((sub ? x4_3 : x3_3) + q.beta, &snB, &csB);  // stage 3 / 4
+    const double s1 = pair_bcast<0>(snA), c1 = pair_bcast<0>(csA), s2 = pair_bcast<1>(snA), c2 = pair_bcast<1>(csA);
+    const double s3 = pair_bcast<0>(snB), c3 = pair_bcast<0>(csB), s4 = pair_bcast<1>(snB), c4 = pair_bcast<1>(csB);
+    const double k1[4] = {x[2] * c1, x[2] * s1, ax, k1_3};
+    const double k2[4] = {x2_2 * c2, x2_2 * s2, ax, k2_3};
+    const double k3[4] = {x3_2 * c3, x3_2 * s3, ax, k3_3};
+    const double k4[4] = {x4_2 * c4, x4_2 * s4, ax, k4_3};
+    double xn[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) xn[r] = 1.0 / 6 * (k1[r] + 2 * k2[r] + 2 * k3[r] + k4[r]) * dT + x[r];
+#pragma unroll
+    for (int r = 0; r < 4; r++) x[r] = xn[r];
+    if ((((i + 1) & 3) >> 1) == sub) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) sx[(i + 1) & 1][r] = xn[r];
+    }
+    if (wr && ((i + 1) & 3) == 3) {
+      double2* d = reinterpret_cast<double2*>(Xn + 4 * (i - 2 + 2 * sub));
+      d[0] = make_double2(sx[0][0], sx[0][1]);
+      d[1] = make_double2(sx[0][2], sx[0][3]);
+      d[2] = make_double2(sx[1][0], sx[1][1]);
+      d[3] = make_double2(sx[1][2], sx[1][3]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) xr[r] = nxr[r];
+#pragma unroll
+    for (int r = 0; r < 8; r++) Kr[r] = nK[r];
+    kr[0] = nk[0]; kr[1] = nk[1];
+    ur[0] = nu[0]; ur[1] = nu[1];
+  }
+  // the last group (partial, or U's knot N-1 alone): U's knot N-1 is zero; X's group went out in
+  // the loop when N-1 = 3 (mod 4)
+  const int gl = (N - 1) & 3, g0 = N - 1 - gl;
+  if ((gl >> 1) == sub) su[gl & 1][0] = su[gl & 1][1] = 0.0;
+  if (wr && 2 * sub <= gl) {
+    const int kn = g0 + 2 * sub;
+    const bool two = 2 * sub + 1 <= gl;
+    double2* du = reinterpret_cast<double2*>(Un + 2 * kn);
+    du[0] = make_double2(su[0][0], su[0][1]);
+    if (two) du[1] = make_double2(su[1][0], su[1][1]);
+    if (gl != 3) {
+      double2* d = reinterpret_cast<double2*>(Xn + 4 * kn);
+      d[0] = make_double2(sx[0][0], sx[0][1]);
+      d[1] = make_double2(sx[0][2], sx[0][3]);
+      if (two) {
+        d[2] = make_double2(sx[1][0], sx[1][1]);
+        d[3] = make_double2(sx[1][2], sx[1][3]);
+      }
+    }
+  }
+  return J + terminal(P.variant, x);
+}
+
 __global__ __launch_bounds__(64) void ilqr_forward_quad_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                                const double* k, const double* Kg, const double* alpha,
                                                                double* Xn, double* Un, double* Jn) {
@@ -1612,7 +1756,7 @@ __device__ __forceinline__ void search_round0(const IlqrDev& P, int B, double* X
   int mw = -1;  // accepted trial index
   bool searching = live;
   // lanes that report a trial's outcome: every lane (L = 1) or the quad's first
-  constexpr unsigned long long lead = L == 1 ? ~0ull : 0x1111111111111111ull;
+  constexpr unsigned long long lead = L == 1 ? ~0ull : L == 2 ? 0x5555555555555555ull : 0x1111111111111111ull;
   for (int r = 0; __any(searching) && !(one_round && r > 0); r++) {
     const int m = r * G + g;
     const bool mine = searching && m <= P.ls_cap && m <= ms;  // uniform over a trial's lanes
@@ -1620,6 +1764,8 @@ __device__ __forceinline__ void search_round0(const IlqrDev& P, int B, double* X
     if (mine) {
       if (L == 4) {
         jt = forward_trial_quad(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, sub);
+      } else if (L == 2) {
+        jt = forward_trial_pair(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, sub);
       } else {
         int d = 0;
         jt = forward_trial<false>(P, Xb, Ub, kb, Kb, ldexp(1.0, -m), Xg, Ug, true, d);
@@ -1731,7 +1877,7 @@ __global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, 
 // iteration's round 0 left pending (blocks n0.., instance-major within each 16-trial column), so
 // the rest pass's latency hides under round 0 instead of following it.  An instance's own sequence
 // of operations is unchanged (its next backward pass simply comes one launch later).
-template <int G, int L>
+template <int G, int L, int L0 = L>
 __global__ __launch_bounds__(64) void ilqr_search_pipe_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
                                                               const double* Kg, double* Xs, double* Us, double* Jcur,
                                                               int* active, int* iters, int* flags, int* n_active,
@@ -1741,8 +1887,8 @@ __global__ __launch_bounds__(64) void ilqr_search_pipe_kernel(IlqrDev P, int B, 
                                                               int n0) {
   const int bx = blockIdx.x;
   if (bx < n0) {
-    search_round0<G, L>(P, B, X, U, k, Kg, Xs, Us, Jcur, active, iters, flags, n_active, 1, pend_new, mstar_new,
-                        pend_old, npend_new, bx);
+    search_round0<G, L0>(P, B, X, U, k, Kg, Xs, Us, Jcur, active, iters, flags, n_active, 1, pend_new, mstar_new,
+                         pend_old, npend_new, bx);
   } else {
     const int r = bx - n0;
     search_rest<G, L>(P, B, X, U, k, Kg, Jcur, pend_old, mstar_old, Xs2, Us2, Jt, winm_old, G, T2, r % B, r / B);
@@ -2120,7 +2266,8 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
       continue;
     }
     // G = 16: a lane quad per trial (4 waves per SIMD at B = 4096); the narrower fallbacks one lane
-    const int ipw = G == kSearchG ? 64 / (kSearchG * kSearchL) : 64 / G;
+    const int l0 = pipe && n_act >= kPairMin ? kRound0L : kSearchL;
+    const int ipw = G == kSearchG ? 64 / (kSearchG * l0) : 64 / G;
     const dim3 gs((unsigned)((B + ipw - 1) / ipw));
     if (pipe) {
       const int cur = q2 & 1, old = cur ^ 1;
@@ -2129,7 +2276,9 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
       int* winm_o = dpw + (2 + old) * B;  // pend_n is 0 and winm[cur] 0x7f7f7f7f: reset by the finish
       int *ms_n = dpw + (4 + cur) * B, *ms_o = dpw + (4 + old) * B;  // kernel that last used them
       const unsigned ncol = (unsigned)((T2 + 64 / kSearchL - 1) / (64 / kSearchL));
-      hipLaunchKernelGGL((ilqr_search_pipe_kernel<kSearchG, kSearchL>), dim3(gs.x + (unsigned)B * ncol), b1, 0,
+      auto pipe_k = l0 == kRound0L ? ilqr_search_pipe_kernel<kSearchG, kSearchL, kRound0L>
+                                   : ilqr_search_pipe_kernel<kSearchG, kSearchL, kSearchL>;
+      hipLaunchKernelGGL(pipe_k, dim3(gs.x + (unsigned)B * ncol), b1, 0,
                          ctx->stream, D, B, dX, dU, dk, dK, dXn, dUn, dJ, dact, dit, dfl, dn, pend_n, ms_n, dnp,
                          pend_o, ms_o, dXs2, dUs2, dJt, winm_o, T2, (int)gs.x);
       MP_HIP(ctx, hipGetLastError());

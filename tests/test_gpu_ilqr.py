@@ -177,7 +177,9 @@ def test_solve_configs2_horizon_bitexact(ctx):
     assert stalled > 0  # the rest pass (trials 16..max_ls) was exercised
 
 
-def test_solve_pipelined_search_bitexact(ctx):
+# N-1 = 19, 20, 21, 22: every residue of the trial's last 4-knot store group in round 0
+@pytest.mark.parametrize("B,N", [(2048, 20), (768, 21), (768, 22), (768, 23)])
+def test_solve_pipelined_search_bitexact(ctx, B, N):
     """mp_ilqr_solve's pipelined line search on a batch large enough to stay in it for many
     iterations (2048 instances: > 512 active): each iteration's rest pass runs in the next launch
     beside round 0, the instances it holds sit one backward pass out, and the switch to the one-pass
@@ -185,7 +187,6 @@ def test_solve_pipelined_search_bitexact(ctx):
     controls must equal the oracle's sequential loop."""
     from concurrent.futures import ThreadPoolExecutor
 
-    B, N = 2048, 20
     p = ilqr.params(N=N, max_iter=60)
     x0, U0 = ilqr.cfg3_instances(B, N, seed=11)
     X0, _ = ilqr.ilqr_rollout(p, x0, U0, ctx=ctx)
