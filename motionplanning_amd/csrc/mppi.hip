@@ -27,8 +27,11 @@ namespace {
 
 constexpr int NT = 256;     // threads per block (4 waves)
 constexpr int RPB = NT / 2; // rollouts per block
-constexpr size_t kMaxLds = 150 * 1024;  // dynamic LDS budget per block (160 KiB per CU on gfx950)
-constexpr size_t kCoLds = 76 * 1024;    // budget that keeps two blocks co-resident per CU
+#ifndef MPPI_PRIO
+#define MPPI_PRIO 0  // issue-priority levels of the rollout loop (see ctrl())
+#endif
+constexpr size_t kMaxLds = 148 * 1024;  // dynamic LDS budget per block (160 KiB per CU on gfx950)
+constexpr size_t kCoLds = 72 * 1024;    // budget that keeps two blocks co-resident per CU
 
 __device__ __forceinline__ double block_reduce_min(double v, double* sh) {
   for (int o = 32; o >= 1; o >>= 1) v = nanmin(v, __shfl_xor(v, o));
@@ -164,9 +167,13 @@ __global__ __launch_bounds__(256) void noise_prep_kernel(MppiDev P, int S, const
 template <int BT, int LPR, bool INL>
 __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   constexpr int NT = BT, RPB = BT / LPR, NQ = BT / 128;
+  // WPART: the block partial Σ e·u is formed per wave over the wave's own 32 rollouts (lane pair
+  // layout, H <= 64), with the HBM control lists prefetched into registers as soon as the wave's
+  // rollouts end -- their latency then hides behind the block's slower waves and the reductions.
+  constexpr bool WPART = LPR == 2;
   __shared__ double sh_red[NT / 64];
   __shared__ double sh_e[RPB];
-  __shared__ double sh_q[NQ][128];
+  __shared__ double sh_q[WPART ? NT / 64 : NQ][128];  // per-wave (WPART) or per-quarter control sums
   __shared__ int sh_last, sh_m, sh_bstar, sh_fc;
   __shared__ double sh_eta;
   __shared__ double atab[20];  // mpj_atan_tab range constants
@@ -256,12 +263,24 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       // Self-balancing issue priority: a wave's priority drops by one per quarter of the
       // horizon it has completed, so the waves sharing a SIMD (oldest-first arbitration
       // otherwise lets one run ahead and leaves the other to finish alone) end together.
+#if MPPI_PRIO == 0
       if ((4 * j) % H < 4 && j > 0) {
         const int q = (4 * j) / H;
         if (q == 1) __builtin_amdgcn_s_setprio(2);
         else if (q == 2) __builtin_amdgcn_s_setprio(1);
         else if (q == 3) __builtin_amdgcn_s_setprio(0);
       }
+#else
+      // (A/B) levels crowded towards the end of the horizon, where a lag turns into lone-wave time:
+      // 1: H/2, 3H/4, 7H/8;  2: H-12, H-6, H-3
+      if (j > 0) {
+        const int t1 = MPPI_PRIO == 1 ? H / 2 : H - 12, t2 = MPPI_PRIO == 1 ? 3 * H / 4 : H - 6,
+                  t3 = MPPI_PRIO == 1 ? 7 * H / 8 : H - 3;
+        if (j == t1) __builtin_amdgcn_s_setprio(2);
+        else if (j == t2) __builtin_amdgcn_s_setprio(1);
+        else if (j == t3) __builtin_amdgcn_s_setprio(0);
+      }
+#endif
     };
     auto store = [&](int j, const double* u) {
       if (LPR == 2) {
@@ -293,6 +312,28 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
     if (c != c) atomicOr(A.flags, 1);
   }
   // ---------------- block partial (online softmax), MPPIUtils.jl:154-167
+  // WPART: lane l of wave w sums outputs t = l and l + 64 (t = 2h + side) over the wave's rollouts
+  // [32w, 32w + nr) of the block in rollout order; the block value is then the wave sums added in
+  // wave order.  Single- and multi-scene launches share this order (scene batching invariance).
+  const int wid = tid >> 6, lane = tid & 63;
+  const bool wp = WPART && H2 <= 128;  // block-uniform
+  const int nr = wp ? max(0, min(32, K - b * RPB - 32 * wid)) : 0;  // wave-uniform
+  // The register prefetch only in the 8-wave (multi-scene) kernels: it holds 128 VGPRs across the
+  // reductions, which slowed the 4-wave single-scene kernel's rollout loop (LDS path anyway).
+  constexpr bool PREF = BT == 512;
+  double v0[32], v1[32];
+  if (PREF && wp && !ush) {
+    // this wave's own control-list stores -> its own loads (same wave, same CU): wait for the stores
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const double* cb = A.ctrl_all + (((size_t)s * H + (lane >> 1)) * K + (size_t)b * RPB + 32 * wid) * 2 + (lane & 1);
+    const size_t up = (size_t)64 * K;  // t + 64 is step h + 32, same side
+#pragma unroll
+    for (int r = 0; r < 32; r++) v0[r] = (r < nr && lane < H2) ? cb[2 * r] : 0.0;
+    if (H2 > 64) {
+#pragma unroll
+      for (int r = 0; r < 32; r++) v1[r] = (r < nr && lane + 64 < H2) ? cb[up + 2 * r] : 0.0;
+    }
+  }
   const double cm = active ? c : __builtin_inf();
   const double rho_b = block_reduce_min(cm, sh_red);
   const double e = active ? mpj_exp(P.nil * (c - rho_b)) : 0.0;
@@ -301,8 +342,45 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   const double fc_b = block_reduce_sum((side == 0 && active && feas) ? 1.0 : 0.0, sh_red);
   __syncthreads();  // control-list stores of this block -> visible to its own loads below (same CU)
   double* part = A.part + ((size_t)s * A.nb + b) * A.pstride;
-  {
-    // Σ_i e_i u_i[t] over this block's rollouts; two fixed halves per output, summed in order
+  if (wp) {
+    const double* ew = sh_e + 32 * wid;
+    double a0 = 0.0, a1 = 0.0;
+    if (ush) {
+      const double* uw = ush + (size_t)(32 * wid) * ustr + lane;
+      for (int r = 0; r < nr; r++) {
+        const double er = ew[r];
+        if (lane < H2) a0 = a0 + er * uw[r * ustr];
+        if (lane + 64 < H2) a1 = a1 + er * uw[r * ustr + 64];
+      }
+    } else if (PREF) {
+#pragma unroll
+      for (int r = 0; r < 32; r++) {
+        if (r < nr) {
+          const double er = ew[r];
+          a0 = a0 + er * v0[r];
+          if (H2 > 64) a1 = a1 + er * v1[r];
+        }
+      }
+    } else {  // the same sums, loads issued here
+      const double* cb = A.ctrl_all + (((size_t)s * H + (lane >> 1)) * K + (size_t)b * RPB + 32 * wid) * 2 + (lane & 1);
+      const size_t up = (size_t)64 * K;
+      for (int r = 0; r < nr; r++) {
+        const double er = ew[r];
+        if (lane < H2) a0 = a0 + er * cb[2 * r];
+        if (lane + 64 < H2) a1 = a1 + er * cb[up + 2 * r];
+      }
+    }
+    sh_q[wid][lane] = a0;
+    sh_q[wid][lane + 64] = a1;
+    __syncthreads();
+    if (tid < H2) {
+      double v = sh_q[0][tid];
+#pragma unroll
+      for (int w = 1; w < NT / 64; w++) v = v + sh_q[w][tid];
+      part[4 + tid] = v;
+    }
+  } else {
+    // Σ_i e_i u_i[t] over this block's rollouts; fixed quarters per output, summed in order
     const int t = tid % 128, q = tid / 128;
     const int r0 = q * (RPB / NQ), r1 = r0 + RPB / NQ;
     for (int t0 = 0; t0 < H2; t0 += 128) {  // block-uniform trip count: barriers are safe
