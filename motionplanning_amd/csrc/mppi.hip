@@ -28,7 +28,7 @@ namespace {
 constexpr int NT = 256;     // threads per block (4 waves)
 constexpr int RPB = NT / 2; // rollouts per block
 #ifndef MPPI_PRIO
-#define MPPI_PRIO 0  // issue-priority levels of the rollout loop (see ctrl())
+#define MPPI_PRIO 3  // issue-priority scheme of the rollout loop (see ctrl()); 0 = quarters (round 2)
 #endif
 constexpr size_t kMaxLds = 148 * 1024;  // dynamic LDS budget per block (160 KiB per CU on gfx950)
 constexpr size_t kCoLds = 72 * 1024;    // budget that keeps two blocks co-resident per CU
@@ -227,6 +227,29 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   }
   double* ctrl_g = A.ctrl_all ? A.ctrl_all + ((size_t)s * H * K + kk) * 2 + side : nullptr;  // LPR 1: + 0
 
+#if MPPI_PRIO == 3
+  // Sibling-paced issue priority: each wave publishes its step in LDS and finds the other wave of the
+  // block on its SIMD (HW_ID.SIMD_ID); per step it drops below the sibling when ahead of it and rises
+  // above it when behind, so the pair ends together instead of one wave finishing the horizon alone.
+  __shared__ int sh_simd[NT / 64];
+  __shared__ volatile int sh_prog[NT / 64];
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int sib = -1;
+  {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    if ((tid & 63) == 0) {
+      sh_simd[wv] = (int)((hw >> 4) & 3u);
+      sh_prog[wv] = 0;
+    }
+    __syncthreads();
+    const int me = sh_simd[wv];
+    for (int w = 0; w < NT / 64; w++)
+      if (w != wv && sh_simd[w] == me) sib = w;
+    sib = __builtin_amdgcn_readfirstlane(sib);
+  }
+  int sib_j = 0;
+#endif
   // ---------------- phase 1: the rollout of this lane pair
   int feas;
   double c;
@@ -269,6 +292,16 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
         if (q == 1) __builtin_amdgcn_s_setprio(2);
         else if (q == 2) __builtin_amdgcn_s_setprio(1);
         else if (q == 3) __builtin_amdgcn_s_setprio(0);
+      }
+#elif MPPI_PRIO == 3
+      if (sib >= 0) {
+        // sib_j was read one step ago (its LDS latency hidden behind the step)
+        const int o = __builtin_amdgcn_readfirstlane(sib_j);
+        if (j > o) __builtin_amdgcn_s_setprio(0);
+        else if (j < o) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+        sh_prog[wv] = j;
+        sib_j = sh_prog[sib];
       }
 #else
       // (A/B) levels crowded towards the end of the horizon, where a lag turns into lone-wave time:
