@@ -1512,6 +1512,9 @@ __device__ __forceinline__ double pair_bcast(double v) {
 // (round 0 at full activity).  Same operations on the same operands: bit-identical.
 // The trajectory goes out in 4-knot groups: knot j of a group is held by lane (j & 3) >> 1, slot
 // j & 1, and each lane writes its two consecutive knots (64 B of X, 32 B of U).
+#ifndef ILQR_PAIR_PRIO
+#define ILQR_PAIR_PRIO 0  // (A/B) quarter priority levels in the pair trial
+#endif
 __device__ double forward_trial_pair(const IlqrDev& P, const double* X, const double* U, const double* k,
                                      const double* Kg, double alpha, double* Xn, double* Un, bool wr, int sub) {
   const int N = P.N;
@@ -1529,7 +1532,17 @@ __device__ double forward_trial_pair(const IlqrDev& P, const double* X, const do
   for (int r = 0; r < 8; r++) Kr[r] = Kg[r];
   kr[0] = k[0]; kr[1] = k[1];
   ur[0] = U[0]; ur[1] = U[1];
+#if ILQR_PAIR_PRIO
+  // (A/B) self-balancing issue priority over the trial's knots (a wave drops one level per quarter)
+  const int q1 = (N - 1) / 4, q2 = (N - 1) / 2, q3 = 3 * (N - 1) / 4;
+  __builtin_amdgcn_s_setprio(3);
+#endif
   for (int i = 0; i < N - 1; i++) {
+#if ILQR_PAIR_PRIO
+    if (i == q1) __builtin_amdgcn_s_setprio(2);
+    else if (i == q2) __builtin_amdgcn_s_setprio(1);
+    else if (i == q3) __builtin_amdgcn_s_setprio(0);
+#endif
     const int in = i + 2 < N ? i + 1 : i;  // knot i+1 (clamped)
     double nxr[4], nK[8], nk[2], nu[2];
 #pragma unroll

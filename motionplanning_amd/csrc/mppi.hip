@@ -302,6 +302,11 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
         else __builtin_amdgcn_s_setprio(1);
         sh_prog[wv] = j;
         sib_j = sh_prog[sib];
+      } else if ((4 * j) % H < 4 && j > 0) {  // no sibling in the block on this SIMD: quarter levels
+        const int q = (4 * j) / H;
+        if (q == 1) __builtin_amdgcn_s_setprio(2);
+        else if (q == 2) __builtin_amdgcn_s_setprio(1);
+        else if (q == 3) __builtin_amdgcn_s_setprio(0);
       }
 #else
       // (A/B) levels crowded towards the end of the horizon, where a lag turns into lone-wave time:
