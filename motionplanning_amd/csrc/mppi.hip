@@ -5,8 +5,11 @@
 //   phase 1  every block: NT/2 rollouts (lane pairs) — noise draw, clamp, RK2
 //            dynamics and all step costs fused; per-rollout cost/flag and the
 //            control list go to HBM (the TrajectoryCollection contract);
-//            then the block's online-softmax partial (ρ_b, η_b, Σ e·u) is
-//            published with an agent-scope release and an arrival ticket.
+//            the two waves sharing a SIMD pace each other by issue priority
+//            (MPPI_PRIO 3).  Then the block's online-softmax partial (ρ_b, η_b,
+//            Σ e·u; the latter per wave over its own rollouts, from registers
+//            prefetched when the wave ends) is published with an agent-scope
+//            release and an arrival ticket.
 //   phase 2  the last block to arrive for a scene (acquire) applies the
 //            FeasibilityCount prefix (MPPIUtils.jl:175), combines the partials
 //            with a log-sum-exp rescale into MPPICtrl (:186-190) and runs the
