@@ -218,7 +218,9 @@ def main():
         "metric": BASE["metric"],
         "value": value,
         "unit": "rollout-steps/s",
-        "n_gpus": dist.get_world_size() if world > 1 else 1,
+        # distinct devices the ranks ran on: a --share-device rehearsal runs every rank on cuda:0 and
+        # reports 1 here (its aggregate is a one-GPU number, see "rehearsal")
+        "n_gpus": len({(int(r[2]), int(r[3])) for r in joined}),
         "ranks": [{"rank": int(r[0]), "local_rank": int(r[1]), "device": int(r[2]), "pci_bus_id": int(r[3])}
                   for r in joined],
         "gpus_requested": a.gpus,
@@ -250,6 +252,9 @@ def main():
         },
         "valid": ok,
     }
+    if a.share_device and world > 1:
+        out["rehearsal"] = (f"--share-device: {world} ranks on one GPU over gloo; value is that one GPU's "
+                            "aggregate, not a multi-GPU result")
     tr = load_traffic(a.traffic, S, K, H)
     if tr is not None:
         out["roofline"]["traffic"] = tr["traffic_bytes"]
@@ -264,6 +269,12 @@ def main():
                 "insts_per_launch": tr["valu_insts"], "achieved": rate, "peak": peak, "unit": "wave-insts/s",
                 "frac": rate / peak, "source": tr["source"] + " SQ_INSTS_VALU",
             }
+            # the bound that binds is fp64 VALU issue: the headline fields carry it, the
+            # HBM roofline (algorithmic bytes / live kernel time vs 8 TB/s) is kept beside it under "hbm"
+            hbm = {k: out["roofline"][k] for k in ("achieved", "peak", "unit", "frac")}
+            hbm["algorithmic_bytes"] = nbytes
+            out["roofline"].update(bound="valu", achieved=rate, peak=peak, unit="wave-insts/s", frac=rate / peak,
+                                   hbm=hbm)
             if tr.get("valu_active") and tr.get("wave_cycles") and tr.get("waves"):
                 # measured, clock-independent: the share of each SIMD's time its waves spend issuing VALU
                 # instructions = (VALU-issue quad-cycles / wave quad-cycles) x waves per SIMD
@@ -283,11 +294,10 @@ def main():
         out["hybrid_astar"] = bench_hastar(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
         rl = load_roofline(a.roofline)
         if rl:
-            out["ilqr"]["roofline"] = valu_roofline(rl, ["ilqr_backward_quad_kernel", "ilqr_forward_quad_kernel",
-                                                         "ilqr_deriv_kernel", "ilqr_search_kernel<16, 4>",
-                                                         "ilqr_search_rest_kernel<16, 4>"])
-            out["hybrid_astar"]["roofline"] = valu_roofline(rl, ["ha_iter_kernel<4, 16>", "ha_book_kernel",
-                                                                 "ha_iter_kernel<12, 4>"])
+            # the kernels of a whole mp_ilqr_solve / mp_ha_plan, ranked by their share of its kernel time
+            # (tools/pmc_roofline.py legs, from solve-only / plan-only traces); the largest is the headline
+            out["ilqr"]["roofline"] = leg_roofline(rl, "ilqr_solve")
+            out["hybrid_astar"]["roofline"] = leg_roofline(rl, "ha_plan")
         out["closed_loop"] = bench_closed_loop(ctx, world, rank, cpu=(rank == 0 and world == 1 and not a.no_cpu))
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_seconds > 0:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
@@ -320,21 +330,22 @@ def load_roofline(path):
         return None
 
 
-def valu_roofline(rl, names):
-    """roofline of a latency/VALU-bound leg: per kernel SQ_INSTS_VALU per launch / kernel-trace average
-    duration vs the fp64 VALU issue peak (tools/pmc_roofline.py, a PMC pass of this tree); the first
-    listed kernel present is the headline ("kernel"), the others follow under "kernels"."""
-    ks = {n: rl["kernels"][n] for n in names if n in rl["kernels"] and "valu_frac" in rl["kernels"][n]}
-    if not ks:
+def leg_roofline(rl, leg):
+    """VALU roofline of one latency/VALU-bound leg: every kernel a solve-only (plan-only) rocprofv3 trace
+    launched, ranked by its share of the leg's kernel time, with SQ_INSTS_VALU per launch (a --pmc pass of
+    the same command) / the trace's average duration vs the fp64 VALU issue peak.  The largest kernel is
+    the headline ("kernel")."""
+    lg = rl.get("legs", {}).get(leg)
+    if not lg or not lg.get("kernels"):
         return None
-    head = next(iter(ks))
-    e = ks[head]
-    return {"bound": "valu", "kernel": head, "achieved": e["valu_achieved"], "peak": rl["peak_wave_insts_per_s"],
-            "unit": "wave-insts/s", "frac": e["valu_frac"], "traffic": None,
-            "kernels": {n: {"insts_per_launch": k["SQ_INSTS_VALU"], "avg_us": k["avg_ns"] / 1e3,
-                            "frac": k["valu_frac"], "wave_valu_busy": k.get("wave_valu_busy")}
-                        for n, k in ks.items()},
-            "source": rl["path"] + " (from " + str(rl.get("source")) + ")"}
+    ks = lg["kernels"]
+    head = ks[0]
+    return {"bound": "valu", "kernel": head["name"], "share_of_leg": head["share"],
+            "achieved": head.get("valu_achieved"), "peak": rl["peak_wave_insts_per_s"], "unit": "wave-insts/s",
+            "frac": head.get("valu_frac"), "traffic": None,
+            "kernels": [{k: e.get(k) for k in ("name", "calls", "avg_us", "share", "SQ_INSTS_VALU", "valu_frac",
+                                               "wave_valu_busy", "SQ_WAVES")} for e in ks],
+            "leg_kernel_ms": lg["total_ms"], "source": rl["path"] + " legs." + leg + " (from " + lg["source"] + ")"}
 
 
 def _sync_max(x, world, dev):
@@ -442,8 +453,9 @@ def bench_hastar(ctx, world, rank, cpu=False):
            "ms_runs": [r * 1e3 for r in runs],
            "scenarios": len(hs), "found": int(g["found"].sum()), "total_pops": pops, "scaling": "strong",
            "dtype": "f64", "valid": bool((g["pops"] > 0).all()),
-           "bound": "latency (device-resident lockstep search: ha_iter_kernel + ha_book_kernel per "
-                    "iteration, no host round trip)"}
+           "bound": "latency (device-resident lockstep search, no host round trip)"}
+    if world == 1:
+        out["shards_world8"] = hastar_shard_projection(ctx, el)
     if cpu:
         import oracle
 
@@ -461,6 +473,34 @@ def bench_hastar(ctx, world, rank, cpu=False):
         out["cpu_baseline"] = {"value": cp / dt, "unit": "node expansions/s", "cores": T, "kind": "port",
                                "sample": f"{n} scenarios ({cp} pops) in {dt:.1f} s on {T} threads, scalar C oracle"}
     out["tracker"] = bench_tracker(ctx, world, rank, hs, cpu=cpu)
+    return out
+
+
+def hastar_shard_projection(ctx, t_all, world=8):
+    """The one-GPU proxy of configs[3]'s 1->8 strong scaling: each of the 8 shards a world-8 job would
+    give one rank, planned alone on this GPU (median of 3), for the contiguous split the bench used
+    through round 3 and the strided one it uses now (distributed.shard_indices).  The 8-GPU plan time is
+    at least the slowest shard's, so T(256) / max T(shard) projects the speed-up."""
+    from motionplanning_amd import distributed as D
+    from motionplanning_amd import hybrid_astar as ha
+
+    out = {"workload": f"scenario_batch(256, seed=4) split {world} ways, each shard planned alone on one GPU",
+           "t256_ms": t_all * 1e3}
+    for name, strided in (("contiguous", False), ("strided", True)):
+        hs = ha.scenario_batch(256, seed=4)
+        ms, pops = [], []
+        for r in range(world):
+            mine = [hs[i] for i in D.shard_indices(len(hs), r, world, strided)]
+            runs = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                ha.plan_batch(mine, ctx=ctx)
+                runs.append(time.perf_counter() - t0)
+            ms.append(sorted(runs)[1] * 1e3)
+            pops.append(max(h.r.loop_count for h in mine))
+        sp = t_all * 1e3 / max(ms)
+        out[name] = {"shard_ms": ms, "shard_max_pops": pops, "projected_speedup": sp,
+                     "projected_efficiency": sp / world}
     return out
 
 
@@ -632,10 +672,21 @@ def cpu_baseline(budget_s):
     u1, n1, t1 = timed_pool(work, budget_s / 3, 1)
     T = cpu_threads()
     uT, nT, tT = timed_pool(work, budget_s, T)
-    return {"value": uT / tT, "unit": "rollout-steps/s", "cores": T, "kind": "port", "host": host_cpu(),
-            "sample": f"{nT} full cfg2 MPPIPlan solves (K=8192, H=50, grid, Philox noise) in {tT:.1f} s on {T} "
-                      f"threads (one solve per thread at a time), scalar C oracle, {os.cpu_count()}-CPU host",
-            "single_thread": {"value": u1 / t1, "cores": 1, "sample": f"{n1} solves in {t1:.1f} s"}}
+    host = host_cpu()
+    out = {"value": uT / tT, "unit": "rollout-steps/s", "cores": T, "kind": "port", "host": host,
+           "sample": f"{nT} full cfg2 MPPIPlan solves (K=8192, H=50, grid, Philox noise) in {tT:.1f} s on {T} "
+                     f"threads (one solve per thread at a time), scalar C oracle, {os.cpu_count()}-CPU host",
+           "single_thread": {"value": u1 / t1, "cores": 1, "sample": f"{n1} solves in {t1:.1f} s"},
+           "why_these_threads": "the GPU pool gives each one-GPU job a 16-CPU share of the host (it sets "
+                                "OMP_NUM_THREADS=16 and asks worker pools to stay within it); the other CPUs of "
+                                "the affinity set belong to the other GPUs' jobs, so they are not timed"}
+    # all cores of the affinity set: the solves are independent, so the measured per-thread
+    # rate at T threads scaled to every usable CPU is an upper bound on what the whole host would give
+    n_all = host["usable_cpus"] or T
+    out["all_cores_projection"] = {"value": uT / tT / T * n_all, "cores": n_all, "kind": "projected",
+                                   "basis": f"measured {uT / tT / T:.4g} rollout-steps/s per thread at {T} threads "
+                                            f"x {n_all} usable CPUs (linear: no shared state between solves)"}
+    return out
 
 
 if __name__ == "__main__":

@@ -228,7 +228,8 @@ int mp_mppi_closed_loop(mp_ctx* ctx, const mp_mppi_params* p, const mp_mppi_loop
  * (ncclCommInitAll over the contexts' devices, xGMI between MI355X GPUs).  ctxs[i] is rank i; every
  * call below takes the same array in the same order.  Errors are reported on ctxs[0]
  * (mp_last_error(ctxs[0])).  RCCL is loaded on first use: MP_ERR_UNSUPPORTED without librccl.
- * Call mp_comm_destroy before destroying the contexts.
+ * Call mp_comm_destroy before destroying the contexts: mp_ctx_destroy refuses (MP_ERR_INVALID) a
+ * context that still belongs to a communicator.
  */
 int mp_comm_init(mp_ctx** ctxs, int32_t n);
 int mp_comm_destroy(mp_ctx** ctxs, int32_t n);

@@ -3,24 +3,31 @@
 // with ncclCommInitAll; collectives are enqueued on each context's own stream inside
 // ncclGroupStart/End (one thread, several devices).  RCCL is loaded with dlopen on first use, so
 // libmpgpu has no link-time dependency on it and a host without librccl gets MP_ERR_UNSUPPORTED
-// from mp_comm_init instead of a load failure of the whole library.
+// from mp_comm_init instead of a load failure of the whole library.  The few RCCL types and entry
+// points used here are declared locally (the stable NCCL 2.x C ABI), so building libmpgpu does not
+// need the RCCL headers either.
 #include <dlfcn.h>
-#include <rccl/rccl.h>
 
 #include <mutex>
 #include <vector>
 
 #include "runtime.hpp"
 
+// NCCL 2.x ABI (rccl.h): ncclComm_t is an opaque pointer, ncclResult_t / ncclDataType_t are C enums
+typedef struct ncclComm* ncclComm_t;
+typedef int ncclResult_t;
+static constexpr ncclResult_t ncclSuccess = 0;
+static constexpr int ncclUint8 = 1;
+
 namespace {
 
 struct Rccl {
-  decltype(&ncclCommInitAll) init_all = nullptr;
-  decltype(&ncclCommDestroy) destroy = nullptr;
-  decltype(&ncclAllGather) all_gather = nullptr;
-  decltype(&ncclGroupStart) group_start = nullptr;
-  decltype(&ncclGroupEnd) group_end = nullptr;
-  decltype(&ncclGetErrorString) err = nullptr;
+  ncclResult_t (*init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char* (*err)(ncclResult_t) = nullptr;
   bool ok = false;
   std::string why;
 };
@@ -71,12 +78,20 @@ int mp_comm_allgather(mp_ctx** ctxs, int n, void* const* send, void* const* recv
   if (st) return st;
   const Rccl& R = rccl();
   mp_comm_group* g = ctxs[0]->comm;
+  int dev0 = 0;
+  hipGetDevice(&dev0);
   ncclResult_t e = R.group_start();
+  bool dev_ok = true;
   for (int i = 0; i < n && e == ncclSuccess; i++) {
-    if (hipSetDevice(ctxs[i]->device) != hipSuccess) return mp_fail(ctxs[0], MP_ERR_HIP, "hipSetDevice failed");
+    if (hipSetDevice(ctxs[i]->device) != hipSuccess) {
+      dev_ok = false;  // leave the loop, but still close the group below
+      break;
+    }
     e = R.all_gather(send[i], recv[i], bytes, ncclUint8, g->comms[i], ctxs[i]->stream);
   }
-  const ncclResult_t e2 = R.group_end();
+  const ncclResult_t e2 = R.group_end();  // always: a group left open would poison the next RCCL call
+  hipSetDevice(dev0);
+  if (!dev_ok) return mp_fail(ctxs[0], MP_ERR_HIP, "hipSetDevice failed inside the all-gather group");
   if (e == ncclSuccess) e = e2;
   if (e != ncclSuccess) return mp_fail(ctxs[0], MP_ERR_HIP, "ncclAllGather: %s", R.err(e));
   return MP_OK;

@@ -2203,12 +2203,15 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
               mp_ws_affordable(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2, 0.5) &&
               mp_ws_affordable(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2, 0.25);
   double *dXs2 = nullptr, *dUs2 = nullptr, *dJt = nullptr;
-  int* dpw = nullptr;  // pending[B], winm[B], mstar[B]; pipelined: pend[2][B], winm[2][B], mstar[2][B]
+  // pending[B], winm[B], mstar[B]; pipelined: pend[2][B], winm[2][B], mstar[2][B] at [0, 6B);
+  // the one-pass search has its own winm[B], mstar[B] at [6B, 8B), so it never reads a slot the
+  // pipelined launches left set
+  int* dpw = nullptr;
   if (rest) {
     dXs2 = (double*)mp_ws(ctx, WS_ILQR1, sizeof(double) * 4 * N * B * T2);
     dUs2 = dXs2 ? (double*)mp_ws(ctx, WS_ILQR2, sizeof(double) * 2 * N * B * T2) : nullptr;
     dJt = dUs2 ? (double*)mp_ws(ctx, WS_IO12, sizeof(double) * B * T2) : nullptr;
-    dpw = dJt ? (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 6 * (size_t)B) : nullptr;
+    dpw = dJt ? (int*)mp_ws(ctx, WS_IO13, sizeof(int) * 8 * (size_t)B) : nullptr;
     if (!dXs2 || !dUs2 || !dJt || !dpw) {
       rest = false;      // fall back to the multi-round 16-wide search
       ctx->err.clear();  // (the failed allocation left a message; mp_ws already cleared the HIP error)
@@ -2262,15 +2265,20 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     if ((st = run_backward(ctx, D, B, dX, dU, dn + 1, dn, n_act, dk, dK))) return st;
     MP_HIP(ctx, hipMemsetAsync(dnp, 0, 2 * sizeof(int), ctx->stream));
     mp_time_begin(ctx);
-    if (rest && n_act <= kOnePassMax) {
-      if (!onepass_armed) MP_HIP(ctx, hipMemsetAsync(dpw + B, 0x7f, sizeof(int) * B, ctx->stream));  // winm
+    // The switch to the one-pass search is terminal (once armed it stays, whatever later polls
+    // say).  Instances the last pipelined launch left pending keep their active flag and their
+    // gains (they sat the backward pass out), so the one-pass search reruns them from trial 0:
+    // trials 0..15 give the bits round 0 gave, so they end exactly where their rest pass would.
+    if (rest && (onepass_armed || n_act <= kOnePassMax)) {
+      int *winm1 = dpw + 6 * (size_t)B, *ms1 = dpw + 7 * (size_t)B;
+      if (!onepass_armed) MP_HIP(ctx, hipMemsetAsync(winm1, 0x7f, sizeof(int) * B, ctx->stream));
       onepass_armed = true;
       hipLaunchKernelGGL((ilqr_search_rest_kernel<kSearchG, kSearchL>),
                          dim3((unsigned)B, (unsigned)((T2 + 64 / kSearchL - 1) / (64 / kSearchL))), b1, 0, ctx->stream, D,
-                         B, dX, dU, dk, dK, dJ, dact, dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, 0, T2);
+                         B, dX, dU, dk, dK, dJ, dact, ms1, dXs2, dUs2, dJt, winm1, 0, T2);
       MP_HIP(ctx, hipGetLastError());
       hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dact,
-                         dpw + 2 * B, dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, 0, T2, 2);
+                         ms1, dXs2, dUs2, dJt, winm1, dJ, dact, dit, dfl, dn, 0, T2, 2);
       MP_HIP(ctx, hipGetLastError());
       mp_time_end(ctx);
       bool stop;

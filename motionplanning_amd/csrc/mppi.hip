@@ -1364,16 +1364,39 @@ int mp_mppi_plan_sharded(mp_ctx** ctxs, int32_t n, const mp_mppi_params* p, int3
   const int base = S / n, rem = S % n, smax = base + (rem > 0);
   auto lo = [&](int r) { return r * base + (r < rem ? r : rem); };
   std::vector<void*> send(n), recv(n);
+  // the caller's current device is restored on every return; an error after some ranks have
+  // enqueued work drains those ranks first, so nothing of this call is left running
+  int dev0 = 0;
+  hipGetDevice(&dev0);
+  int enq = 0;  // ranks [0, enq) have work enqueued
+  auto done = [&](int status) {
+    for (int r = 0; r < enq; r++) {
+      hipSetDevice(ctxs[r]->device);
+      mp_sync_all(ctxs[r]);
+    }
+    hipSetDevice(dev0);
+    return status;
+  };
+#define MP_SH(call)                                                                       \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return done(mp_fail(c0, MP_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)));       \
+  } while (0)
   // every rank plans its block [a, b) of scenes (Philox counter word scene_base + a: the same noise as
   // one mp_mppi_plan over all S) and packs its results; all launches are enqueued before any wait
   for (int r = 0; r < n; r++) {
     mp_ctx* c = ctxs[r];
-    MP_HIP(c0, hipSetDevice(c->device));
+    MP_SH(hipSetDevice(c->device));
     const int a = lo(r), cnt = lo(r + 1) - a;
     const size_t sa = a, sc = cnt;
     send[r] = mp_ws(c, WS_SHARD_SEND, sizeof(double) * (size_t)smax * Dr);
     recv[r] = mp_ws(c, WS_SHARD_RECV, sizeof(double) * (size_t)n * smax * Dr);
-    if (!send[r] || !recv[r]) return mp_fail(c0, MP_ERR_NOMEM, "rank %d: %s", r, c->err.c_str());
+    if (!send[r] || !recv[r]) return done(mp_fail(c0, MP_ERR_NOMEM, "rank %d: %s", r, c->err.c_str()));
+    // every rank's NaN flag is cleared, also on a rank without scenes: the flags of all ranks are
+    // read back below, and a flag left from an earlier call must not report a NaN of this one
+    enq = r + 1;
+    MP_SH(hipMemsetAsync(c->flags, 0, sizeof(int), c->stream));
     if (cnt == 0) continue;  // more ranks than scenes: this rank only takes part in the gather
     st = MP_OK;
     const double* dX0 = mp_upload(c, WS_IO0, X0 + 7 * sa, 7 * sc, &st);
@@ -1391,32 +1414,34 @@ int mp_mppi_plan_sharded(mp_ctx** ctxs, int32_t n, const mp_mppi_params* p, int3
     int32_t* drc = (int32_t*)mp_ws(c, WS_IO10, sizeof(int32_t) * sc);
     int32_t* dfc = (int32_t*)mp_ws(c, WS_IO11, sizeof(int32_t) * sc);
     if (st || !dU || !dtraj || !dcost || !dfe || !drc || !dfc)
-      return mp_fail(c0, st ? st : MP_ERR_NOMEM, "rank %d: %s", r, c->err.c_str());
-    MP_HIP(c0, hipMemsetAsync(c->flags, 0, sizeof(int), c->stream));
+      return done(mp_fail(c0, st ? st : MP_ERR_NOMEM, "rank %d: %s", r, c->err.c_str()));
     MppiDev Dr_ = D;
     Dr_.scene_base = p->scene_base + a;
     if ((st = plan_launch(c, Dr_, cnt, dX0, dgoal, dun, dobs, dgrid, dnoise, dU, dtraj, dcost, dfe, drc, dfc, nullptr,
                           nullptr, nullptr, nullptr, p->final_stream)))
-      return mp_fail(c0, st, "rank %d: %s", r, c->err.c_str());
-    if (p->final_stream && (st = mp_ctx_join(c))) return mp_fail(c0, st, "rank %d: %s", r, c->err.c_str());
+      return done(mp_fail(c0, st, "rank %d: %s", r, c->err.c_str()));
+    if (p->final_stream && (st = mp_ctx_join(c))) return done(mp_fail(c0, st, "rank %d: %s", r, c->err.c_str()));
     const long long tot = (long long)cnt * (long long)Dr;
     hipLaunchKernelGGL(shard_pack_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, c->stream, cnt, (int)H,
                        dU, dtraj, dcost, dfe, drc, dfc, (double*)send[r]);
-    MP_HIP(c0, hipGetLastError());
+    MP_SH(hipGetLastError());
   }
   // the exchange step: every GPU ends with every scene's results (RCCL all-gather over xGMI)
-  if ((st = mp_comm_allgather(ctxs, n, send.data(), recv.data(), sizeof(double) * (size_t)smax * Dr))) return st;
+  if ((st = mp_comm_allgather(ctxs, n, send.data(), recv.data(), sizeof(double) * (size_t)smax * Dr)))
+    return done(st);
   std::vector<double> all((size_t)n * smax * Dr);
-  MP_HIP(c0, hipSetDevice(c0->device));
-  MP_HIP(c0, hipMemcpyAsync(all.data(), recv[0], all.size() * sizeof(double), hipMemcpyDeviceToHost, c0->stream));
+  MP_SH(hipSetDevice(c0->device));
+  MP_SH(hipMemcpyAsync(all.data(), recv[0], all.size() * sizeof(double), hipMemcpyDeviceToHost, c0->stream));
   int nan = 0;
   for (int r = 0; r < n; r++) {
     int f = 0;
-    MP_HIP(c0, hipSetDevice(ctxs[r]->device));
-    MP_HIP(c0, hipMemcpyAsync(&f, ctxs[r]->flags, sizeof(int), hipMemcpyDeviceToHost, ctxs[r]->stream));
-    MP_HIP(c0, hipStreamSynchronize(ctxs[r]->stream));
+    MP_SH(hipSetDevice(ctxs[r]->device));
+    MP_SH(hipMemcpyAsync(&f, ctxs[r]->flags, sizeof(int), hipMemcpyDeviceToHost, ctxs[r]->stream));
+    MP_SH(hipStreamSynchronize(ctxs[r]->stream));
     nan |= f & 1;
   }
+#undef MP_SH
+  hipSetDevice(dev0);
   for (int r = 0; r < n; r++)
     for (int s = lo(r), j = 0; s < lo(r + 1); s++, j++) {
       const double* q = all.data() + ((size_t)r * smax + j) * Dr;

@@ -209,6 +209,10 @@ int mp_ctx_create(int device, mp_ctx** out) {
 
 int mp_ctx_destroy(mp_ctx* ctx) {
   if (!ctx) return MP_OK;
+  // a context still joined to an RCCL communicator would leave the group's other ranks with a
+  // dangling rank: the caller must run mp_comm_destroy over the whole group first
+  MP_CHECK(ctx, ctx->comm == nullptr, "context is rank %d of a communicator: call mp_comm_destroy first",
+           ctx->comm_rank);
   hipSetDevice(ctx->device);
   mp_sync_all(ctx);
   for (void* p : ctx->ws_ptr)

@@ -9,8 +9,9 @@ does exactly one all-gather at the end, the exchange step the north star names:
   the rank's block with ``scene_base = a`` (the Philox counter word), so every scene draws
   the stream it would draw on one GPU; then an all-gather of the optimal controls
   (S×H×2 f64 — 6.4 KB per rank at 8 scenes × H=50) plus the per-scene scalars;
-* Hybrid A* (configs[3]): scenarios [a, b) per rank, each rank runs its own lockstep
-  search (``mp_ha_plan``); all-gather of the outcome (found, pops, nodes, RS length);
+* Hybrid A* (configs[3]): scenarios r, r + world, r + 2 world, ... per rank (strided: every rank
+  gets the same mix of perpendicular and parallel scenes), each rank runs its own lockstep search
+  (``mp_ha_plan``); all-gather of the outcome (found, pops, nodes, RS length) back into batch order;
 * iLQR (configs[2]): instances [a, b) per rank (replicas of the solver); all-gather of
   J and the iteration counts.
 
@@ -57,9 +58,21 @@ def shard_bounds(n, rank, world):
     return a, a + base + (1 if rank < rem else 0)
 
 
-def all_gather_rows(local, n_total, device=None):
-    """Concatenate every rank's leading-axis block (shard_bounds order) into n_total rows.
-    Blocks are padded to the largest shard so one fixed-size collective suffices
+def shard_indices(n, rank, world, strided=False):
+    """The units of `rank`: the contiguous block shard_bounds gives, or (strided) every world-th unit
+    from `rank` on.  Both give rank r the same number of units (the first n % world ranks one extra).
+    Hybrid A* uses the strided split: scenario_batch lists its 128 perpendicular scenes before the 128
+    parallel ones, and a contiguous split hands every long perpendicular search to the first half of
+    the ranks, while the strided split gives every rank the same mix."""
+    if strided:
+        return np.arange(rank, n, world)
+    a, b = shard_bounds(n, rank, world)
+    return np.arange(a, b)
+
+
+def all_gather_rows(local, n_total, device=None, strided=False):
+    """Every rank's leading-axis rows (its shard_indices) gathered back into n_total rows in unit
+    order.  Blocks are padded to the largest shard so one fixed-size collective suffices
     (all_gather_into_tensor on RCCL; all_gather on gloo)."""
     rank, world = _world()
     arr = np.ascontiguousarray(local)
@@ -79,11 +92,11 @@ def all_gather_rows(local, n_total, device=None):
     else:
         parts = [torch.empty_like(t) for _ in range(world)]
         dist.all_gather(parts, t)
-    blocks = []
+    out = np.empty((n_total,) + tail, dtype=arr.dtype)
     for r in range(world):
-        a, b = shard_bounds(n_total, r, world)
-        blocks.append(parts[r][: b - a].cpu().numpy())
-    return np.concatenate(blocks, axis=0)
+        idx = shard_indices(n_total, r, world, strided)
+        out[idx] = parts[r][: len(idx)].cpu().numpy()
+    return out
 
 
 def _params_copy(p):
@@ -127,19 +140,18 @@ def hybrid_astar_sharded(searchers, planner=None, ctx=None, max_pops=5000):
 
     rank, world = _world()
     n = len(searchers)
-    a, b = shard_bounds(n, rank, world)
-    mine = searchers[a:b]
+    mine = [searchers[i] for i in shard_indices(n, rank, world, strided=True)]
     if mine:
         (planner or (lambda hs: ha.plan_batch(hs, ctx=ctx, max_pops=max_pops)))(mine)
     out = np.array([[int(h.r.found), h.r.loop_count, h.r.n_nodes, h.r.RSpath_final.shape[1]] for h in mine],
                    np.int64).reshape(-1, 4)
-    g = all_gather_rows(out, n)
+    g = all_gather_rows(out, n, strided=True)
     return dict(found=g[:, 0].astype(bool), pops=g[:, 1], n_nodes=g[:, 2], rs_len=g[:, 3])
 
 
 def track_sharded(searchers, ctx=None, settings=None, runner=None):
     """retrievePath + the main_Tracker.jl loop for this rank's shard of a planned batch (the same
-    [a, b) split as hybrid_astar_sharded, so each rank tracks what it planned).  Every rank returns
+    strided split as hybrid_astar_sharded, so each rank tracks what it planned).  Every rank returns
     the gathered {status, n_steps} for the whole batch.  `runner(mine)` replaces the device calls
     (the gloo tests run the oracle there)."""
     from . import hybrid_astar as ha
@@ -147,8 +159,7 @@ def track_sharded(searchers, ctx=None, settings=None, runner=None):
 
     rank, world = _world()
     n = len(searchers)
-    a, b = shard_bounds(n, rank, world)
-    mine = searchers[a:b]
+    mine = [searchers[i] for i in shard_indices(n, rank, world, strided=True)]
     if mine and runner is not None:
         runner(mine)
     elif mine:
@@ -156,7 +167,7 @@ def track_sharded(searchers, ctx=None, settings=None, runner=None):
         tracker.track_batch(mine, ctx=ctx, settings=settings)
     inv = {v: k for k, v in tracker.STATUS.items()}
     out = np.array([[inv[h.r.tracking["status"]], h.r.tracking["n_steps"]] for h in mine], np.int64).reshape(-1, 2)
-    g = all_gather_rows(out, n)
+    g = all_gather_rows(out, n, strided=True)
     return dict(status=g[:, 0], n_steps=g[:, 1])
 
 

@@ -162,7 +162,9 @@ def params_of(mppi, noise_mode):
 def mppi_plan_batch(p: MPPIParams, X0, goal, U_nom, obstacles=None, grid=None, noise=None, collect=False,
                     ctx=None):
     """S independent MPPIPlan solves in one launch.  Shapes: X0 (S,7), goal (S,2), U_nom (S,H,2),
-    obstacles (S,n_obs,3), grid (S,ny,nx) uint8, noise (S,K,H,2) or None (Philox)."""
+    obstacles (S,n_obs,3), grid (S,ny,nx) uint8, noise (S,K,H,2) or None (Philox).
+    collect: True = the whole TrajectoryCollection, "costs" = only its costs and feasibility flags
+    (the large state / control lists stay on the device), False = none."""
     ctx = ctx or default_context()
     X0 = f64(X0).reshape(-1, 7)
     S, K, H = X0.shape[0], p.K, p.H
@@ -182,14 +184,15 @@ def mppi_plan_batch(p: MPPIParams, X0, goal, U_nom, obstacles=None, grid=None, n
     coll = {}
     if collect:
         # device layout: structure of arrays, rollout index fastest (include/mpgpu.h)
-        coll = dict(traj_soa=np.zeros((S, H + 1, 7, K)), ctrl_soa=np.zeros((S, H, K, 2)), cost=np.zeros((S, K)),
-                    feas=np.zeros((S, K), np.uint8))
+        coll = dict(cost=np.zeros((S, K)), feas=np.zeros((S, K), np.uint8))
+        if collect != "costs":
+            coll.update(traj_soa=np.zeros((S, H + 1, 7, K)), ctrl_soa=np.zeros((S, H, K, 2)))
     st = ctx.lib.mp_mppi_plan(ctx.handle, ctypes.byref(p), S, ptr(X0), ptr(goal), ptr(U_nom), ptr(obstacles),
                               ptr(grid), ptr(noise), ptr(out["U"]), ptr(out["traj"]), ptr(out["cost"]),
                               ptr(out["feasible"]), ptr(out["rollout_count"]), ptr(out["feasible_count"]),
                               ptr(coll.get("traj_soa")), ptr(coll.get("ctrl_soa")), ptr(coll.get("cost")),
                               ptr(coll.get("feas")))
-    if collect:  # reference-shaped views: traj (S, K, H+1, 7), ctrl (S, K, H, 2)
+    if collect and collect != "costs":  # reference-shaped views: traj (S, K, H+1, 7), ctrl (S, K, H, 2)
         coll["traj"] = coll["traj_soa"].transpose(0, 3, 1, 2)
         coll["ctrl"] = coll["ctrl_soa"].transpose(0, 2, 1, 3)
     out["nan"] = st == MP_ERR_NUMERIC

@@ -122,6 +122,20 @@ def test_shard_bounds():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_shard_indices_partition():
+    """Both splits partition 0..n-1 with the same shard sizes; the strided one gives every rank of the
+    configs[3] batch (128 perpendicular scenes, then 128 parallel) the same mix of the two."""
+    for n in range(0, 20):
+        for w in (1, 2, 3, 8):
+            for strided in (False, True):
+                parts = [D.shard_indices(n, r, w, strided) for r in range(w)]
+                assert sorted(np.concatenate(parts).tolist()) == list(range(n))
+                assert [len(q) for q in parts] == [b - a for a, b in (D.shard_bounds(n, r, w) for r in range(w))]
+    for r in range(8):
+        idx = D.shard_indices(256, r, 8, strided=True)
+        assert (idx < 128).sum() == 16 and (idx >= 128).sum() == 16
+
+
 def test_params_copy_is_deep():
     p = configs.cfg1()["params"]
     q = D._params_copy(p)

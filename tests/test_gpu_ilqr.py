@@ -177,6 +177,32 @@ def test_solve_configs2_horizon_bitexact(ctx):
     assert stalled > 0  # the rest pass (trials 16..max_ls) was exercised
 
 
+def test_solve_bench_workload_full_size_bitexact(ctx):
+    """The bench's own configs[2] solve (bench.py bench_ilqr: 4,096 instances x H=100 from
+    cfg3_instances(seed=3), rolled out, then mp_ilqr_solve with max_iter 60; ILQR.jl:44-88) vs the
+    oracle's sequential loop for EVERY instance (threaded): iteration counts, J, X and U bit for bit.
+    Covers the pipelined search at full activity, the switch to the one-pass search with instances
+    still pending, the trial-fixpoint cutoff and the max_ls stops."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    B, N = 4096, 100
+    p = ilqr.params(N=N, max_iter=60)
+    x0, U0 = ilqr.cfg3_instances(B, N, seed=3)
+    X0, _ = ilqr.ilqr_rollout(p, x0, U0, ctx=ctx)
+    X, U, J, it, ok = ilqr.ilqr_solve(p, X0, U0, ctx=ctx)
+
+    def ref(b):
+        return oracle.ilqr_solve(p, X0[b], U0[b])
+
+    with ThreadPoolExecutor(16) as ex:
+        refs = list(ex.map(ref, range(B)))
+    bad = [b for b, (Xo, Uo, Jo, ito, flags) in enumerate(refs)
+           if not (it[b] == ito and J[b] == Jo and np.array_equal(X[b], Xo) and np.array_equal(U[b], Uo))]
+    assert not bad, (len(bad), bad[:8])
+    stalled = sum(bool(r[4] & 1) for r in refs)
+    assert stalled > 0 and int(it.max()) > 20  # max_ls stops and long searches were exercised
+
+
 # N-1 = 19, 20, 21, 22: every residue of the trial's last 4-knot store group in round 0
 @pytest.mark.parametrize("B,N", [(2048, 20), (768, 21), (768, 22), (768, 23)])
 def test_solve_pipelined_search_bitexact(ctx, B, N):

@@ -209,11 +209,11 @@ def test_jlmath_bitexact(ctx):
         assert np.array_equal(out.view(np.int64), cpu.view(np.int64)), (fn, names[fn], x[out.view(np.int64) != cpu.view(np.int64)][:5])
 
 
-@pytest.mark.parametrize("base", [0, 56])
+@pytest.mark.parametrize("base", [0, 8, 16, 24, 32, 40, 48, 56])
 def test_bench_workload_full_size_bitexact(ctx, base):
     """The headline bench workload itself (bench.py run(): configs[4] per-GPU shard = 8 of the 64 scenes,
     each configs[1], K=8192, H=50, its own X0 and its own occupancy grid from obstacle_field.mat field g+1
-    (rank 0's fields 1-8 and rank 7's fields 57-64), device Philox noise seeded 20260415, step offset 3,
+    (every rank's shard of the world-8 job: fields base+1..base+8), device Philox noise seeded 20260415, step offset 3,
     final rollout on the side stream) vs 8 oracle MPPIPlan solves with the same Philox stream (threaded):
     every rollout's cost, feasibility, controls and states bit for bit, MPPICtrl / final trajectory within
     the stated tolerance."""
@@ -242,7 +242,8 @@ def test_bench_workload_full_size_bitexact(ctx, base):
 def test_scene_batching_invariance(ctx):
     """Sharding correctness on the device: a scene planned inside an 8-scene launch equals the same scene
     planned alone with scene_base = its global index (the Philox counter word a rank of a sharded job
-    passes), bit for bit -- so results do not depend on how scenes are grouped into launches or ranks."""
+    passes), bit for bit, while both launches use the same layout (here K=1024: lane pairs, 256-thread
+    blocks).  Across layouts see test_scene_batching_across_layouts."""
     import ctypes as _ct
 
     from motionplanning_amd.abi import MP_NOISE_PHILOX, MPPIParams
@@ -265,6 +266,39 @@ def test_scene_batching_invariance(ctx):
         for key in ("cost", "feas", "ctrl", "traj"):
             assert np.array_equal(one["coll"][key][0], whole["coll"][key][s]), (s, key)
         assert np.array_equal(one["U"][0], whole["U"][s]) and one["cost"][0] == whole["cost"][s]
+
+
+def test_scene_batching_across_layouts(ctx):
+    """configs[4] at full size: the 64 scenes planned as eight 8-scene launches (each rank's shard:
+    lane pairs, 512-thread blocks) and as one 64-scene launch (one rollout per lane).  The launch layout
+    follows S*K (mppi.hip plan_launch), and the log-sum-exp combine of MPPICtrl sums block partials whose
+    grouping follows the layout, so:
+      * every rollout (noise, costs, feasibility flags) and the counts are bit-identical;
+      * MPPICtrl, the final trajectory and its cost agree within the stated tolerance (rtol 1e-9), not
+        bit for bit."""
+    from motionplanning_amd.abi import MP_NOISE_PHILOX
+
+    c = configs.cfg5_shard(0, 64, noise_mode=MP_NOISE_PHILOX, seed=20260415)
+    p = c["params"]
+    p.offset = 5
+    X0, goal, grid = c["X0"], c["goal"], c["grid"]
+    un = np.zeros((64, p.H, 2))
+    whole = mppi_plan_batch(p, X0, goal, un, None, grid, None, collect="costs", ctx=ctx)
+    base0 = p.scene_base
+    for a in range(0, 64, 8):
+        p.scene_base = base0 + a
+        part = mppi_plan_batch(p, X0[a:a + 8], goal[a:a + 8], un[a:a + 8], None, grid[a:a + 8], None,
+                               collect="costs", ctx=ctx)
+        sl = slice(a, a + 8)
+        assert np.array_equal(part["coll"]["cost"], whole["coll"]["cost"][sl]), a
+        assert np.array_equal(part["coll"]["feas"], whole["coll"]["feas"][sl]), a
+        assert np.array_equal(part["rollout_count"], whole["rollout_count"][sl])
+        assert np.array_equal(part["feasible_count"], whole["feasible_count"][sl])
+        np.testing.assert_allclose(part["U"], whole["U"][sl], rtol=1e-9, atol=1e-12)
+        np.testing.assert_allclose(part["traj"], whole["traj"][sl], rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(part["cost"], whole["cost"][sl], rtol=1e-9)
+        assert np.array_equal(part["feasible"], whole["feasible"][sl])
+    p.scene_base = base0
 
 
 def test_cfg2_default_feasibility_count_full_size(ctx):

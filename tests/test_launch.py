@@ -63,4 +63,5 @@ def test_bench_gpus_flag_reaches_the_launcher():
     src = open(os.path.join(ROOT, "bench.py")).read()
     main = src[src.index("def main():"):]
     assert main.index("relaunch_if_needed(a.gpus)") < main.index("torch.cuda.set_device")
-    assert '"n_gpus": dist.get_world_size()' in src
+    # n_gpus counts the distinct devices the ranks joined on (a --share-device rehearsal reports 1)
+    assert '"n_gpus": len({(int(r[2]), int(r[3])) for r in joined})' in src

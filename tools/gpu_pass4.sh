@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-4 GPU pass: parity tests, PMC passes (each its own run), kernel-trace stats, per-leg traces
+# (solve-only iLQR, plan-only Hybrid A*), rooflines, bench, the N=2 share-device rehearsal.
+# usage: bash tools/gpu_pass4.sh TAG [pytest-args...]      (TAG=...-notest skips pytest)
+set -o pipefail
+TAG=${1:-run}; shift
+O=gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+if [[ "$TAG" != *notest* ]]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $O/pytest_gpu.log 2>&1
+  rc=$?
+  echo "pytest exit $rc"; tail -5 $O/pytest_gpu.log
+  if [ $rc -ne 0 ]; then exit $rc; fi
+fi
+BM="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-single --no-extras"  # MPPI headline launches only
+BX="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-single"
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA"
+timeout -k 10 200 rocprofv3 --pmc $SQ -d $O/pmc1 -o run --output-format csv -- $BM > $O/pmc1.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc $SQ -d $O/pmc4 -o run --output-format csv -- $BX > $O/pmc4.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pmc2 -o run --output-format csv -- $BM > $O/pmc2.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pmc3 -o run --output-format csv -- $BM > $O/pmc3.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_ilqr -o run --output-format csv -- python3 tools/ilqr_time.py --solve-only > $O/prof_ilqr.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --pmc $SQ -d $O/pmc_ilqr -o run --output-format csv -- python3 tools/ilqr_time.py --solve-only > $O/pmc_ilqr.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_ha -o run --output-format csv -- python3 tools/ha_plan_time.py > $O/prof_ha.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --pmc $SQ -d $O/pmc_ha -o run --output-format csv -- python3 tools/ha_plan_time.py > $O/pmc_ha.log 2>&1 &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 30 --warmup 3 --no-cpu > $O/prof.log 2>&1 &&
+python3 tools/pmc_traffic.py $O 8 8192 50 > $O/traffic.json &&
+python3 tools/pmc_roofline.py $O > $O/roofline.json &&
+timeout -k 10 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 10 --traffic $O/traffic.json --roofline $O/roofline.json > $O/bench.log 2>&1
+rc=$?
+echo "chain exit $rc"; tail -c 3000 $O/bench.log
+[ $rc -ne 0 ] && exit $rc
+# N>1 rehearsal of the driver's launch (bench.py --gpus 2 spawns two ranks; both on cuda:0, gloo)
+timeout -k 10 400 python bench.py --gpus 2 --share-device --steps 10 --warmup 2 --no-cpu > $O/bench_n2.log 2>&1
+rc=$?
+echo "n2 exit $rc"; tail -c 1500 $O/bench_n2.log
+exit $rc
