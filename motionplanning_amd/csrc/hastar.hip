@@ -400,6 +400,8 @@ struct IterArgs {
   int do_rs, do_exp;
   int rs_path_free_only;  // RS_connected writes its path only when it is collision-free (the planner
                           // reads it only then); the standalone entry point writes every path
+  int coherent;           // ha_step_kernel: the per-scene outputs the same launch's bookkeeping reads
+                          // (neighbour records, rs_ok / rs_len) are stored agent-coherent (st_ag)
   // RS_connected outputs (per scene)
   unsigned char* rs_ok;  // [B]
   double* rs_path;       // [B][501][3]
@@ -410,6 +412,24 @@ struct IterArgs {
   unsigned char* fr;     // [B][n_prim]
   double* h;             // [B][n_prim]
 };
+
+// Agent-coherent relaxed stores / loads (global_store / global_load with the sc1 policy: they reach
+// and read the device coherence point, past the per-XCD L2).  ha_step_kernel hands per-scene records
+// from one block to another inside a launch with these, ordered by s_waitcnt + an arrival ticket,
+// so no block needs an agent-scope release fence (an L2 write-back of the whole XCD).
+template <class T>
+__device__ __forceinline__ void st_ag(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_ag(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_out(bool coh, T* p, T v) {
+  if (coh) st_ag(p, v);
+  else *p = v;
+}
 
 // output addressing: per scene
 struct OutRef {
@@ -583,10 +603,10 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     transform1(node, A.sc + 3 * k, t);
     regulate(P, t, nb);
     const long long ix = encode(P, nb);
-    R.nb[3 * k] = nb[0];
-    R.nb[3 * k + 1] = nb[1];
-    R.nb[3 * k + 2] = nb[2];
-    R.idx[k] = ix;
+    st_out(A.coherent, R.nb + 3 * k, nb[0]);
+    st_out(A.coherent, R.nb + 3 * k + 1, nb[1]);
+    st_out(A.coherent, R.nb + 3 * k + 2, nb[2]);
+    st_out(A.coherent, R.idx + k, ix);
     g_nb[tid][0] = nb[0];
     g_nb[tid][1] = nb[1];
     g_nb[tid][2] = nb[2];
@@ -756,15 +776,15 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   __syncthreads();
   if (rs) {
     if (tid == 0) {
-      *R.ok = (unsigned char)g_free[0];
-      *R.len = sh_n;
+      st_out(A.coherent, R.ok, (unsigned char)g_free[0]);
+      st_out(A.coherent, R.len, sh_n);
     }
     if (A.rs_path_free_only && g_free[0])  // block-uniform (after the barrier above)
       for (int i = tid; i < 3 * sh_n; i += HT) R.path[i] = path_s[i];
   } else if (tid < 64 && (lane & 3) == 0 && j < nk) {
     const int fr = g_ix[j] != 0 && g_free[j];
-    R.fr[k0 + j] = (unsigned char)fr;
-    R.h[k0 + j] = fr ? cb * P.minR : 0.0;
+    st_out(A.coherent, R.fr + k0 + j, (unsigned char)fr);
+    st_out(A.coherent, R.h + k0 + j, fr ? cb * P.minR : 0.0);
   }
   return true;
 }
@@ -904,9 +924,12 @@ struct HaSearch {
   long long* start_index;// [B]
   long long* pop_seq;    // [B][mp]
   double* states;        // [B][mp][3] hybrid_astar_states (goal side first)
-  double* node;          // [B][3] popped node state: the next iteration's input
+  double* node;          // [2][B][3] popped node state: the next iteration's input (iteration i pops into
+                         // buffer i & 1 while its blocks read buffer (i - 1) & 1)
   int* live;             // [mp + 2] scenes still searching after iteration i
   int* lst;              // [2][B] those scenes' indices (iteration i writes list i & 1, in any order)
+  int* tk;               // [2][B] ha_step_kernel arrival tickets: neighbour groups, then (RS block, bookkeeping)
+  long long* rec;        // [B][8] ha_step_kernel: the bookkeeping's record for the scene's finisher
 };
 enum { SI_NNODES = 0, SI_NOPEN, SI_LOOP, SI_CUR, SI_ACTIVE, SI_FOUND, SI_NSTATES, SI_RSLEN, SI_N };
 
@@ -949,13 +972,19 @@ __device__ __forceinline__ void key_min_dpp(double& f, long long& sq, int& p) {
 // reduction (the key order is total, so the reduction order does not matter); wave 0 removes
 // it by moving the last entry into its place.  Returns false (block-uniform) when the search
 // ends here (open list empty / max_pops).
+// NT threads (a multiple of 64).  The popped state goes to node_out[3 * b]; direct: the pop count and
+// pop_seq are written here (ha_init_kernel, ha_book_kernel), else they are left to the scene's finisher
+// in ha_step_kernel and the popped Encode index is returned in *iw_out (lane 0 of wave 0).
 constexpr int BKT = 256;
-__device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int tid) {
-  __shared__ double r_f[BKT / 64];
-  __shared__ long long r_s[BKT / 64];
-  __shared__ int r_p[BKT / 64];
-  __shared__ double r_pay[BKT / 64][5];  // the wave winner's entry: g, Encode index, state
-  __shared__ int r_id[BKT / 64];
+template <int NT>
+__device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int tid,
+                                       double* node_out, bool direct, long long* iw_out) {
+  static_assert(NT % 64 == 0, "whole waves");
+  __shared__ double r_f[NT / 64];
+  __shared__ long long r_s[NT / 64];
+  __shared__ int r_p[NT / 64];
+  __shared__ double r_pay[NT / 64][5];  // the wave winner's entry: g, Encode index, state
+  __shared__ int r_id[NT / 64];
   const size_t base = (size_t)b * Q.C;
   if (n_open == 0 || loop >= Q.mp) return false;
   const int lane = tid & 63, wave = tid >> 6;
@@ -975,18 +1004,18 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   double bf = __builtin_inf();
   long long bs = 0x7fffffffffffffffLL;
   int bp = -1;
-  for (int p0 = tid; p0 < n_open; p0 += 4 * BKT) {
+  for (int p0 = tid; p0 < n_open; p0 += 4 * NT) {
     double fv[4];
     long long sv[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int p = p0 + u * BKT;
+      const int p = p0 + u * NT;
       fv[u] = p < n_open ? Q.of[base + p] : 0.0;
       sv[u] = p < n_open ? Q.oseq[base + p] : 0;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int p = p0 + u * BKT;
+      const int p = p0 + u * NT;
       if (p < n_open && (bp < 0 || key_before(fv[u], sv[u], bf, bs))) { bf = fv[u]; bs = sv[u]; bp = p; }
     }
   }
@@ -1035,7 +1064,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   __syncthreads();
   if (tid >= 64) return true;
   int ww = 0;
-  for (int w = 1; w < BKT / 64; w++) {
+  for (int w = 1; w < NT / 64; w++) {
     const int op = r_p[w];
     if (op >= 0 && (bp < 0 || key_before(r_f[w], r_s[w], bf, bs))) { bf = r_f[w]; bs = r_s[w]; bp = op; ww = w; }
   }
@@ -1057,13 +1086,17 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   if (lane == 0) {
     Q.pos[base + id] = -1;
     Q.sc_i[SI_NOPEN * B + b] = last;
-    Q.sc_i[SI_LOOP * B + b] = loop + 1;
     Q.sc_i[SI_CUR * B + b] = id;
-    Q.pop_seq[(size_t)b * Q.mp + loop] = iw;
+    if (direct) {
+      Q.sc_i[SI_LOOP * B + b] = loop + 1;
+      Q.pop_seq[(size_t)b * Q.mp + loop] = iw;
+    } else {
+      *iw_out = iw;
+    }
     Q.cur_g[b] = gw;
     Q.cur_ix[b] = iw;
   }
-  if (lane < 3) Q.node[3 * b + lane] = stw;
+  if (lane < 3) node_out[3 * b + lane] = stw;
   return true;
 }
 
@@ -1097,7 +1130,7 @@ __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B
     if (si >= 0 && si < Q.C) Q.nid[base + si] = 0;
   }
   __syncthreads();
-  const bool go = ha_pop(Q, B, b, 1, 0, tid);
+  const bool go = ha_pop<256>(Q, B, b, 1, 0, tid, Q.node, true, nullptr);  // node buffer 0: iteration 1 reads it
   if (tid == 0) Q.sc_i[SI_ACTIVE * B + b] = go;
 }
 
@@ -1293,7 +1326,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   BTIME(6);
   const int n_open = s_nopen;
   // ---- next popfirst!
-  const bool go = ha_pop(Q, B, b, n_open, loop, tid);
+  const bool go = ha_pop<BKT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, true, nullptr);
   BTIME(7);
   if (tid == 0) {
     if (go) Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;
@@ -1309,6 +1342,266 @@ __global__ __launch_bounds__(BKT) void ha_book_kernel(HaDev P, HaSearch Q, IterA
   // (iteration 1: every scene, inactive ones return at once)
   if (A.n_live && (int)blockIdx.x >= *A.n_live) return;
   ha_book(P, Q, A, B, it, A.scene_of ? A.scene_of[blockIdx.x] : (int)blockIdx.x);
+}
+
+// ---------------------------------------------------------------- fused iteration (ha_step_kernel)
+// One launch per search iteration does the expansion AND the bookkeeping.  FindNewNode (:418-446) and
+// the next popfirst! need only the 62 neighbour records, not RS_connected's answer, so the last of a
+// scene's neighbour-group blocks to finish runs them at once, speculatively, beside the scene's
+// RS_connected block (the iteration's longest chain).  Whichever of the two arrives second at the
+// scene's final ticket finishes the iteration: RS_connected found a path -> the termination of
+// :259-271 (the speculative pop is undone: its pop count, node count and pop_seq entry are never
+// published, and the Dict changes of a finished scene are never read again; the parent chain it walks
+// cannot have changed: FindNewNode only re-parents nodes whose g exceeds the popped node's, and every
+// ancestor's g is below it); else the pop's results are published and the scene re-listed.  Records
+// cross blocks through agent-coherent stores (st_ag), each writer's stores acknowledged (s_waitcnt)
+// before its arrival ticket.
+
+// every store of this thread acknowledged at the device coherence point; also a compiler barrier
+__device__ __forceinline__ void ha_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+enum { RC_GO = 0, RC_LOOP, RC_NN0, RC_NNEW, RC_NOPEN, RC_CUR, RC_IW, RC_N = 8 };
+
+// FindNewNode + popfirst! for scene b on an NT-thread block (ha_book without its termination branch):
+// the neighbour records are read agent-coherently; the node count, the pop count and pop_seq go to the
+// scene's record (Q.rec) for the finisher instead of the scene's counters.
+template <int NT>
+__device__ __forceinline__ void ha_book_spec(const HaDev& P, const HaSearch& Q, const IterArgs& A, int B, int it, int b) {
+  __shared__ int s_nopen, s_nnew;
+  __shared__ long long s_vix[64];
+  __shared__ int s_dup[4][64];
+  static_assert(NT >= 256, "the duplicate check below runs on four waves");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const size_t base = (size_t)b * Q.C;
+  const int np = P.n_prim;
+  const int loop = Q.sc_i[SI_LOOP * B + b];
+  const int n_open0 = Q.sc_i[SI_NOPEN * B + b];
+  const int nn0 = Q.sc_i[SI_NNODES * B + b];
+  const int cur0 = Q.sc_i[SI_CUR * B + b];
+  const long long ctr = Q.ctr[b];
+  const double cur_g = Q.cur_g[b];
+  const long long cidx = Q.cur_ix[b];
+  long long ix = 0;
+  int frk = 0;
+  double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
+  if (tid < np) {
+    const size_t q = (size_t)b * np + tid;
+    ix = ld_ag(A.idx + q);
+    frk = ld_ag(A.fr + q);
+    hk = ld_ag(A.h + q);
+    nb0 = ld_ag(A.nb + 3 * q);
+    nb1 = ld_ag(A.nb + 3 * q + 1);
+    nb2 = ld_ag(A.nb + 3 * q + 2);
+  }
+  // duplicates: lane k of wave 0 is neighbour k; an earlier valid lane with the same Encode index makes
+  // it one (the comparisons split over four waves, as in ha_book)
+  const bool valid = tid < np && ix != 0 && frk;
+  if (tid < 64) s_vix[tid] = valid ? ix : 0;
+  __syncthreads();
+  if (tid < 256) {
+    const int w = tid >> 6;
+    const long long key = s_vix[lane];
+    bool d = false;
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) {
+      const int j = 16 * w + jj;
+      const long long oj = s_vix[j];
+      d = d | ((oj == key) & (j < lane) & (key != 0));
+    }
+    s_dup[w][lane] = d;
+  }
+  int hit = -1;
+  double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
+  int po = 0;
+  long long so0 = 0, io = 0;
+  if (valid) {
+    hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
+    if (hit >= 0) {
+      gd = Q.g[base + hit];
+      po = Q.pos[base + hit];
+      fo_ = Q.f[base + hit];
+      so0 = Q.seq[base + hit];
+      io = Q.index[base + hit];
+      dst0 = Q.st[(base + hit) * 3];
+      dst1 = Q.st[(base + hit) * 3 + 1];
+      dst2 = Q.st[(base + hit) * 3 + 2];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    int n_open = n_open0;
+    const int k = lane;
+    const bool dup = s_dup[0][k] | s_dup[1][k] | s_dup[2][k] | s_dup[3][k];
+    const bool first = valid && !dup;
+    const double tg = cur_g + P.expand_time;
+    double th = 0.0, tf = 0.0;
+    int id = -1;
+    bool chg = false, app = false, isnew = false;
+    double fo = 0.0;
+    long long so_ = 0;
+    double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;
+    long long nix = ix;
+    if (first) {
+      th = __builtin_fmax(hk, 0.0);
+      if (hk != hk) th = hk;
+      tf = tg + th;
+      if (hit >= 0) {
+        id = hit;
+        nst0 = dst0;
+        nst1 = dst1;
+        nst2 = dst2;
+        nix = io;
+        if (tg < gd) {
+          if (po >= 0) {
+            chg = true;
+            fo = fo_;
+            so_ = so0;
+          } else {
+            app = true;
+          }
+        }
+      } else {
+        isnew = true;
+        app = true;
+        nst0 = nb0;
+        nst1 = nb1;
+        nst2 = nb2;
+      }
+    }
+    const unsigned long long m_new = __ballot(isnew), m_chg = __ballot(chg), m_app = __ballot(app);
+    const unsigned long long below = (1ull << k) - 1;
+    const int n_new = __popcll(m_new), n_chg = __popcll(m_chg), n_app = __popcll(m_app);
+    if (isnew) id = nn0 + __popcll(m_new & below);
+    int r = 0;
+    for (unsigned long long m = m_chg; m; m &= m - 1) {
+      const int j = __builtin_ctzll(m);
+      const double fj = __shfl(fo, j);
+      const long long sj = __shfl(so_, j);
+      r += chg && key_before(fj, sj, fo, so_);
+    }
+    long long nseq = 0;
+    if (chg) nseq = ctr + r;
+    else if (app) nseq = ctr + n_chg + __popcll(m_app & below);
+    if (chg || app) {
+      const size_t q = base + id;
+      if (isnew) {
+        Q.st[q * 3] = nst0;
+        Q.st[q * 3 + 1] = nst1;
+        Q.st[q * 3 + 2] = nst2;
+        Q.index[q] = ix;
+        if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
+      }
+      Q.g[q] = tg;
+      Q.h[q] = th;
+      Q.f[q] = tf;
+      Q.parent[q] = cidx;
+      Q.seq[q] = nseq;
+      const int p = chg ? Q.pos[q] : n_open + __popcll(m_app & below);
+      Q.of[base + p] = tf;
+      Q.oseq[base + p] = nseq;
+      Q.og[base + p] = tg;
+      if (!chg) {
+        Q.oid[base + p] = id;
+        Q.oix[base + p] = nix;
+        Q.ost[(base + p) * 3] = nst0;
+        Q.ost[(base + p) * 3 + 1] = nst1;
+        Q.ost[(base + p) * 3 + 2] = nst2;
+        Q.pos[q] = p;
+      }
+    }
+    n_open += n_app;
+    if (lane == 0) {
+      Q.ctr[b] = ctr + n_chg + n_app;
+      s_nopen = n_open;
+      s_nnew = nn0 + n_new;
+    }
+  }
+  __syncthreads();  // the open-list writes of wave 0 before the block-wide scan
+  const int n_open = s_nopen;
+  long long iw = 0;
+  const bool go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, false, &iw);
+  if (tid == 0) {
+    long long* rc = Q.rec + (size_t)RC_N * b;
+    st_ag(rc + RC_GO, (long long)go);
+    st_ag(rc + RC_LOOP, (long long)loop);
+    st_ag(rc + RC_NN0, (long long)nn0);
+    st_ag(rc + RC_NNEW, (long long)s_nnew);
+    st_ag(rc + RC_NOPEN, (long long)n_open);
+    st_ag(rc + RC_CUR, (long long)cur0);
+    st_ag(rc + RC_IW, iw);
+  }
+}
+
+// the scene's iteration ends (one thread): the termination of :259-271 when RS_connected found a path,
+// else the speculative pop's results published and the scene listed for the next iteration
+__device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, int B, int it, int b) {
+  const long long* rc = Q.rec + (size_t)RC_N * b;
+  const int go = (int)ld_ag(rc + RC_GO), loop = (int)ld_ag(rc + RC_LOOP);
+  const int rs_ok = ld_ag(A.rs_ok + b);
+  if (rs_ok) {
+    const size_t base = (size_t)b * Q.C;
+    Q.sc_i[SI_FOUND * B + b] = 1;
+    Q.sc_i[SI_ACTIVE * B + b] = 0;
+    Q.sc_i[SI_RSLEN * B + b] = ld_ag(A.rs_len + b);
+    Q.sc_i[SI_LOOP * B + b] = loop;
+    Q.sc_i[SI_NNODES * B + b] = (int)ld_ag(rc + RC_NN0);
+    double* so = Q.states + (size_t)b * Q.mp * 3;
+    int c = (int)ld_ag(rc + RC_CUR), ns = 0;
+    for (int r = 0; r < 3; r++) so[r] = Q.st[(base + c) * 3 + r];
+    ns++;
+    while (Q.parent[base + c] >= 0 && Q.index[base + c] != Q.start_index[b] && ns < Q.mp) {
+      const long long pc = Q.parent[base + c];
+      c = (pc >= 0 && pc < Q.C) ? Q.nid[base + pc] : -1;
+      if (c < 0) break;
+      for (int r = 0; r < 3; r++) so[3 * ns + r] = Q.st[(base + c) * 3 + r];
+      ns++;
+    }
+    Q.sc_i[SI_NSTATES * B + b] = ns;
+    return;
+  }
+  Q.sc_i[SI_NNODES * B + b] = (int)ld_ag(rc + RC_NNEW);
+  if (go) {
+    Q.sc_i[SI_LOOP * B + b] = loop + 1;
+    Q.pop_seq[(size_t)b * Q.mp + loop] = ld_ag(rc + RC_IW);
+    Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;
+  } else {
+    Q.sc_i[SI_ACTIVE * B + b] = 0;
+    Q.sc_i[SI_NOPEN * B + b] = (int)ld_ag(rc + RC_NOPEN);
+  }
+}
+
+template <int HWt, int NBGt>
+__global__ __launch_bounds__(64 * HWt) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
+  __shared__ int role;
+  if (!ha_iter_body<HWt, NBGt>(P, A)) return;  // block-uniform: no work for this block (not counted)
+  const int per = 1 + (P.n_prim + NBGt - 1) / NBGt;
+  const int slot = blockIdx.x / per, item = blockIdx.x % per;
+  const int s = A.scene_of ? A.scene_of[slot] : slot;
+  ha_stores_done();  // this thread's records acknowledged before the block's ticket
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int r = 2;  // RS_connected: straight to the final ticket
+    if (item > 0) {
+      const int t = __hip_atomic_fetch_add(Q.tk + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      r = t == per - 2 ? 1 : 0;  // the last of the per - 1 neighbour groups does the bookkeeping
+      if (r) st_ag(Q.tk + s, 0);
+    }
+    role = r;
+  }
+  __syncthreads();
+  const int r = role;
+  if (r == 0) return;
+  if (r == 1) {
+    ha_book_spec<64 * HWt>(P, Q, A, B, it, s);
+    ha_stores_done();
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(Q.tk + B + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+    asm volatile("" ::: "memory");
+    st_ag(Q.tk + B + s, 0);
+    ha_finish(Q, A, B, it, s);
+  }
 }
 
 
@@ -1664,8 +1957,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   const size_t C = (size_t)ncell + 1, nB = (size_t)B;
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24;
-  char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 24 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 2 * nB + 256 * 32);
+  char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + 256 * 36);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -1694,9 +1987,11 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.start_index = (long long*)take(nB * 8);
   Q.pop_seq = (long long*)take(nB * mp * 8);
   Q.states = (double*)take(nB * mp * 24);
-  Q.node = (double*)take(nB * 24);
+  Q.node = (double*)take(nB * 48);
   Q.live = (int*)take(sizeof(int) * (mp + 2));
   Q.lst = (int*)take(sizeof(int) * 2 * nB);
+  Q.tk = (int*)take(sizeof(int) * 2 * nB);
+  Q.rec = (long long*)take(nB * RC_N * 8);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
@@ -1716,7 +2011,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                        A.walls, wt);
     A.wtab = wt;
   }
-  A.node = Q.node;
+  // MPGPU_HA_SPLIT=1: the round-3 shape (ha_iter_kernel + ha_book_kernel per iteration), for A/B runs
+  static const bool split = getenv("MPGPU_HA_SPLIT") && atoi(getenv("MPGPU_HA_SPLIT")) == 1;
+  A.coherent = split ? 0 : 1;
   A.scene_of = nullptr;  // slot = scene
   A.active = Q.sc_i + SI_ACTIVE * B;
   A.sc = ctx->ha_states_candi;
@@ -1727,16 +2024,17 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.n_active = B;
   MP_HIP(ctx, hipMemsetAsync(Q.pop_seq, 0xff, nB * mp * 8, ctx->stream));  // -1 past each scene's pops
   MP_HIP(ctx, hipMemsetAsync(Q.live, 0, sizeof(int) * (mp + 2), ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.tk, 0, sizeof(int) * 2 * nB, ctx->stream));  // the finishers reset them
   hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
   MP_HIP(ctx, hipGetLastError());
-  // The whole search loop is enqueued without host round trips: iteration i = ha_iter_kernel
-  // (RS_connected + 62 neighbours of every live scene) then ha_book_kernel (bookkeeping + the
-  // next pop).  live[i] (scenes still searching after iteration i) is copied back once per
-  // chunk of CH iterations; the host stays at most two chunks ahead of the device and stops
-  // enqueueing when a copied count is 0 (at most every scene's max_pops iterations).
-  // (Fusing the bookkeeping into the expansion launch -- the last of a scene's 5 blocks doing it
-  // after an arrival ticket -- measured 67-90 ms vs 40 ms per 256-scenario plan: every one of
-  // the 1,280 blocks then needs an agent-scope release, an L2 write-back.)
+  // The whole search loop is enqueued without host round trips: iteration i = one ha_step_kernel
+  // (RS_connected + 62 neighbours of every live scene, the bookkeeping + the next pop by the scene's
+  // last neighbour-group block, beside RS_connected; the finisher publishes or undoes).  live[i] (scenes
+  // still searching after iteration i) is copied back once per chunk of CH iterations; the host stays
+  // at most two chunks ahead of the device and stops enqueueing when a copied count is 0 (at most
+  // every scene's max_pops iterations).  (Round 1 fused the bookkeeping behind an agent-scope release
+  // in every block -- an L2 write-back each -- and measured 67-90 ms vs 40 ms; ha_step_kernel hands
+  // its records over with agent-coherent stores instead, so no block writes back its L2.)
   constexpr int CH = 16, NCK = 4;
   int* hl = (int*)mp_pinned(ctx, sizeof(int) * NCK);
   if (!hl) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
@@ -1759,12 +2057,22 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     A.scene_of = it == 1 ? nullptr : Q.lst + ((it - 1) & 1) * B;
     A.n_live = it == 1 ? nullptr : Q.live + (it - 1);
     A.n_active = known;
-    if (known * per_tail <= tail_blocks)
-      hipLaunchKernelGGL((ha_iter_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)), dim3(64 * HW_TAIL), 0,
-                         ctx->stream, D, A);
-    else
-      hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
-    hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
+    A.node = Q.node + (size_t)((it - 1) & 1) * 3 * B;  // the previous iteration's pops
+    const bool tail = known * per_tail <= tail_blocks;
+    if (split) {
+      if (tail)
+        hipLaunchKernelGGL((ha_iter_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)), dim3(64 * HW_TAIL),
+                           0, ctx->stream, D, A);
+      else
+        hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
+      hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
+    } else if (tail) {
+      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)), dim3(64 * HW_TAIL), 0,
+                         ctx->stream, D, Q, A, B, it);
+    } else {
+      hipLaunchKernelGGL((ha_step_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, Q, A, B,
+                         it);
+    }
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
     if (it % CH == 0 || it == mp) {
       const int slot = chunk % NCK;

@@ -29,6 +29,8 @@ python3 tools/pmc_traffic.py $O 8 8192 50 > $O/traffic.json &&
 python3 tools/pmc_roofline.py $O > $O/roofline.json &&
 timeout -k 10 400 python bench.py --steps 50 --warmup 5 --cpu-seconds 10 --traffic $O/traffic.json --roofline $O/roofline.json > $O/bench.log 2>&1
 rc=$?
+# raw per-dispatch CSVs (tens of MB) compressed: gpurun copies back at most 64 MiB
+find $O -name 'run_counter_collection.csv' -o -name 'run_kernel_trace.csv' | xargs -r gzip -f
 echo "chain exit $rc"; tail -c 3000 $O/bench.log
 [ $rc -ne 0 ] && exit $rc
 # N>1 rehearsal of the driver's launch (bench.py --gpus 2 spawns two ranks; both on cuda:0, gloo)
