@@ -1,11 +1,11 @@
 #!/bin/bash
-# Hybrid A* A/B: the fused ha_step_kernel (default) vs the split iter + book launches (MPGPU_HA_SPLIT=1),
-# alternating, each a fresh process of tools/ha_plan_time.py (256 scenarios, 5 plans).
+# A/B of Hybrid A* builds: configs[3] plan time (tools/ha_plan_time.py) per libmpgpu variant.
+# usage: bash tools/ha_ab.sh TAG lib-suffix...   ("" = libmpgpu.so)
 set -o pipefail
-O=gpurun_out/${1:-ha_ab}
-mkdir -p $O
-for r in 1 2; do
-  timeout -k 10 120 python3 tools/ha_plan_time.py > $O/fused_$r.log 2>&1 || exit $?
-  MPGPU_HA_SPLIT=1 timeout -k 10 120 python3 tools/ha_plan_time.py > $O/split_$r.log 2>&1 || exit $?
+TAG=$1; shift
+D=gpurun_out/$TAG; mkdir -p $D
+for v in "$@"; do
+  echo "== lib$v" >> $D/ha.log
+  MPGPU_LIB=$PWD/motionplanning_amd/lib/libmpgpu$v.so timeout -k 10 120 python3 tools/ha_plan_time.py >> $D/ha.log 2>&1 || exit 1
 done
-for f in $O/*.log; do echo "== $f"; cat $f; done
+cat $D/ha.log
