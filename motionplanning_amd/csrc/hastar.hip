@@ -402,6 +402,12 @@ struct IterArgs {
                           // reads it only then); the standalone entry point writes every path
   int coherent;           // ha_step_kernel: the per-scene outputs the same launch's bookkeeping reads
                           // (neighbour records, rs_ok / rs_len) are stored agent-coherent (st_ag)
+  // the search's Dict (mp_ha_plan; nullptr elsewhere): a neighbour group skips rs_heuristic when no
+  // neighbour of it can use the value (its Encode cell already holds a node with g <= the tentative g)
+  const int* dnid;        // [B][C] cell -> node id (-1 absent)
+  const double* dg;       // [B][C] node g
+  const double* cur_g;    // [B] the popped node's g
+  int C;
   // RS_connected outputs (per scene)
   unsigned char* rs_ok;  // [B]
   double* rs_path;       // [B][501][3]
@@ -555,6 +561,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   __shared__ double g_nb[NBG][3];
   __shared__ long long g_ix[NBG];
   __shared__ int g_free[NBG];
+  __shared__ int g_need[NBG];
   __shared__ int sh_n;
   const int per = 1 + (P.n_prim + NBG - 1) / NBG;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
@@ -597,12 +604,14 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     }
   }
   if (tid < NBG) g_free[tid] = 1;
+  int hit = -1;  // (groups with a Dict) the neighbour's node id in the scene's Dict
   if (tid < nk) {  // transform + regulate_states + Encode of the group's neighbours (:396-405)
     const int k = k0 + tid;
     double t[3], nb[3];
     transform1(node, A.sc + 3 * k, t);
     regulate(P, t, nb);
     const long long ix = encode(P, nb);
+    if (!rs && A.dnid) hit = ix > 0 && ix < A.C ? A.dnid[(size_t)s * A.C + ix] : -1;
     st_out(A.coherent, R.nb + 3 * k, nb[0]);
     st_out(A.coherent, R.nb + 3 * k + 1, nb[1]);
     st_out(A.coherent, R.nb + 3 * k + 2, nb[2]);
@@ -756,13 +765,20 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     HTIME(5);
   } else {
     // dg_cost first (primitive poses 1:5:n_col): rs_heuristic is only used for neighbours that
-    // are collision-free and in bounds, so a group without one skips the 48 RS candidates
+    // are collision-free and in bounds, so a group without one skips the 48 RS candidates.
+    // FindNewNode (:418-446) also leaves a neighbour alone whose cell already holds a node with
+    // g <= tg = g(popped) + expand_time (the same tg for every neighbour): its heuristic is never read.
+    // The Dict at this launch is the one this iteration's FindNewNode starts from (the bookkeeping
+    // that changes it runs after every neighbour group of the scene, ha_step_kernel / ha_book_kernel).
+    double gd = 0.0;
+    if (hit >= 0) gd = A.dg[(size_t)s * A.C + hit];  // loaded now, used after the sweep
     sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
     HTIME(4);
+    if (tid < nk) g_need[tid] = !A.dnid || !(hit >= 0 && !(A.cur_g[s] + P.expand_time < gd));
     __syncthreads();
     HTIME(5);
     int any = 0;
-    for (int q = 0; q < nk; q++) any |= (g_ix[q] != 0) & g_free[q];
+    for (int q = 0; q < nk; q++) any |= (g_ix[q] != 0) & g_free[q] & g_need[q];
     if (any) {  // block-uniform
       double ns[3];
       change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
@@ -2014,6 +2030,12 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // MPGPU_HA_SPLIT=1: the round-3 shape (ha_iter_kernel + ha_book_kernel per iteration), for A/B runs
   static const bool split = getenv("MPGPU_HA_SPLIT") && atoi(getenv("MPGPU_HA_SPLIT")) == 1;
   A.coherent = split ? 0 : 1;
+  // MPGPU_HA_NOSKIP=1: every neighbour group evaluates rs_heuristic (A/B of the Dict pre-check)
+  static const bool noskip = getenv("MPGPU_HA_NOSKIP") && atoi(getenv("MPGPU_HA_NOSKIP")) == 1;
+  A.dnid = noskip ? nullptr : Q.nid;
+  A.dg = Q.g;
+  A.cur_g = Q.cur_g;
+  A.C = (int)C;
   A.scene_of = nullptr;  // slot = scene
   A.active = Q.sc_i + SI_ACTIVE * B;
   A.sc = ctx->ha_states_candi;
