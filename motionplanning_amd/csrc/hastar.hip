@@ -2071,7 +2071,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
 #ifndef HA_TAIL_BLOCKS
 #define HA_TAIL_BLOCKS 512
 #endif
-  const int tail_blocks = HA_TAIL_BLOCKS;
+  // (A/B) MPGPU_HA_TAIL_BLOCKS overrides the tail threshold; MPGPU_HA_MID_BLOCKS > 0 adds a middle shape
+  // (12-wave blocks, 16 neighbours each: 5 blocks per scene) once known * 5 fits in that many blocks
+  const int tail_blocks = getenv("MPGPU_HA_TAIL_BLOCKS") ? atoi(getenv("MPGPU_HA_TAIL_BLOCKS")) : HA_TAIL_BLOCKS;
+  const int mid_blocks = getenv("MPGPU_HA_MID_BLOCKS") ? atoi(getenv("MPGPU_HA_MID_BLOCKS")) : 0;
   int known = B;
   int chunk = 0, checked = 0;
   bool finished = false;
@@ -2090,6 +2093,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     } else if (tail) {
       hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)), dim3(64 * HW_TAIL), 0,
+                         ctx->stream, D, Q, A, B, it);
+    } else if (known * per <= mid_blocks) {
+      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG>), dim3((unsigned)(known * per)), dim3(64 * HW_TAIL), 0,
                          ctx->stream, D, Q, A, B, it);
     } else {
       hipLaunchKernelGGL((ha_step_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, Q, A, B,
