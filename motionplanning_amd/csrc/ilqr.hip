@@ -338,9 +338,10 @@ __device__ __forceinline__ double cst(int variant, const double* s, const SigCac
 template <bool F>
 __device__ __forceinline__ void knot_cost_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
                                                  size_t stride, int& bad);
+// the dynamics Jacobians of knot_derivs (LocallyLinearizeDynamics, GetMatrix.jl:70-91): A, B
 template <bool F>
-__device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
-                                            size_t stride, int& bad) {
+__device__ __forceinline__ void knot_dyn_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
+                                                size_t stride, int& bad) {
   const double e = P.eps;
 #define DOUT(q) out[(size_t)(q) * stride]
   // ---- dynamics Jacobians: A (row-major 4x4) at 0, B (4x2) at 16
@@ -379,8 +380,13 @@ __device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, c
 #pragma unroll
     for (int r = 0; r < 4; r++) DOUT(16 + 2 * r + 1) = (fp[r] - fm[r]) / (2 * e);
   }
-  knot_cost_derivs<F>(P, s, u, out, stride, bad);
 #undef DOUT
+}
+template <bool F>
+__device__ __forceinline__ void knot_derivs(const IlqrDev& P, const double* s, const double* u, double* out,
+                                            size_t stride, int& bad) {
+  knot_dyn_derivs<F>(P, s, u, out, stride, bad);
+  knot_cost_derivs<F>(P, s, u, out, stride, bad);
 }
 
 // the cost derivatives of knot_derivs (GetMatrix.jl CalculateMatrix): lx 24, lu 28, lxx 30, luu 46, lux 50
@@ -1020,9 +1026,20 @@ __device__ __forceinline__ void qgather(double v, double* out) {  // out[k] = la
 // are evaluated on all four lanes (the pinv is the chain every lane waits on anyway).  Quad
 // broadcasts (DPP) assemble T24, KK, Vx and Vxx where a full copy is needed.  The lone wave issues
 // ~40 % of the one-lane sweep's instructions per knot, leaving the pinv chain as the bound.
-template <int IPB>
+// The staged sweep's record source: knot t's records sit in LDS buffer t & 1, handed over by the
+// loader wave at one s_barrier per knot.
+struct QuadFetchStaged {
+  const double* lds;
+  __device__ __forceinline__ const double* at(int t, int IPB) const {
+    lds_barrier();  // knot j's records staged by the loader wave before barrier t
+    return lds + (size_t)(t & 1) * ND * IPB;
+  }
+  __device__ __forceinline__ void done(int) const {}
+};
+
+template <int IPB, class Fetch = QuadFetchStaged>
 __device__ __forceinline__ void backward_sweep_quad(const IlqrDev& P, int b, bool live, const double* X,
-                                                    double* kout, double* Kout, const double* lds, int inst, int q) {
+                                                    double* kout, double* Kout, const Fetch& src, int inst, int q) {
   const int N = P.N;
   const double e = P.eps;
   const int V = P.variant;
@@ -1060,8 +1077,7 @@ __device__ __forceinline__ void backward_sweep_quad(const IlqrDev& P, int b, boo
       }
   }
   for (int j = N - 2, t = 0; j >= 0; j--, t++) {
-    lds_barrier();  // knot j's records staged by the loader wave before barrier t
-    const double* bf = lds + (size_t)(t & 1) * ND * IPB + inst;
+    const double* bf = src.at(t, IPB) + inst;
     // no run-time index into a register array (q is per lane): column q of A comes from LDS, column
     // q of Vxx from the selects below
     double A[16], Bm[8], Acol[4], Vcol[4];
@@ -1186,6 +1202,7 @@ __device__ __forceinline__ void backward_sweep_quad(const IlqrDev& P, int b, boo
 #pragma unroll
       for (int k = 0; k < 4; k++) Vxx[4 * k + c] = col[k];
     }
+    src.done(t);
   }
 }
 
@@ -1261,7 +1278,135 @@ __global__ __launch_bounds__(128) void ilqr_backward_quad_kernel(IlqrDev P, int 
   const bool live = i0 < n;
   const int i = live ? i0 : n - 1;  // dead quads recompute the last column and store nothing
   const int b = list ? list[i] : i;
-  backward_sweep_quad<kQuadIPB>(P, b, live, X, kout, Kout, recs, live ? inst : (n - 1 - col0), q);
+  backward_sweep_quad<kQuadIPB>(P, b, live, X, kout, Kout, QuadFetchStaged{recs}, live ? inst : (n - 1 - col0), q);
+}
+
+// ---------------------------------------------------------------- fused derivatives + Riccati sweep
+// ilqr_backward_quad_kernel's compute wave (16 instances on lane quads) with the derivative records
+// computed in the same block instead of read from HBM: kFusedDW derivative waves evaluate
+// LocallyLinearizeDynamics / CalculateMatrix (GetMatrix.jl:3-91) of the block's instances for the knots
+// in sweep order (N-2 first) and write them into an LDS ring that the sweep consumes.  A derivative
+// wave takes one part of knot_derivs_part (a wave-uniform role, as ilqr_deriv4_kernel) for a group of
+// kFusedGK knots x 16 instances (64 lanes); two waves per part alternate groups.  Per ring slot a
+// cumulative count of parts written (kFusedParts per group) and one count of groups the sweep has finished are the
+// only synchronisation (LDS, polled with s_sleep; every wave of the block is resident).  The records are
+// the same operations on the same operands as the two-kernel path, so the gains are the same bits; the
+// 464 B per knot record round trip through HBM and the separate derivative launch are gone, and the
+// derivative work runs on the SIMDs the sweep leaves idle (one compute wave per CU).
+#ifndef ILQR_FUSED_DW
+#define ILQR_FUSED_DW 7
+#endif
+// derivative waves per block: at most 7, so no SIMD holds more than two of the block's waves and the
+// sweep keeps the ~230 VGPRs it needs (9 waves cap every wave at 168: the sweep spilled 240 B per lane).
+// One wave per part (4) could not keep up with the sweep: 0.292 ms per backward pass vs 0.264 ms for
+// the two-kernel path (profiles/r04_ilqr_fused_ab.txt).
+constexpr int kFusedDW = ILQR_FUSED_DW;
+#ifndef ILQR_FUSED_PARTS
+#define ILQR_FUSED_PARTS 2
+#endif
+// wave-uniform parts per record: 2 = the Jacobians (9 RK4 sharing stage sincos) / the cost
+// derivatives; 4 = knot_derivs_part (three Jacobian parts without the sharing + the costs)
+constexpr int kFusedParts = ILQR_FUSED_PARTS;
+static_assert(kFusedParts == 2 || kFusedParts == 4, "2 or 4 parts");
+static_assert(kFusedDW >= 1 && kFusedDW <= 7, "at most two waves per SIMD");
+constexpr int kFusedGK = 4;  // knots per group: 4 knots x 16 instances = 64 lanes
+#ifndef ILQR_FUSED_RG
+#define ILQR_FUSED_RG 4
+#endif
+constexpr int kFusedRG = ILQR_FUSED_RG;  // ring slots (groups); LDS = RG x GK x ND x 16 x 8 B
+constexpr size_t kFusedLds = sizeof(double) * kFusedRG * kFusedGK * ND * kQuadIPB;
+
+__device__ __forceinline__ int lds_ld(const int* p) {
+  return __hip_atomic_load(const_cast<int*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct QuadFetchRing {
+  const double* ring;
+  const int* ready;  // [RG] cumulative parts written into the slot
+  int* consumed;     // groups the sweep has finished with
+  int NK;
+  __device__ __forceinline__ const double* at(int t, int IPB) const {
+    const int g = t / kFusedGK, kk = t - g * kFusedGK, slot = g % kFusedRG;
+    if (kk == 0) {  // wave-uniform: the group's four parts written
+      const int want = kFusedParts * (g / kFusedRG + 1);
+      while (lds_ld(ready + slot) < want) __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    return ring + ((size_t)slot * kFusedGK + kk) * ND * IPB;
+  }
+  __device__ __forceinline__ void done(int t) const {
+    const int g = t / kFusedGK, kk = t - g * kFusedGK;
+    if (kk == kFusedGK - 1 || t == NK - 1) {  // the group's records read (LDS reads retired) -> slot free
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store(consumed, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+};
+
+__global__ __launch_bounds__(64 * (1 + kFusedDW)) void ilqr_backward_fused_kernel(
+    IlqrDev P, int B, const double* X, const double* U, const int* list, const int* n_dev, int nmax, double* kout,
+    double* Kout) {
+  extern __shared__ double ring[];  // [RG][GK][ND][IPB]
+  __shared__ int ready[kFusedRG];
+  __shared__ int consumed;
+  const int tid = threadIdx.x;
+  const int n = n_dev ? *n_dev : nmax;
+  const int col0 = blockIdx.x * kQuadIPB;
+  if (col0 >= n) return;  // block-uniform: the grid covers nmax >= n
+  if (tid < kFusedRG) ready[tid] = 0;
+  if (tid == 0) consumed = 0;
+  __syncthreads();  // the last block-wide barrier: the roles below synchronise through LDS counts only
+  const int N = P.N, NK = N - 1, NG = (NK + kFusedGK - 1) / kFusedGK;
+  if (tid >= 64) {
+    // derivative wave w: tasks w, w + DW, w + 2 DW, ... of the sequence (group g, part p) = (t / 4, t % 4),
+    // in order.  No deadlock: the sweep waits for the least unfinished group g0, every task of a group
+    // <= g0 + RG - 1 runs without waiting for a slot, and a wave reaches its task of g0 after finishing
+    // only tasks of earlier groups.  (A shared task counter -- one lane's LDS atomic broadcast to the
+    // wave -- was miscompiled into a loop that reran a task without fetching the next: the kernel hung.)
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6) - 1, lane = tid & 63;
+    const int kk = lane / kQuadIPB, ci = lane % kQuadIPB;
+    const int ncol = n - col0;
+    const int col = col0 + (ci < ncol ? ci : ncol - 1);  // columns past the list end repeat the last one
+    const int b = list ? list[col] : col;
+    for (int task = w; task < kFusedParts * NG; task += kFusedDW) {
+      const int g = task / kFusedParts, part = task - g * kFusedParts;
+      const int slot = g % kFusedRG;
+      if (g >= kFusedRG) {  // the slot's previous group consumed by the sweep
+        while (lds_ld(&consumed) < g - kFusedRG + 1) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
+      const int jj = g * kFusedGK + kk;
+      const int j = jj < NK ? NK - 1 - jj : 0;  // past the last knot: knot 0 again, written where no one reads
+      const double* xs = X + ((size_t)b * N + j) * 4;
+      const double* us = U + ((size_t)b * N + j) * 2;
+      const double sv[4] = {xs[0], xs[1], xs[2], xs[3]};
+      const double uv[2] = {us[0], us[1]};
+      double* out = ring + ((size_t)slot * kFusedGK + kk) * ND * kQuadIPB + ci;
+      if (kFusedParts == 2) {  // the Jacobians (shared stage sincos, knot_dyn_derivs) / the cost derivatives
+        int bad = 0;
+        if (part == 0) knot_dyn_derivs<false>(P, sv, uv, out, kQuadIPB, bad);
+        else knot_cost_derivs<false>(P, sv, uv, out, kQuadIPB, bad);
+      } else {
+        if (part == 0) knot_derivs_part<0>(P, sv, uv, out, kQuadIPB);
+        else if (part == 1) knot_derivs_part<1>(P, sv, uv, out, kQuadIPB);
+        else if (part == 2) knot_derivs_part<2>(P, sv, uv, out, kQuadIPB);
+        else knot_derivs_part<3>(P, sv, uv, out, kQuadIPB);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's record writes retired
+      if (lane == 0) __hip_atomic_fetch_add(ready + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return;
+  }
+  // the sweep: issue priority above the derivative waves sharing its SIMD (its chain sets the pace)
+  __builtin_amdgcn_s_setprio(3);
+  const int inst = tid >> 2, q = tid & 3;
+  const int i0 = col0 + inst;
+  const bool live = i0 < n;
+  const int i = live ? i0 : n - 1;
+  const int b = list ? list[i] : i;
+  backward_sweep_quad<kQuadIPB>(P, b, live, X, kout, Kout, QuadFetchRing{ring, ready, &consumed, NK},
+                                live ? inst : (n - 1 - col0), q);
 }
 
 // Compute lanes per instance.  Round 2 ran two (the whole sweep on both, the closed-form pinv's
@@ -2024,6 +2169,29 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
   na = B;
 #endif
   const size_t n = (size_t)na * (D.N - 1);
+#if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR) && !defined(MP_ILQR_STAGED)
+  // derivatives + sweep in one launch (ilqr_backward_fused_kernel) while more than kDeriv4Max instances
+  // are active; MPGPU_ILQR_FUSED=0: always the two-kernel path, =2: always fused.  A fused block makes
+  // the records of its 16 instances on its own CU, so with few blocks (the solve's tail) the derivative
+  // work, spread over the whole chip by ilqr_deriv4_kernel, is confined to a few CUs: measured 252 us per
+  // fused launch over a whole solve vs 32 + 180 us split, and 210 vs 108 + 180 us at full activity
+  // (profiles/r04_ilqr_fused_ab.txt)
+  static const int fused_mode = getenv("MPGPU_ILQR_FUSED") ? atoi(getenv("MPGPU_ILQR_FUSED")) : 1;
+  if (fused_mode == 2 || (fused_mode == 1 && na > kDeriv4Max)) {
+    if (!ctx->ilqr_fused_attr) {
+      MP_HIP(ctx, hipSetDevice(ctx->device));
+      MP_HIP(ctx, hipFuncSetAttribute((const void*)ilqr_backward_fused_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLds));
+      ctx->ilqr_fused_attr = true;
+    }
+    mp_time_begin(ctx);
+    hipLaunchKernelGGL(ilqr_backward_fused_kernel, dim3((na + kQuadIPB - 1) / kQuadIPB), dim3(64 * (1 + kFusedDW)),
+                       kFusedLds, ctx->stream, D, B, dX, dU, list, n_dev, na, dk, dK);
+    MP_HIP(ctx, hipGetLastError());
+    mp_time_end(ctx);
+    return MP_OK;
+  }
+#endif
   double* dD = (double*)mp_ws(ctx, WS_ILQR0, sizeof(double) * (size_t)B * (D.N - 1) * ND);  // knot stride ND*B
   if (!dD) return MP_ERR_NOMEM;
   mp_time_begin(ctx);  // the timed region covers both kernels of the backward pass

@@ -49,6 +49,7 @@ struct mp_ctx {
   // kernel attributes (150 KiB dynamic LDS) are per device: set once per context, on its device
   // (a context is used by one thread at a time, so the flags need no lock)
   bool mppi_lds_attr = false, fin_lds_attr = false;
+  bool ilqr_fused_attr = false;  // the fused iLQR backward kernel's dynamic-LDS attribute is set
   // multi-GPU in one process (mp_comm_init): the group and this context's rank in it
   mp_comm_group* comm = nullptr;
   int comm_rank = -1;
