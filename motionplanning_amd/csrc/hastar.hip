@@ -408,6 +408,19 @@ struct IterArgs {
   const double* dg;       // [B][C] node g
   const double* cur_g;    // [B] the popped node's g
   int C;
+  // ha_step_kernel: the neighbour groups also read the rest of each neighbour's Dict entry (pos, f, seq,
+  // Encode index, state: the loads overlap the collision sweep) into pre[B][n_prim][PRE_N], so the
+  // scene's bookkeeping starts from records instead of two levels of dependent Dict loads
+  const int* dpos;
+  const double* df;
+  const long long* dseq;
+  const long long* dindex;
+  const double* dst;
+  long long* pre;
+  // MPGPU_HA_STAMPS=1 (diagnostics): s_memrealtime stamps of every block of every STAMP_EVERY-th
+  // iteration, [slot][block][6]: entry, body done, role decided, bookkeeping done, finish done, role
+  unsigned long long* stamps;
+  int stamp_blocks;
   // RS_connected outputs (per scene)
   unsigned char* rs_ok;  // [B]
   double* rs_path;       // [B][501][3]
@@ -418,6 +431,8 @@ struct IterArgs {
   unsigned char* fr;     // [B][n_prim]
   double* h;             // [B][n_prim]
 };
+
+enum { PRE_HIT = 0, PRE_G, PRE_POS, PRE_F, PRE_SEQ, PRE_IDX, PRE_ST, PRE_N = PRE_ST + 3 };
 
 // Agent-coherent relaxed stores / loads (global_store / global_load with the sc1 policy: they reach
 // and read the device coherence point, past the per-XCD L2).  ha_step_kernel hands per-scene records
@@ -771,10 +786,32 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     // The Dict at this launch is the one this iteration's FindNewNode starts from (the bookkeeping
     // that changes it runs after every neighbour group of the scene, ha_step_kernel / ha_book_kernel).
     double gd = 0.0;
-    if (hit >= 0) gd = A.dg[(size_t)s * A.C + hit];  // loaded now, used after the sweep
+    long long pv[PRE_N - 2];  // pos, f, seq, index, state of the Dict entry (A.pre)
+    if (hit >= 0) {  // loaded now, used after the sweep
+      const size_t q = (size_t)s * A.C + hit;
+      gd = A.dg[q];
+      if (A.pre) {
+        pv[0] = A.dpos[q];
+        pv[1] = __double_as_longlong(A.df[q]);
+        pv[2] = A.dseq[q];
+        pv[3] = A.dindex[q];
+        pv[4] = __double_as_longlong(A.dst[3 * q]);
+        pv[5] = __double_as_longlong(A.dst[3 * q + 1]);
+        pv[6] = __double_as_longlong(A.dst[3 * q + 2]);
+      }
+    }
     sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
     HTIME(4);
     if (tid < nk) g_need[tid] = !A.dnid || !(hit >= 0 && !(A.cur_g[s] + P.expand_time < gd));
+    if (A.pre && tid < nk) {
+      long long* pr = A.pre + ((size_t)s * P.n_prim + k0 + tid) * PRE_N;
+      st_ag(pr + PRE_HIT, (long long)hit);
+      if (hit >= 0) {
+        st_ag(pr + PRE_G, __double_as_longlong(gd));
+#pragma unroll
+        for (int i = 0; i < PRE_N - 2; i++) st_ag(pr + PRE_POS + i, pv[i]);
+      }
+    }
     __syncthreads();
     HTIME(5);
     int any = 0;
@@ -1020,6 +1057,8 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   double bf = __builtin_inf();
   long long bs = 0x7fffffffffffffffLL;
   int bp = -1;
+  int pid = 0;
+  double pg = 0.0, pix = 0.0, p0s = 0.0, p1s = 0.0, p2s = 0.0;
   for (int p0 = tid; p0 < n_open; p0 += 4 * NT) {
     double fv[4];
     long long sv[4];
@@ -1037,8 +1076,6 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   }
   // the thread's own best entry's payload, loaded now so that its latency hides behind the reductions
   // (no dependent load after the winner is known)
-  int pid = 0;
-  double pg = 0.0, pix = 0.0, p0s = 0.0, p1s = 0.0, p2s = 0.0;
   if (bp >= 0) {
     pid = Q.oid[base + bp];
     pg = Q.og[base + bp];
@@ -1377,12 +1414,21 @@ __global__ __launch_bounds__(BKT) void ha_book_kernel(HaDev P, HaSearch Q, IterA
 __device__ __forceinline__ void ha_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 enum { RC_GO = 0, RC_LOOP, RC_NN0, RC_NNEW, RC_NOPEN, RC_CUR, RC_IW, RC_N = 8 };
+#ifndef HA_FIN_SHORTCUT
+#define HA_FIN_SHORTCUT 1  // the bookkeeping block arriving second finishes with its own values
+#endif
+// the bookkeeping's results for the scene's finisher (valid in thread 0)
+struct BookRec {
+  long long v[RC_N];
+};
 
 // FindNewNode + popfirst! for scene b on an NT-thread block (ha_book without its termination branch):
 // the neighbour records are read agent-coherently; the node count, the pop count and pop_seq go to the
 // scene's record (Q.rec) for the finisher instead of the scene's counters.
 template <int NT>
-__device__ __forceinline__ void ha_book_spec(const HaDev& P, const HaSearch& Q, const IterArgs& A, int B, int it, int b) {
+__device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& Q, const IterArgs& A, int B, int it,
+                                                int b, unsigned long long* stp = nullptr) {
+#define BSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
   __shared__ int s_nopen, s_nnew;
   __shared__ long long s_vix[64];
   __shared__ int s_dup[4][64];
@@ -1430,7 +1476,20 @@ __device__ __forceinline__ void ha_book_spec(const HaDev& P, const HaSearch& Q, 
   double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
   int po = 0;
   long long so0 = 0, io = 0;
-  if (valid) {
+  if (valid && A.pre) {  // the neighbour group read the Dict entry (same Dict: nothing changed it since)
+    const long long* pr = A.pre + ((size_t)b * np + tid) * PRE_N;
+    hit = (int)ld_ag(pr + PRE_HIT);
+    if (hit >= 0) {
+      gd = __longlong_as_double(ld_ag(pr + PRE_G));
+      po = (int)ld_ag(pr + PRE_POS);
+      fo_ = __longlong_as_double(ld_ag(pr + PRE_F));
+      so0 = ld_ag(pr + PRE_SEQ);
+      io = ld_ag(pr + PRE_IDX);
+      dst0 = __longlong_as_double(ld_ag(pr + PRE_ST));
+      dst1 = __longlong_as_double(ld_ag(pr + PRE_ST + 1));
+      dst2 = __longlong_as_double(ld_ag(pr + PRE_ST + 2));
+    }
+  } else if (valid) {
     hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
     if (hit >= 0) {
       gd = Q.g[base + hit];
@@ -1444,6 +1503,7 @@ __device__ __forceinline__ void ha_book_spec(const HaDev& P, const HaSearch& Q, 
     }
   }
   __syncthreads();
+  BSTAMP(6);
   if (tid < 64) {
     int n_open = n_open0;
     const int k = lane;
@@ -1533,26 +1593,31 @@ __device__ __forceinline__ void ha_book_spec(const HaDev& P, const HaSearch& Q, 
     }
   }
   __syncthreads();  // the open-list writes of wave 0 before the block-wide scan
+  BSTAMP(7);
   const int n_open = s_nopen;
   long long iw = 0;
   const bool go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, false, &iw);
-  if (tid == 0) {
-    long long* rc = Q.rec + (size_t)RC_N * b;
-    st_ag(rc + RC_GO, (long long)go);
-    st_ag(rc + RC_LOOP, (long long)loop);
-    st_ag(rc + RC_NN0, (long long)nn0);
-    st_ag(rc + RC_NNEW, (long long)s_nnew);
-    st_ag(rc + RC_NOPEN, (long long)n_open);
-    st_ag(rc + RC_CUR, (long long)cur0);
-    st_ag(rc + RC_IW, iw);
-  }
+  BSTAMP(8);
+  BookRec br;
+  br.v[RC_GO] = go;
+  br.v[RC_LOOP] = loop;
+  br.v[RC_NN0] = nn0;
+  br.v[RC_NNEW] = s_nnew;
+  br.v[RC_NOPEN] = n_open;
+  br.v[RC_CUR] = cur0;
+  br.v[RC_IW] = iw;
+  br.v[RC_N - 1] = 0;
+  if (stp) __hip_atomic_store(stp + 9, (unsigned long long)n_open, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#undef BSTAMP
+  return br;
 }
 
 // the scene's iteration ends (one thread): the termination of :259-271 when RS_connected found a path,
 // else the speculative pop's results published and the scene listed for the next iteration
-__device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, int B, int it, int b) {
-  const long long* rc = Q.rec + (size_t)RC_N * b;
-  const int go = (int)ld_ag(rc + RC_GO), loop = (int)ld_ag(rc + RC_LOOP);
+__device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, int B, int it, int b,
+                                          const BookRec& br) {
+  const long long* rc = br.v;
+  const int go = (int)rc[RC_GO], loop = (int)rc[RC_LOOP];
   const int rs_ok = ld_ag(A.rs_ok + b);
   if (rs_ok) {
     const size_t base = (size_t)b * Q.C;
@@ -1560,9 +1625,9 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
     Q.sc_i[SI_ACTIVE * B + b] = 0;
     Q.sc_i[SI_RSLEN * B + b] = ld_ag(A.rs_len + b);
     Q.sc_i[SI_LOOP * B + b] = loop;
-    Q.sc_i[SI_NNODES * B + b] = (int)ld_ag(rc + RC_NN0);
+    Q.sc_i[SI_NNODES * B + b] = (int)rc[RC_NN0];
     double* so = Q.states + (size_t)b * Q.mp * 3;
-    int c = (int)ld_ag(rc + RC_CUR), ns = 0;
+    int c = (int)rc[RC_CUR], ns = 0;
     for (int r = 0; r < 3; r++) so[r] = Q.st[(base + c) * 3 + r];
     ns++;
     while (Q.parent[base + c] >= 0 && Q.index[base + c] != Q.start_index[b] && ns < Q.mp) {
@@ -1575,26 +1640,33 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
     Q.sc_i[SI_NSTATES * B + b] = ns;
     return;
   }
-  Q.sc_i[SI_NNODES * B + b] = (int)ld_ag(rc + RC_NNEW);
+  Q.sc_i[SI_NNODES * B + b] = (int)rc[RC_NNEW];
   if (go) {
     Q.sc_i[SI_LOOP * B + b] = loop + 1;
-    Q.pop_seq[(size_t)b * Q.mp + loop] = ld_ag(rc + RC_IW);
+    Q.pop_seq[(size_t)b * Q.mp + loop] = rc[RC_IW];
     Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;
   } else {
     Q.sc_i[SI_ACTIVE * B + b] = 0;
-    Q.sc_i[SI_NOPEN * B + b] = (int)ld_ag(rc + RC_NOPEN);
+    Q.sc_i[SI_NOPEN * B + b] = (int)rc[RC_NOPEN];
   }
 }
 
+constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 10;  // [6..9]: bookkeeping phases
 template <int HWt, int NBGt>
 __global__ __launch_bounds__(64 * HWt) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
   __shared__ int role;
+  unsigned long long* stp = nullptr;
+  if (A.stamps && it % HA_STAMP_EVERY == 0 && it / HA_STAMP_EVERY < 40 && (int)blockIdx.x < A.stamp_blocks &&
+      threadIdx.x == 0)
+    stp = A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
+  if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!ha_iter_body<HWt, NBGt>(P, A)) return;  // block-uniform: no work for this block (not counted)
   const int per = 1 + (P.n_prim + NBGt - 1) / NBGt;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
   const int s = A.scene_of ? A.scene_of[slot] : slot;
   ha_stores_done();  // this thread's records acknowledged before the block's ticket
   __syncthreads();
+  if (stp) __hip_atomic_store(stp + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x == 0) {
     int r = 2;  // RS_connected: straight to the final ticket
     if (item > 0) {
@@ -1606,17 +1678,61 @@ __global__ __launch_bounds__(64 * HWt) void ha_step_kernel(HaDev P, HaSearch Q, 
   }
   __syncthreads();
   const int r = role;
+  if (stp) {
+    __hip_atomic_store(stp + 2, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(stp + 5, (unsigned long long)r | ((unsigned long long)s << 4) | ((unsigned long long)item << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (r == 0) return;
+  // The final ticket.  The bookkeeping block takes it before publishing anything: arriving second (the
+  // usual case) it finishes with its own values; arriving first it publishes its record and then a
+  // ready flag, which the RS_connected block, arriving second, waits for (a short wait: the bookkeeping
+  // block is running and publishes without waiting on anything).
+  long long* rc = Q.rec + (size_t)RC_N * s;
   if (r == 1) {
-    ha_book_spec<64 * HWt>(P, Q, A, B, it, s);
-    ha_stores_done();
-    __syncthreads();
+    const BookRec br = ha_book_spec<64 * HWt>(P, Q, A, B, it, s, stp);
+    if (!HA_FIN_SHORTCUT) {  // (A/B) always publish the record first
+      if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < RC_N - 1; i++) st_ag(rc + i, br.v[i]);
+        ha_stores_done();
+        st_ag(rc + RC_N - 1, 1LL);
+        if (__hip_atomic_fetch_add(Q.tk + B + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+          asm volatile("" ::: "memory");
+          st_ag(Q.tk + B + s, 0);
+          st_ag(rc + RC_N - 1, 0LL);
+          ha_finish(Q, A, B, it, s, br);
+        }
+      }
+      return;
+    }
+    if (threadIdx.x == 0) {
+      if (stp) __hip_atomic_store(stp + 3, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(Q.tk + B + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+        asm volatile("" ::: "memory");
+        st_ag(Q.tk + B + s, 0);
+        ha_finish(Q, A, B, it, s, br);
+        if (stp) __hip_atomic_store(stp + 4, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+#pragma unroll
+        for (int i = 0; i < RC_N - 1; i++) st_ag(rc + i, br.v[i]);
+        ha_stores_done();
+        st_ag(rc + RC_N - 1, 1LL);  // record ready
+      }
+    }
+    return;
   }
   if (threadIdx.x == 0 &&
       __hip_atomic_fetch_add(Q.tk + B + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
     asm volatile("" ::: "memory");
     st_ag(Q.tk + B + s, 0);
-    ha_finish(Q, A, B, it, s);
+    while (ld_ag(rc + RC_N - 1) == 0) __builtin_amdgcn_s_sleep(1);
+    BookRec br;
+#pragma unroll
+    for (int i = 0; i < RC_N - 1; i++) br.v[i] = ld_ag(rc + i);
+    st_ag(rc + RC_N - 1, 0LL);  // consumed: the next iteration's bookkeeping block sets it again
+    ha_finish(Q, A, B, it, s, br);
+    if (stp) __hip_atomic_store(stp + 4, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2036,6 +2152,28 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.dg = Q.g;
   A.cur_g = Q.cur_g;
   A.C = (int)C;
+  // MPGPU_HA_NOPRE=1: the bookkeeping reads the Dict itself (A/B of the prefetched entries)
+  static const bool nopre = getenv("MPGPU_HA_NOPRE") && atoi(getenv("MPGPU_HA_NOPRE")) == 1;
+  A.dpos = Q.pos;
+  A.df = Q.f;
+  A.dseq = Q.seq;
+  A.dindex = Q.index;
+  A.dst = Q.st;
+  A.pre = nullptr;
+  if (!split && !nopre && A.dnid) {
+    A.pre = (long long*)mp_ws(ctx, WS_HA4, sizeof(long long) * PRE_N * nB * np);
+    if (!A.pre) return MP_ERR_NOMEM;
+  }
+  static const bool stamps_on = getenv("MPGPU_HA_STAMPS") && atoi(getenv("MPGPU_HA_STAMPS")) == 1;
+  const int stamp_slots = std::min(mp / HA_STAMP_EVERY + 1, 40);  // iterations < 1,000
+  A.stamps = nullptr;
+  A.stamp_blocks = B * (1 + (np + NBG_TAIL - 1) / NBG_TAIL);
+  if (stamps_on) {
+    A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA3, sizeof(unsigned long long) * HA_STAMP_N * (size_t)stamp_slots * A.stamp_blocks);
+    if (!A.stamps) return MP_ERR_NOMEM;
+    MP_HIP(ctx, hipMemsetAsync(A.stamps, 0, sizeof(unsigned long long) * HA_STAMP_N * (size_t)stamp_slots * A.stamp_blocks,
+                               ctx->stream));
+  }
   A.scene_of = nullptr;  // slot = scene
   A.active = Q.sc_i + SI_ACTIVE * B;
   A.sc = ctx->ha_states_candi;
@@ -2047,6 +2185,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.pop_seq, 0xff, nB * mp * 8, ctx->stream));  // -1 past each scene's pops
   MP_HIP(ctx, hipMemsetAsync(Q.live, 0, sizeof(int) * (mp + 2), ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.tk, 0, sizeof(int) * 2 * nB, ctx->stream));  // the finishers reset them
+  MP_HIP(ctx, hipMemsetAsync(Q.rec, 0, sizeof(long long) * RC_N * nB, ctx->stream));  // record-ready flags
   hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
   MP_HIP(ctx, hipGetLastError());
   // The whole search loop is enqueued without host round trips: iteration i = one ha_step_kernel
@@ -2121,6 +2260,18 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         known = std::min(known, std::max(hl[cs], 1));
         checked++;
       }
+    }
+  }
+  if (A.stamps) {  // diagnostics: raw stamps to $MPGPU_HA_STAMPS_OUT (tools/ha_stamps.py reads them)
+    std::vector<unsigned long long> h((size_t)HA_STAMP_N * stamp_slots * A.stamp_blocks);
+    MP_HIP(ctx, hipMemcpyAsync(h.data(), A.stamps, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const char* fn = getenv("MPGPU_HA_STAMPS_OUT");
+    if (FILE* f = fopen(fn ? fn : "ha_stamps.bin", "wb")) {
+      const long long hdr[5] = {B, stamp_slots, A.stamp_blocks, HA_STAMP_EVERY, HA_STAMP_N};
+      fwrite(hdr, sizeof hdr, 1, f);
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
     }
   }
   // outputs: per-scene counters, then the used prefix of pop_seq / states / RS paths

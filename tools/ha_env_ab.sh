@@ -1,0 +1,15 @@
+#!/bin/bash
+# Hybrid A* A/B of env knobs: default vs each "NAME=VALUE" argument, alternating fresh processes of
+# tools/ha_plan_time.py; prints the library-call ms of plans 3-5 per run.
+# usage: bash tools/ha_env_ab.sh OUTTAG MPGPU_HA_NOPRE=1 [...]
+set -o pipefail
+O=gpurun_out/$1; shift
+mkdir -p $O
+for r in 1 2; do
+  timeout -k 10 120 python3 tools/ha_plan_time.py > $O/base_$r.log 2>&1 || exit $?
+  echo "base $(tail -3 $O/base_$r.log | sed -E 's/.*library call ([0-9.]+) ms.*/\1/' | tr '\n' ' ')"
+  for kv in "$@"; do
+    env $kv timeout -k 10 120 python3 tools/ha_plan_time.py > $O/${kv//=/_}_$r.log 2>&1 || exit $?
+    echo "$kv $(tail -3 $O/${kv//=/_}_$r.log | sed -E 's/.*library call ([0-9.]+) ms.*/\1/' | tr '\n' ' ')"
+  done
+done
