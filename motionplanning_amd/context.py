@@ -40,8 +40,12 @@ class Context:
         return self.lib.mp_ctx_stream(self.handle)
 
     def close(self):
+        """mp_ctx_destroy.  A context still joined to a communicator is refused (MPGPUError): close the
+        CommGroup (mp_comm_destroy) first; the handle then stays valid."""
         if getattr(self, "handle", None):
-            self.lib.mp_ctx_destroy(self.handle)
+            st = self.lib.mp_ctx_destroy(self.handle)
+            if st != MP_OK:
+                raise MPGPUError(st, self.lib.mp_last_error(self.handle).decode())
             self.handle = None
 
     def __del__(self):

@@ -317,6 +317,22 @@ def test_cfg2_default_feasibility_count_full_size(ctx):
     _check_plan(gpu, ref)
 
 
+def test_ctx_destroy_refused_inside_communicator():
+    """mp_ctx_destroy refuses a context that still belongs to an RCCL communicator (a dangling
+    rank otherwise); after mp_comm_destroy the same context closes normally."""
+    from motionplanning_amd.abi import MPGPUError
+    from motionplanning_amd.context import CommGroup
+
+    g = CommGroup([0])
+    try:
+        with pytest.raises(MPGPUError, match="mp_comm_destroy"):
+            g.ctxs[0].close()
+        assert g.ctxs[0].handle  # still valid
+    finally:
+        g.close()
+    assert g.ctxs[0].handle is None
+
+
 def test_sharded_plan_one_gpu_equals_plan(ctx):
     """mp_comm_init + mp_mppi_plan_sharded over a one-GPU communicator (RCCL all-gather with one rank)
     equals mp_mppi_plan of the same scenes bit for bit (U, final trajectory, cost, flags, counts).
