@@ -8,9 +8,10 @@
 //            the two waves sharing a SIMD pace each other by issue priority
 //            (MPPI_PRIO 3).  Then the block's online-softmax partial (ρ_b, η_b,
 //            Σ e·u; the latter per wave over its own rollouts, from registers
-//            prefetched when the wave ends) is published with an agent-scope
-//            release and an arrival ticket.
-//   phase 2  the last block to arrive for a scene (acquire) applies the
+//            prefetched when the wave ends) is published with agent-coherent
+//            stores (sc1), every thread's stores acknowledged, then an arrival
+//            ticket (round 4: no agent-scope release / acquire fences).
+//   phase 2  the last block to arrive for a scene applies the
 //            FeasibilityCount prefix (MPPIUtils.jl:175), combines the partials
 //            with a log-sum-exp rescale into MPPICtrl (:186-190) and runs the
 //            final TrajectoryRollout (:192-198).  It resets the ticket.
@@ -160,6 +161,22 @@ __global__ __launch_bounds__(256) void noise_prep_kernel(MppiDev P, int S, const
   }
   reinterpret_cast<double2*>(zh)[i] = make_double2(z[0], z[1]);
 }
+
+// Agent-coherent relaxed stores / loads (global_store / global_load with the sc1 policy): the records
+// one block hands to the scene's last block (block partials, per-rollout costs and feasibility flags)
+// reach the device coherence point directly, so the arrival needs no agent-scope release fence (an L2
+// write-back of the whole XCD) and the last block no acquire (L1/L2 invalidate).
+template <class T>
+__device__ __forceinline__ void st_ag(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_ag(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#ifndef MPPI_COHERENT_PARTS
+#define MPPI_COHERENT_PARTS 1  // 0: the round-3 arrival (agent-scope release / acquire fences)
+#endif
 
 // BT threads per block (4 or 8 waves); LPR lanes per rollout: 2 = lane pair (dyn_pair, the
 // two tire chains on the two lanes), 1 = one rollout per lane (dyn_lane) when the launch has a
@@ -348,8 +365,8 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   MP_STAMP(1);
   MP_STAMP_WAVE();
   if (active && side == 0) {
-    A.cost_all[(size_t)s * K + k] = c;
-    A.feas_all[(size_t)s * K + k] = (unsigned char)feas;
+    st_ag(A.cost_all + (size_t)s * K + k, c);
+    st_ag(A.feas_all + (size_t)s * K + k, (unsigned char)feas);
     if (c != c) atomicOr(A.flags, 1);
   }
   // ---------------- block partial (online softmax), MPPIUtils.jl:154-167
@@ -418,7 +435,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       double v = sh_q[0][tid];
 #pragma unroll
       for (int w = 1; w < NT / 64; w++) v = v + sh_q[w][tid];
-      part[4 + tid] = v;
+      st_ag(part + 4 + tid, v);
     }
   } else {
     // Σ_i e_i u_i[t] over this block's rollouts; fixed quarters per output, summed in order
@@ -444,25 +461,32 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
         double v = sh_q[0][t];
 #pragma unroll
         for (int i = 1; i < NQ; i++) v = v + sh_q[i][t];
-        part[4 + tt] = v;
+        st_ag(part + 4 + tt, v);
       }
       __syncthreads();
     }
   }
   if (tid == 0) {
-    part[0] = rho_b;
-    part[1] = eta_b;
-    part[2] = fc_b;
+    st_ag(part + 0, rho_b);
+    st_ag(part + 1, eta_b);
+    st_ag(part + 2, fc_b);
   }
-  // ---------------- arrival: release (Guideline 16 recipe), ticket
+  // ---------------- arrival: every thread's records acknowledged, then the ticket
   MP_STAMP(2);
-  __syncthreads();  // every wave's stores done (workgroup release waits vmcnt(0))
+  // (__syncthreads() on gfx950 waits for LDS only: each thread waits for its own stores first, so the
+  // partial written by waves 1.. is complete before wave 0 takes the ticket)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (tid == 0) {
-    __threadfence();  // agent-scope release: write back this XCD's L2
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = atomicAdd(A.tickets + s, 1u);
+    if (!MPPI_COHERENT_PARTS) {
+      __threadfence();  // agent-scope release: write back this XCD's L2
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned t = __hip_atomic_fetch_add(A.tickets + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sh_last = (t == (unsigned)(A.nb - 1));
-    if (sh_last) {
+    // the last block reads the partials agent-coherently while it stages them in LDS; without the
+    // stage (too little LDS) it reads them with plain loads, after an acquire
+    if (sh_last && (!MPPI_COHERENT_PARTS || A.lds_part < 0)) {
       __threadfence();  // agent-scope acquire: invalidate this CU's L1
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -480,7 +504,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   if (A.lds_part >= 0) {
     double* pl = dyn + A.lds_part;
     const int n = A.nb * A.pstride;
-    for (int i = tid; i < n; i += NT) pl[i] = partG[i];
+    for (int i = tid; i < n; i += NT) pl[i] = ld_ag(partG + i);
     __syncthreads();
     partS = pl;
   }
@@ -498,7 +522,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
       }
       for (int r = 0; r < RPB; r++) {
         const int kr = bstar * RPB + r;
-        cum += A.feas_all[(size_t)s * K + kr];
+        cum += ld_ag(A.feas_all + (size_t)s * K + kr);
         if (cum == P.FC + 1) { m = kr + 1; break; }
       }
       fcount = P.FC + 1;
@@ -516,7 +540,7 @@ __global__ __launch_bounds__(BT) void mppi_plan_kernel(MppiDev P, PlanArgs A) {
   if (has_p) {
     const int kr = p0 + pair;
     const bool in = kr < m;
-    const double cr = in ? A.cost_all[(size_t)s * K + kr] : __builtin_inf();
+    const double cr = in ? ld_ag(A.cost_all + (size_t)s * K + kr) : __builtin_inf();
     rho_p = block_reduce_min(cr, sh_red);
     const double er = in ? mpj_exp(P.nil * (cr - rho_p)) : 0.0;
     if (side == 0) sh_e[pair] = er;
