@@ -2448,7 +2448,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // every scene's max_pops iterations).  (Round 1 fused the bookkeeping behind an agent-scope release
   // in every block -- an L2 write-back each -- and measured 67-90 ms vs 40 ms; ha_step_kernel hands
   // its records over with agent-coherent stores instead, so no block writes back its L2.)
-  constexpr int CH = 16, NCK = 4;
+  // (A/B) MPGPU_HA_POLL_CH: iterations per live-count poll (default 16)
+  static const int CH = getenv("MPGPU_HA_POLL_CH") ? std::max(1, atoi(getenv("MPGPU_HA_POLL_CH"))) : 16;
+  constexpr int NCK = 4;
   int* hl = (int*)mp_pinned(ctx, sizeof(int) * NCK);
   if (!hl) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
   hipEvent_t ev[NCK];

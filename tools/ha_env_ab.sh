@@ -8,8 +8,10 @@ mkdir -p $O
 for r in 1 2; do
   timeout -k 10 120 python3 tools/ha_plan_time.py > $O/base_$r.log 2>&1 || exit $?
   echo "base $(tail -3 $O/base_$r.log | sed -E 's/.*library call ([0-9.]+) ms.*/\1/' | tr '\n' ' ')"
+  i=0
   for kv in "$@"; do
-    env $kv timeout -k 10 120 python3 tools/ha_plan_time.py > $O/${kv//=/_}_$r.log 2>&1 || exit $?
-    echo "$kv $(tail -3 $O/${kv//=/_}_$r.log | sed -E 's/.*library call ([0-9.]+) ms.*/\1/' | tr '\n' ' ')"
+    i=$((i + 1))
+    env $kv timeout -k 10 120 python3 tools/ha_plan_time.py > $O/v${i}_$r.log 2>&1 || exit $?
+    echo "$(echo $kv | sed -E 's#=/[^ ]*/#=#g') $(tail -3 $O/v${i}_$r.log | sed -E 's/.*library call ([0-9.]+) ms.*/\1/' | tr '\n' ' ')"
   done
 done
