@@ -114,7 +114,17 @@ __constant__ signed char kRsTr[12][5] = {{0, 1, 2}, {0, 1, 2}, {0, 1, 2}, {0, 1,
                                          {0, 3, 1, 2}, {0, 1, 3, 2}, {0, 3, 1, 3, 2}};
 __constant__ signed char kRsN[12] = {3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 5};
 
-__device__ __forceinline__ double rs_word(int w_, const RsPre& R, Cmd* c) {
+// (A/B) HA_RS_NOINLINE=1: one out-of-line copy of rs_word instead of one per call site (the step
+// kernel's instruction footprint)
+#ifndef HA_RS_NOINLINE
+#define HA_RS_NOINLINE 0
+#endif
+#if HA_RS_NOINLINE
+#define RS_WORD_ATTR __attribute__((noinline))
+#else
+#define RS_WORD_ATTR __forceinline__
+#endif
+__device__ RS_WORD_ATTR double rs_word(int w_, const RsPre& R, Cmd* c) {
   const int w = __builtin_amdgcn_readfirstlane(w_);  // wave-uniform word: scalar branches and table loads
   const double p = R.p;
   const bool useA = (w == 1) | (w == 3) | (w == 4) | (w == 5) | (w == 8) | (w == 9);
@@ -186,7 +196,7 @@ __device__ __forceinline__ double rs_word(int w_, const RsPre& R, Cmd* c) {
   else if (w <= 6) valid = rho <= 4;
   else if (w == 7) valid = (rho <= 6) && (0 <= u1) && (u1 <= 1);
   else valid = rho >= 4;
-  {
+  if (c) {
     const int wi = w - 1;
     c->n = kRsN[wi];
 #pragma unroll
@@ -408,19 +418,6 @@ struct IterArgs {
   const double* dg;       // [B][C] node g
   const double* cur_g;    // [B] the popped node's g
   int C;
-  // ha_step_kernel: the neighbour groups also read the rest of each neighbour's Dict entry (pos, f, seq,
-  // Encode index, state: the loads overlap the collision sweep) into pre[B][n_prim][PRE_N], so the
-  // scene's bookkeeping starts from records instead of two levels of dependent Dict loads
-  const int* dpos;
-  const double* df;
-  const long long* dseq;
-  const long long* dindex;
-  const double* dst;
-  long long* pre;
-  // ha_step_kernel with a scan block per scene (bps = per + 1; 0: per): block `per` of each scene scans
-  // the open list as the launch found it and publishes its HA_TOPK least entries in cand[B][CAND_N]
-  int bps;
-  long long* cand;
   // MPGPU_HA_STAMPS=1 (diagnostics): s_memrealtime stamps of every block of every STAMP_EVERY-th
   // iteration, [slot][block][6]: entry, body done, role decided, bookkeeping done, finish done, role
   unsigned long long* stamps;
@@ -435,12 +432,6 @@ struct IterArgs {
   unsigned char* fr;     // [B][n_prim]
   double* h;             // [B][n_prim]
 };
-
-enum { PRE_HIT = 0, PRE_G, PRE_POS, PRE_F, PRE_SEQ, PRE_IDX, PRE_ST, PRE_N = PRE_ST + 3 };
-// the scan block's candidates: [0] count, then HA_TOPK records of CF fields (key order)
-constexpr int HA_TOPK = 8;
-enum { CF_F = 0, CF_SEQ, CF_POS, CF_ID, CF_G, CF_IX, CF_ST, CF_N = CF_ST + 3 };
-constexpr int CAND_N = 1 + HA_TOPK * CF_N;
 
 // Agent-coherent relaxed stores / loads (global_store / global_load with the sc1 policy: they reach
 // and read the device coherence point, past the per-XCD L2).  ha_step_kernel hands per-scene records
@@ -495,6 +486,11 @@ static_assert(12 % HW == 0, "HA_WAVES must divide the 12 Reeds-Shepp words");
 // plan): 12 waves per block (one Reeds-Shepp word per wave) and 4 neighbours per expansion block
 // (16 blocks per scene: the collision sweep is one pose per thread), so a lone scene's iteration
 // spreads over 17 CUs instead of 5.
+// diagnostics: -DHA_STAMP_CODE=1 compiles the per-block phase stamps in (MPGPU_HA_STAMPS=1 then turns
+// them on; tools/ha_stamps.py reads them) -- out by default: the code alone cost 0.4 ms per plan (r04zb)
+#ifndef HA_STAMP_CODE
+#define HA_STAMP_CODE 0
+#endif
 #ifndef HA_NBG_TAIL
 #define HA_NBG_TAIL 4
 #endif
@@ -515,19 +511,15 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   HTIME(12);
   double bc = __builtin_inf();
   int bi = 1 << 20;
-  Cmd cb;  // CMD: the commands of this lane's best word (its variant, this wave's words)
 #pragma unroll 1
   for (int w = WPW * wave + 1; w <= WPW * wave + WPW; w++) {
-    Cmd c;
-    const double cost = rs_word(w, R, &c);
+    const double cost = rs_word(w, R, nullptr);
     const int id = 4 * (w - 1) + var;
     if (rs_before(cost, id, bc, bi)) {
       bc = cost;
       bi = id;
-      if (CMD) cb = c;
     }
   }
-  int own = bi;  // this lane's own best (before the lane exchange)
 #pragma unroll
   for (int o = 2; o >= 1; o >>= 1) {
     const double ov = __shfl_xor(bc, o);
@@ -546,9 +538,14 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
     if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; }
   }
   *best_id = ix;
-  if (CMD && own == ix && tid == 64 * ((ix / 4) / WPW) + (ix & 3)) {
-    // the lane that evaluated the winning candidate stores its commands with allpath's
-    // gear/steer flips (timeflip: gear, reflect: steer, reverse: both), as rs_commands does
+  // CMD: the wave that evaluated the winning word evaluates it again for its commands (the same
+  // operations on the same operands: the same bits) -- cheaper than carrying every lane's best
+  // commands through the word loop, which set the kernel's register peak -- and the lane of the
+  // winning variant stores them with allpath's gear/steer flips (timeflip: gear, reflect: steer,
+  // reverse: both), as rs_commands does
+  if (CMD && wave == (ix / 4) / WPW) {  // wave-uniform
+    Cmd cb;
+    rs_word(ix / 4 + 1, R, &cb);
     const int n = v < __builtin_inf() ? cb.n : 0;
 #pragma unroll
     for (int r = 0; r < 5; r++) {
@@ -560,9 +557,11 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
         if (var == 1 || var == 3) ge = -1 * ge;
         if (var == 2 || var == 3) st = -1 * st;
       }
-      cmd_out[r * 3 + 0] = tr;
-      cmd_out[r * 3 + 1] = ge;
-      cmd_out[r * 3 + 2] = st;
+      if (lane == (ix & 3)) {
+        cmd_out[r * 3 + 0] = tr;
+        cmd_out[r * 3 + 1] = ge;
+        cmd_out[r * 3 + 2] = st;
+      }
     }
   }
   return v;
@@ -586,9 +585,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   __shared__ int g_free[NBG];
   __shared__ int g_need[NBG];
   __shared__ int sh_n;
-  const int per = 1 + (P.n_prim + NBG - 1) / NBG, bps = A.bps ? A.bps : per;
-  const int slot = blockIdx.x / bps, item = blockIdx.x % bps;
-  if (item >= per) return false;  // the scan block (ha_step_kernel)
+  const int per = 1 + (P.n_prim + NBG - 1) / NBG;
+  const int slot = blockIdx.x / per, item = blockIdx.x % per;
   // the live count and the slot's scene are independent loads (slot < the grid's bound <= B keeps the
   // list read in bounds); a scene on the bookkeeping's list (n_live set) is live, so its flag is not
   // read: the node and goal loads then follow one round trip instead of three
@@ -795,32 +793,10 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     // The Dict at this launch is the one this iteration's FindNewNode starts from (the bookkeeping
     // that changes it runs after every neighbour group of the scene, ha_step_kernel / ha_book_kernel).
     double gd = 0.0;
-    long long pv[PRE_N - 2];  // pos, f, seq, index, state of the Dict entry (A.pre)
-    if (hit >= 0) {  // loaded now, used after the sweep
-      const size_t q = (size_t)s * A.C + hit;
-      gd = A.dg[q];
-      if (A.pre) {
-        pv[0] = A.dpos[q];
-        pv[1] = __double_as_longlong(A.df[q]);
-        pv[2] = A.dseq[q];
-        pv[3] = A.dindex[q];
-        pv[4] = __double_as_longlong(A.dst[3 * q]);
-        pv[5] = __double_as_longlong(A.dst[3 * q + 1]);
-        pv[6] = __double_as_longlong(A.dst[3 * q + 2]);
-      }
-    }
+    if (hit >= 0) gd = A.dg[(size_t)s * A.C + hit];  // loaded now, used after the sweep
     sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
     HTIME(4);
     if (tid < nk) g_need[tid] = !A.dnid || !(hit >= 0 && !(A.cur_g[s] + P.expand_time < gd));
-    if (A.pre && tid < nk) {
-      long long* pr = A.pre + ((size_t)s * P.n_prim + k0 + tid) * PRE_N;
-      st_ag(pr + PRE_HIT, (long long)hit);
-      if (hit >= 0) {
-        st_ag(pr + PRE_G, __double_as_longlong(gd));
-#pragma unroll
-        for (int i = 0; i < PRE_N - 2; i++) st_ag(pr + PRE_POS + i, pv[i]);
-      }
-    }
     __syncthreads();
     HTIME(5);
     int any = 0;
@@ -1162,110 +1138,6 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   return true;
 }
 
-// The scan block of ha_step_kernel: the HA_TOPK least (f, seq) entries of scene b's open list as this
-// launch found it (the bookkeeping changes it only after every group and this block have arrived), with
-// their payload, published agent-coherently in cand[b].  The bookkeeping then pops from these
-// candidates and the entries FindNewNode changed or appended (ha_pop_merge), without scanning the list.
-template <int NT>
-__device__ __forceinline__ void ha_scan_topk(const HaSearch& Q, long long* cand, int B, int b) {
-  constexpr int K = HA_TOPK;
-  __shared__ double t_f[NT / 64];
-  __shared__ long long t_s[NT / 64];
-  __shared__ int t_p[NT / 64];
-  __shared__ int c_p[K];
-  __shared__ int s_n;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const size_t base = (size_t)b * Q.C;
-  if (tid == 0) s_n = Q.sc_i[SI_NOPEN * B + b];
-  __syncthreads();
-  const int n = s_n;
-  // this thread's K least entries, ascending (insertion into a sorted register list)
-  double lf[K];
-  long long ls[K];
-  int lp[K];
-#pragma unroll
-  for (int i = 0; i < K; i++) { lf[i] = __builtin_inf(); ls[i] = 0x7fffffffffffffffLL; lp[i] = -1; }
-  for (int p0 = tid; p0 < n; p0 += 4 * NT) {
-    double fv[4];
-    long long sv[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int p = p0 + u * NT;
-      fv[u] = p < n ? Q.of[base + p] : 0.0;
-      sv[u] = p < n ? Q.oseq[base + p] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int p = p0 + u * NT;
-      if (p < n && (lp[K - 1] < 0 || key_before(fv[u], sv[u], lf[K - 1], ls[K - 1]))) {
-        lf[K - 1] = fv[u]; ls[K - 1] = sv[u]; lp[K - 1] = p;
-#pragma unroll
-        for (int i = K - 1; i > 0; i--) {
-          if (lp[i - 1] < 0 || key_before(lf[i], ls[i], lf[i - 1], ls[i - 1])) {
-            const double tf = lf[i]; lf[i] = lf[i - 1]; lf[i - 1] = tf;
-            const long long ts = ls[i]; ls[i] = ls[i - 1]; ls[i - 1] = ts;
-            const int tp = lp[i]; lp[i] = lp[i - 1]; lp[i - 1] = tp;
-          }
-        }
-      }
-    }
-  }
-  // K rounds of a block argmin over the threads' list heads; the owner drops its head
-  const int nc = n < K ? n : K;
-  for (int r = 0; r < nc; r++) {
-    double bf = lf[0];
-    long long bs = ls[0];
-    int bp = lp[0];
-    key_min_dpp<0xB1>(bf, bs, bp);
-    key_min_dpp<0x4E>(bf, bs, bp);
-    key_min_dpp<0x141>(bf, bs, bp);
-    key_min_dpp<0x140>(bf, bs, bp);
-    {
-      double wf = __longlong_as_double(readlane_l(__double_as_longlong(bf), 0));
-      long long ws = readlane_l(bs, 0);
-      int wp_ = __builtin_amdgcn_readlane(bp, 0);
-#pragma unroll
-      for (int q = 1; q < 4; q++) {
-        const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(bf), 16 * q));
-        const long long os = readlane_l(bs, 16 * q);
-        const int op = __builtin_amdgcn_readlane(bp, 16 * q);
-        if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
-      }
-      bf = wf; bs = ws; bp = wp_;
-    }
-    if (lane == 0) { t_f[wave] = bf; t_s[wave] = bs; t_p[wave] = bp; }
-    __syncthreads();
-    if (tid == 0) {
-      for (int w = 1; w < NT / 64; w++) {
-        const int op = t_p[w];
-        if (op >= 0 && (bp < 0 || key_before(t_f[w], t_s[w], bf, bs))) { bf = t_f[w]; bs = t_s[w]; bp = op; }
-      }
-      c_p[r] = bp;
-    }
-    __syncthreads();
-    if (lp[0] >= 0 && lp[0] == c_p[r]) {  // the owner of the round's least entry: next head
-#pragma unroll
-      for (int i = 0; i < K - 1; i++) { lf[i] = lf[i + 1]; ls[i] = ls[i + 1]; lp[i] = lp[i + 1]; }
-      lf[K - 1] = __builtin_inf(); ls[K - 1] = 0x7fffffffffffffffLL; lp[K - 1] = -1;
-    }
-  }
-  // the candidates' records (one thread each), in key order
-  long long* cr = cand + (size_t)b * CAND_N;
-  if (tid < nc) {
-    const size_t q = base + c_p[tid];
-    long long* c = cr + 1 + tid * CF_N;
-    st_ag(c + CF_F, __double_as_longlong(Q.of[q]));
-    st_ag(c + CF_SEQ, Q.oseq[q]);
-    st_ag(c + CF_POS, (long long)c_p[tid]);
-    st_ag(c + CF_ID, (long long)Q.oid[q]);
-    st_ag(c + CF_G, __double_as_longlong(Q.og[q]));
-    st_ag(c + CF_IX, Q.oix[q]);
-#pragma unroll
-    for (int i = 0; i < 3; i++) st_ag(c + CF_ST + i, __double_as_longlong(Q.ost[q * 3 + i]));
-  }
-  if (tid == 0) st_ag(cr, (long long)nc);
-}
-
 // starting node (setup.jl:112-121) and the first popfirst!; block b = scene b
 __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B, const double* start) {
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -1542,8 +1414,7 @@ template <int NT>
 __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& Q, const IterArgs& A, int B, int it,
                                                 int b, unsigned long long* stp = nullptr) {
 #define BSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-  __shared__ int s_nopen, s_nnew, s_full, s_go;
-  __shared__ long long s_iw;
+  __shared__ int s_nopen, s_nnew;
   __shared__ long long s_vix[64];
   __shared__ int s_dup[4][64];
   static_assert(NT >= 256, "the duplicate check below runs on four waves");
@@ -1569,24 +1440,6 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
     nb1 = ld_ag(A.nb + 3 * q + 1);
     nb2 = ld_ag(A.nb + 3 * q + 2);
   }
-  // (scan block) candidate `lane` of the open list's least entries as the launch found it, their count,
-  // and the list's last entry then -- independent loads, issued with the neighbour records
-  long long cv[CF_N];
-  int ncand = -1;
-  double lo_f = 0.0, lo_g = 0.0, lo_s0 = 0.0, lo_s1 = 0.0, lo_s2 = 0.0;
-  long long lo_seq = 0, lo_ix = 0;
-  int lo_id = 0;
-  if (A.cand && tid < 64) {
-    const long long* cr = A.cand + (size_t)b * CAND_N;
-    ncand = (int)ld_ag(cr);
-#pragma unroll
-    for (int i = 0; i < CF_N; i++) cv[i] = lane < HA_TOPK ? ld_ag(cr + 1 + lane * CF_N + i) : 0;
-    if (n_open0 > 0) {
-      const size_t q = base + n_open0 - 1;
-      lo_f = Q.of[q]; lo_seq = Q.oseq[q]; lo_id = Q.oid[q]; lo_g = Q.og[q]; lo_ix = Q.oix[q];
-      lo_s0 = Q.ost[q * 3]; lo_s1 = Q.ost[q * 3 + 1]; lo_s2 = Q.ost[q * 3 + 2];
-    }
-  }
   // duplicates: lane k of wave 0 is neighbour k; an earlier valid lane with the same Encode index makes
   // it one (the comparisons split over four waves, as in ha_book)
   const bool valid = tid < np && ix != 0 && frk;
@@ -1608,20 +1461,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
   int po = 0;
   long long so0 = 0, io = 0;
-  if (valid && A.pre) {  // the neighbour group read the Dict entry (same Dict: nothing changed it since)
-    const long long* pr = A.pre + ((size_t)b * np + tid) * PRE_N;
-    hit = (int)ld_ag(pr + PRE_HIT);
-    if (hit >= 0) {
-      gd = __longlong_as_double(ld_ag(pr + PRE_G));
-      po = (int)ld_ag(pr + PRE_POS);
-      fo_ = __longlong_as_double(ld_ag(pr + PRE_F));
-      so0 = ld_ag(pr + PRE_SEQ);
-      io = ld_ag(pr + PRE_IDX);
-      dst0 = __longlong_as_double(ld_ag(pr + PRE_ST));
-      dst1 = __longlong_as_double(ld_ag(pr + PRE_ST + 1));
-      dst2 = __longlong_as_double(ld_ag(pr + PRE_ST + 2));
-    }
-  } else if (valid) {
+  if (valid) {
     hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
     if (hit >= 0) {
       gd = Q.g[base + hit];
@@ -1718,106 +1558,10 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
       }
     }
     n_open += n_app;
-    // popfirst! from the scan block's candidates (the least entries of the list as the launch found it)
-    // and the entries FindNewNode changed or appended: exact whenever one candidate is unchanged (every
-    // unchanged entry outside the candidates has a key above all of theirs) or the list held fewer than
-    // HA_TOPK entries; else (every candidate changed) the full scan below.
-    int full = 1, go_m = 0;
-    long long iw_m = 0;
-    if (A.cand) {
-      const int nc = __builtin_amdgcn_readfirstlane(ncand);
-      const int cid = (int)cv[CF_ID];
-      bool inval = false;
-      for (unsigned long long m = m_chg; m; m &= m - 1) inval |= __shfl(id, __builtin_ctzll(m)) == cid;
-      const bool hasB = lane < nc && !inval;
-      const unsigned long long m_b = __ballot(hasB);
-      full = nc == HA_TOPK && m_b == 0;
-      if (!full && n_open > 0 && loop < Q.mp) {
-        const bool hasA = chg || app;
-        const int pA = chg ? po : n_open0 + __popcll(m_app & below);
-        const double fB = __longlong_as_double(cv[CF_F]);
-        const long long sB = cv[CF_SEQ];
-        const bool useA = hasA && (!hasB || key_before(tf, nseq, fB, sB));
-        double bf = useA ? tf : (hasB ? fB : __builtin_inf());
-        long long bs = useA ? nseq : sB;
-        int bl = (hasA || hasB) ? lane : -1;
-        const int cpos = useA ? pA : (int)cv[CF_POS];
-        const int cidv = useA ? id : cid;
-        const double cg = useA ? tg : __longlong_as_double(cv[CF_G]);
-        const long long cix = useA ? nix : cv[CF_IX];
-        const double cs0 = useA ? nst0 : __longlong_as_double(cv[CF_ST]);
-        const double cs1 = useA ? nst1 : __longlong_as_double(cv[CF_ST + 1]);
-        const double cs2 = useA ? nst2 : __longlong_as_double(cv[CF_ST + 2]);
-        key_min_dpp<0xB1>(bf, bs, bl);
-        key_min_dpp<0x4E>(bf, bs, bl);
-        key_min_dpp<0x141>(bf, bs, bl);
-        key_min_dpp<0x140>(bf, bs, bl);
-        double wf = __longlong_as_double(readlane_l(__double_as_longlong(bf), 0));
-        long long ws = readlane_l(bs, 0);
-        int wl = __builtin_amdgcn_readlane(bl, 0);
-#pragma unroll
-        for (int q4 = 1; q4 < 4; q4++) {
-          const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(bf), 16 * q4));
-          const long long os = readlane_l(bs, 16 * q4);
-          const int ol = __builtin_amdgcn_readlane(bl, 16 * q4);
-          if (ol >= 0 && (wl < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wl = ol; }
-        }
-        // the winner (lane wl's choice) and the list's last entry after FindNewNode
-        const int wpos = __builtin_amdgcn_readlane(cpos, wl), wid = __builtin_amdgcn_readlane(cidv, wl);
-        const double wg = __longlong_as_double(readlane_l(__double_as_longlong(cg), wl));
-        const long long wix = readlane_l(cix, wl);
-        const double ws0 = __longlong_as_double(readlane_l(__double_as_longlong(cs0), wl));
-        const double ws1 = __longlong_as_double(readlane_l(__double_as_longlong(cs1), wl));
-        const double ws2 = __longlong_as_double(readlane_l(__double_as_longlong(cs2), wl));
-        const int last = n_open - 1;
-        double lf = lo_f, lg = lo_g, l0 = lo_s0, l1 = lo_s1, l2 = lo_s2;
-        long long lsq = lo_seq, lix = lo_ix;
-        int lid = lo_id;
-        const unsigned long long m_last = __ballot(hasA && pA == last);  // appended last, or changed last
-        if (m_last) {
-          const int jl = __builtin_ctzll(m_last);
-          lf = __longlong_as_double(readlane_l(__double_as_longlong(tf), jl));
-          lsq = readlane_l(nseq, jl);
-          lg = __longlong_as_double(readlane_l(__double_as_longlong(tg), jl));
-          if (n_app > 0) {  // appended: every field is the lane's
-            lid = __builtin_amdgcn_readlane(id, jl);
-            lix = readlane_l(nix, jl);
-            l0 = __longlong_as_double(readlane_l(__double_as_longlong(nst0), jl));
-            l1 = __longlong_as_double(readlane_l(__double_as_longlong(nst1), jl));
-            l2 = __longlong_as_double(readlane_l(__double_as_longlong(nst2), jl));
-          }
-        }
-        if (wpos != last) {  // the last entry moves into the winner's place (ha_pop's removal)
-          if (lane == 0) {
-            Q.of[base + wpos] = lf;
-            Q.oseq[base + wpos] = lsq;
-            Q.oid[base + wpos] = lid;
-            Q.og[base + wpos] = lg;
-            Q.oix[base + wpos] = lix;
-            Q.pos[base + lid] = wpos;
-          }
-          if (lane < 3) Q.ost[(base + wpos) * 3 + lane] = lane == 0 ? l0 : (lane == 1 ? l1 : l2);
-        }
-        if (lane == 0) {
-          Q.pos[base + wid] = -1;
-          Q.sc_i[SI_NOPEN * B + b] = last;
-          Q.sc_i[SI_CUR * B + b] = wid;
-          Q.cur_g[b] = wg;
-          Q.cur_ix[b] = wix;
-        }
-        double* nd = Q.node + (size_t)(it & 1) * 3 * B;
-        if (lane < 3) nd[3 * b + lane] = lane == 0 ? ws0 : (lane == 1 ? ws1 : ws2);
-        go_m = 1;
-        iw_m = wix;
-      }
-    }
     if (lane == 0) {
       Q.ctr[b] = ctr + n_chg + n_app;
       s_nopen = n_open;
       s_nnew = nn0 + n_new;
-      s_full = full;
-      s_go = go_m;
-      s_iw = iw_m;
     }
   }
   __syncthreads();  // the open-list writes of wave 0 before the block-wide scan
@@ -1825,12 +1569,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   const int n_open = s_nopen;
   long long iw = 0;
   bool go;
-  if (s_full) {  // block-uniform
-    go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, false, &iw);
-  } else {
-    go = s_go;
-    iw = s_iw;
-  }
+  go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, false, &iw);
   BSTAMP(8);
   BookRec br;
   br.v[RC_GO] = go;
@@ -1885,26 +1624,28 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
   }
 }
 
+// Waves per SIMD each shape is compiled for.  The full-width shape (4-wave blocks, 1,280 of them at 256
+// scenes) is occupancy-bound: 133 VGPRs would allow 3 waves per SIMD; 4 costs 20 B of spills and gains
+// 0.3 ms per plan (r04zc: 29.7 vs 30.0 ms; round 4 had drifted to 169 VGPRs, 2 waves, 31.5 ms).  The
+// tail shape's 12-wave blocks take one CU each either way (6 waves: 80 VGPRs + spills, 0.2 ms slower).
+#ifndef HA_WPE_FULL
+#define HA_WPE_FULL 4
+#endif
+#ifndef HA_WPE_TAIL
+#define HA_WPE_TAIL 1
+#endif
 constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 10;  // [6..9]: bookkeeping phases
 template <int HWt, int NBGt>
-__global__ __launch_bounds__(64 * HWt) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
+__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == 4 ? HA_WPE_FULL : HA_WPE_TAIL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
   __shared__ int role;
   unsigned long long* stp = nullptr;
-  if (A.stamps && it % HA_STAMP_EVERY == 0 && it / HA_STAMP_EVERY < 40 && (int)blockIdx.x < A.stamp_blocks &&
+  if (HA_STAMP_CODE && A.stamps && it % HA_STAMP_EVERY == 0 && it / HA_STAMP_EVERY < 40 && (int)blockIdx.x < A.stamp_blocks &&
       threadIdx.x == 0)
     stp = A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int per = 1 + (P.n_prim + NBGt - 1) / NBGt, bps = A.bps ? A.bps : per;
-  const int slot = blockIdx.x / bps, item = blockIdx.x % bps;
-  if (item == per) {  // the scan block (A.bps = per + 1): the open list's least entries for the bookkeeping
-    const int n_live = A.n_live ? *A.n_live : A.n_active;
-    if (slot >= n_live) return;
-    const int sc = A.scene_of ? A.scene_of[slot] : slot;
-    if (!A.n_live && A.active && !A.active[sc]) return;
-    ha_scan_topk<64 * HWt>(Q, A.cand, B, sc);
-  } else if (!ha_iter_body<HWt, NBGt>(P, A)) {
-    return;  // block-uniform: no work for this block (not counted)
-  }
+  const int per = 1 + (P.n_prim + NBGt - 1) / NBGt;
+  const int slot = blockIdx.x / per, item = blockIdx.x % per;
+  if (!ha_iter_body<HWt, NBGt>(P, A)) return;  // block-uniform: no work for this block (not counted)
   const int s = A.scene_of ? A.scene_of[slot] : slot;
   ha_stores_done();  // this thread's records acknowledged before the block's ticket
   __syncthreads();
@@ -1913,7 +1654,7 @@ __global__ __launch_bounds__(64 * HWt) void ha_step_kernel(HaDev P, HaSearch Q, 
     int r = 2;  // RS_connected: straight to the final ticket
     if (item > 0) {
       const int t = __hip_atomic_fetch_add(Q.tk + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      r = t == bps - 2 ? 1 : 0;  // the last of the neighbour groups (and the scan block) does the bookkeeping
+      r = t == per - 2 ? 1 : 0;  // the last of the neighbour groups does the bookkeeping
       if (r) st_ag(Q.tk + s, 0);
     }
     role = r;
@@ -2394,32 +2135,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.dg = Q.g;
   A.cur_g = Q.cur_g;
   A.C = (int)C;
-  // MPGPU_HA_NOPRE=1: the bookkeeping reads the Dict itself (A/B of the prefetched entries)
-  static const bool nopre = getenv("MPGPU_HA_NOPRE") && atoi(getenv("MPGPU_HA_NOPRE")) == 1;
-  A.dpos = Q.pos;
-  A.df = Q.f;
-  A.dseq = Q.seq;
-  A.dindex = Q.index;
-  A.dst = Q.st;
-  A.pre = nullptr;
-  if (!split && !nopre && A.dnid) {
-    A.pre = (long long*)mp_ws(ctx, WS_HA4, sizeof(long long) * PRE_N * nB * np);
-    if (!A.pre) return MP_ERR_NOMEM;
-  }
-  // scan blocks (MPGPU_HA_SCAN: 0 none -- the bookkeeping scans the whole open list; 1 in the tail shape
-  // only; 2 in every launch)
-  static const int scan_mode = getenv("MPGPU_HA_SCAN") ? atoi(getenv("MPGPU_HA_SCAN")) : 1;
-  long long* cand = nullptr;
-  A.cand = nullptr;
-  A.bps = 0;
-  if (!split && scan_mode > 0) {
-    cand = (long long*)mp_ws(ctx, WS_HA5, sizeof(long long) * CAND_N * nB);
-    if (!cand) return MP_ERR_NOMEM;
-  }
-  static const bool stamps_on = getenv("MPGPU_HA_STAMPS") && atoi(getenv("MPGPU_HA_STAMPS")) == 1;
+  static const bool stamps_on = HA_STAMP_CODE && getenv("MPGPU_HA_STAMPS") && atoi(getenv("MPGPU_HA_STAMPS")) == 1;
   const int stamp_slots = std::min(mp / HA_STAMP_EVERY + 1, 40);  // iterations < 1,000
   A.stamps = nullptr;
-  A.stamp_blocks = B * (2 + (np + NBG_TAIL - 1) / NBG_TAIL);
+  A.stamp_blocks = B * (1 + (np + NBG_TAIL - 1) / NBG_TAIL);
   if (stamps_on) {
     A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA3, sizeof(unsigned long long) * HA_STAMP_N * (size_t)stamp_slots * A.stamp_blocks);
     if (!A.stamps) return MP_ERR_NOMEM;
@@ -2485,19 +2204,13 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
       hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     } else if (tail) {
-      A.cand = scan_mode >= 1 ? cand : nullptr;
-      A.bps = A.cand ? per_tail + 1 : 0;
-      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * (per_tail + (A.cand ? 1 : 0)))),
+      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)),
                          dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
     } else if (known * per <= mid_blocks) {
-      A.cand = scan_mode >= 2 ? cand : nullptr;
-      A.bps = A.cand ? per + 1 : 0;
-      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG>), dim3((unsigned)(known * (per + (A.cand ? 1 : 0)))),
+      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG>), dim3((unsigned)(known * per)),
                          dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
     } else {
-      A.cand = scan_mode >= 2 ? cand : nullptr;
-      A.bps = A.cand ? per + 1 : 0;
-      hipLaunchKernelGGL((ha_step_kernel<HW, NBG>), dim3((unsigned)(known * (per + (A.cand ? 1 : 0)))), dim3(HT), 0,
+      hipLaunchKernelGGL((ha_step_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0,
                          ctx->stream, D, Q, A, B, it);
     }
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Hybrid A* A/B of env knobs: default vs each "NAME=VALUE" argument, alternating fresh processes of
 # tools/ha_plan_time.py; prints the library-call ms of plans 3-5 per run.
-# usage: bash tools/ha_env_ab.sh OUTTAG MPGPU_HA_NOPRE=1 [...]
+# usage: bash tools/ha_env_ab.sh OUTTAG MPGPU_HA_TAIL_BLOCKS=256 "MPGPU_LIB=$PWD/variant.so" [...]
 set -o pipefail
 O=gpurun_out/$1; shift
 mkdir -p $O

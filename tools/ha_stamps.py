@@ -1,6 +1,6 @@
 """Phase timing of ha_step_kernel from MPGPU_HA_STAMPS=1 stamps (s_memrealtime, 100 MHz).
 
-usage: MPGPU_HA_STAMPS=1 MPGPU_HA_STAMPS_OUT=gpurun_out/ha_stamps.bin python3 tools/ha_plan_time.py
+usage: (a library built with -DHA_STAMP_CODE=1) MPGPU_HA_STAMPS=1 MPGPU_HA_STAMPS_OUT=gpurun_out/ha_stamps.bin python3 tools/ha_plan_time.py
        python3 tools/ha_stamps.py gpurun_out/ha_stamps.bin
 For every stamped iteration: the kernel span (first entry to last finish), and per scene the RS_connected
 block's body, the neighbour groups' bodies (last one), the bookkeeping and the finisher, in us relative
