@@ -1016,7 +1016,8 @@ __device__ __forceinline__ void key_min_dpp(double& f, long long& sq, int& p) {
 constexpr int BKT = 256;
 template <int NT>
 __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int tid,
-                                       double* node_out, bool direct, long long* iw_out) {
+                                       double* node_out, bool direct, long long* iw_out,
+                                       unsigned long long* stp = nullptr) {
   static_assert(NT % 64 == 0, "whole waves");
   __shared__ double r_f[NT / 64];
   __shared__ long long r_s[NT / 64];
@@ -1069,6 +1070,10 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
     p1s = Q.ost[(base + bp) * 3 + 1];
     p2s = Q.ost[(base + bp) * 3 + 2];
   }
+  if (HA_STAMP_CODE && stp) {  // diagnostics: the scan's loads returned (the payload waited for)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(stp + 10, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   const int own = bp;
   // wave minimum: quad xor 1 / xor 2, half-row and row mirrors, then the four rows by v_readlane
   key_min_dpp<0xB1>(bf, bs, bp);
@@ -1100,12 +1105,28 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
     r_pay[wave][4] = p2s;
   }
   __syncthreads();
+  if (HA_STAMP_CODE && stp)
+    __hip_atomic_store(stp + 11, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (tid >= 64) return true;
-  int ww = 0;
-  for (int w = 1; w < NT / 64; w++) {
-    const int op = r_p[w];
-    if (op >= 0 && (bp < 0 || key_before(r_f[w], r_s[w], bf, bs))) { bf = r_f[w]; bs = r_s[w]; bp = op; ww = w; }
+  // the block minimum: wave w's winner on lane w of wave 0 (one LDS read per lane, all at once), reduced
+  // within the row by the same DPP steps -- not a serial pass over the NT/64 winners (2.9 us for 12 of
+  // them in the r04zk stamps)
+  static_assert(NT / 64 <= 16, "the wave winners fit one row");
+  double cf = __builtin_inf();
+  long long cs = 0x7fffffffffffffffLL;
+  int cp = -1;
+  if (lane < NT / 64) {
+    cp = r_p[lane];
+    cf = r_f[lane];
+    cs = r_s[lane];
   }
+  const int mine = cp;
+  key_min_dpp<0xB1>(cf, cs, cp);
+  key_min_dpp<0x4E>(cf, cs, cp);
+  key_min_dpp<0x141>(cf, cs, cp);
+  key_min_dpp<0x140>(cf, cs, cp);
+  bp = __builtin_amdgcn_readlane(cp, 0);
+  const int ww = __builtin_ctzll(__ballot(lane < NT / 64 && mine == bp));
   const int id = r_id[ww];
   const double gw = r_pay[ww][0];
   const long long iw = __double_as_longlong(r_pay[ww][1]);
@@ -1569,7 +1590,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   const int n_open = s_nopen;
   long long iw = 0;
   bool go;
-  go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, false, &iw);
+  go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, false, &iw, stp);
   BSTAMP(8);
   BookRec br;
   br.v[RC_GO] = go;
@@ -1634,7 +1655,7 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
 #ifndef HA_WPE_TAIL
 #define HA_WPE_TAIL 1
 #endif
-constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 10;  // [6..9]: bookkeeping phases
+constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 12;  // [6..11]: bookkeeping phases
 template <int HWt, int NBGt>
 __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == 4 ? HA_WPE_FULL : HA_WPE_TAIL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
   __shared__ int role;

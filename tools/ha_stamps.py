@@ -51,6 +51,8 @@ def main(fn):
             d = lambda a, b_: np.median((e[bk, b_] - e[bk, a]) * tick)
             ph = (f" | book phases: role {d(1, 2):.1f} loads+dup {d(2, 6):.1f} FindNewNode {d(6, 7):.1f} "
                   f"pop {d(7, 8):.1f} record {d(8, 3):.1f}; n_open {int(np.median(e[bk, 9]))}")
+            if ns >= 12:
+                ph += f" | pop: loads {d(7, 10):.1f} reduce+barrier {d(10, 11):.1f} final+stores {d(11, 8):.1f}"
         print(f"{k * every:5d} {int(done.sum()):6d} {span:7.1f} {med['rs']:8.1f} {med['nb']:8.1f} {med['book']:7.1f} "
               f"{med['fin']:7.1f} | {crit['rs']:.1f} {crit['nb']:.1f} {crit['book']:.1f} {crit['fin']:.1f}{ph}")
 
