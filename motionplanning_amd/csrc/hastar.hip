@@ -511,9 +511,14 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   HTIME(12);
   double bc = __builtin_inf();
   int bi = 1 << 20;
+  // CMD with one word per wave (the tail shape): that word's commands are kept from its one evaluation;
+  // with more (the full-width shape) carrying every lane's best commands through the loop set the kernel's
+  // register peak, so the winning word is evaluated again below
+  constexpr bool KEEP = CMD && WPW == 1;
+  Cmd cb;
 #pragma unroll 1
   for (int w = WPW * wave + 1; w <= WPW * wave + WPW; w++) {
-    const double cost = rs_word(w, R, nullptr);
+    const double cost = rs_word(w, R, KEEP ? &cb : nullptr);
     const int id = 4 * (w - 1) + var;
     if (rs_before(cost, id, bc, bi)) {
       bc = cost;
@@ -544,8 +549,7 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   // winning variant stores them with allpath's gear/steer flips (timeflip: gear, reflect: steer,
   // reverse: both), as rs_commands does
   if (CMD && wave == (ix / 4) / WPW) {  // wave-uniform
-    Cmd cb;
-    rs_word(ix / 4 + 1, R, &cb);
+    if (!KEEP) rs_word(ix / 4 + 1, R, &cb);
     const int n = v < __builtin_inf() ? cb.n : 0;
 #pragma unroll
     for (int r = 0; r < 5; r++) {
@@ -570,7 +574,9 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
 // One search iteration's device work for the block (role by blockIdx: RS_connected or a
 // 16-neighbour group).  Returns false (block-uniformly) when the block has nothing to do.
 template <int HWt, int NBGt>
-__device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) {
+__device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, unsigned long long* hstp = nullptr) {
+// (diagnostics, -DHA_STAMP_CODE=1) phase stamps of the block's thread 0 into ha_step_kernel's slots 12..
+#define HSTAMP(i) if (HA_STAMP_CODE && hstp) __hip_atomic_store(hstp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
   constexpr int HT = 64 * HWt, NBG = NBGt;
   __shared__ double wp[MAXW * 10];
   __shared__ double wpre[MAXW * 24];
@@ -645,6 +651,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
   }
   HMARK(6);
   HTIME(1);
+  HSTAMP(12);
   __syncthreads();
   const int j = lane >> 2;
   // collision sweep: (neighbour, pose) pairs of this group, or the RS path's poses; the tail shape
@@ -679,7 +686,9 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     double ns[3];
     change_basis(node, goal, P.minR, ns);
     HTIME(2);
+    HSTAMP(12);
     cb = rs_best_split<true, HWt>(ns, tid, &best, red_c, red_i, cmd);
+    HSTAMP(13);
     HTIME(3);
     // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment -- per segment the
     // heading recurrence ψ_{t+1} = ψ_t + (st*v)*dt, the per-step increments, then the x and y
@@ -776,6 +785,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       __syncthreads();
     }
     HTIME(8);
+    HSTAMP(14);
     if (tid == 0) path_s[2] = node[2];
     __syncthreads();
     const int n = nst + 1;
@@ -796,9 +806,11 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
     if (hit >= 0) gd = A.dg[(size_t)s * A.C + hit];  // loaded now, used after the sweep
     sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
     HTIME(4);
+    HSTAMP(13);
     if (tid < nk) g_need[tid] = !A.dnid || !(hit >= 0 && !(A.cur_g[s] + P.expand_time < gd));
     __syncthreads();
     HTIME(5);
+    HSTAMP(14);
     int any = 0;
     for (int q = 0; q < nk; q++) any |= (g_ix[q] != 0) & g_free[q] & g_need[q];
     if (any) {  // block-uniform
@@ -806,11 +818,13 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A) 
       change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
       HTIME(2);
       cb = rs_best_split<false, HWt>(ns, tid, &best, red_c, red_i);
+      HSTAMP(15);
       HTIME(3);
     }
   }
   HMARK(20);
   HTIME(10);
+  HSTAMP(16);
   __syncthreads();
   if (rs) {
     if (tid == 0) {
@@ -1655,7 +1669,7 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
 #ifndef HA_WPE_TAIL
 #define HA_WPE_TAIL 1
 #endif
-constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 12;  // [6..11]: bookkeeping phases
+constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 17;  // [6..11]: bookkeeping phases; [12..16]: block body phases
 template <int HWt, int NBGt>
 __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == 4 ? HA_WPE_FULL : HA_WPE_TAIL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
   __shared__ int role;
@@ -1666,7 +1680,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int per = 1 + (P.n_prim + NBGt - 1) / NBGt;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
-  if (!ha_iter_body<HWt, NBGt>(P, A)) return;  // block-uniform: no work for this block (not counted)
+  if (!ha_iter_body<HWt, NBGt>(P, A, stp)) return;  // block-uniform: no work for this block (not counted)
   const int s = A.scene_of ? A.scene_of[slot] : slot;
   ha_stores_done();  // this thread's records acknowledged before the block's ticket
   __syncthreads();

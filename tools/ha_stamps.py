@@ -53,6 +53,14 @@ def main(fn):
                   f"pop {d(7, 8):.1f} record {d(8, 3):.1f}; n_open {int(np.median(e[bk, 9]))}")
             if ns >= 12:
                 ph += f" | pop: loads {d(7, 10):.1f} reduce+barrier {d(10, 11):.1f} final+stores {d(11, 8):.1f}"
+        if ns >= 17:  # block body phases from the block's entry (medians): nb 12 encode, 13 sweep, 14 need
+            # barrier, 15 search, 16 end; RS 12 search start, 13 search end, 14 createActPath, 16 end
+            nbb = np.nonzero(done & (item > 0))[0]
+            rsb = np.nonzero(done & (item == 0))[0]
+            md = lambda ix, j: np.median((e[ix, j] - e[ix, 0]) * tick) if len(ix) and (e[ix, j] > 0).all() else float("nan")
+            ph += (f" | nb: encode {md(nbb, 12):.1f} sweep {md(nbb, 13):.1f} need {md(nbb, 14):.1f} "
+                   f"end {md(nbb, 16):.1f}; rs: search {md(rsb, 12):.1f}-{md(rsb, 13):.1f} path {md(rsb, 14):.1f} "
+                   f"end {md(rsb, 16):.1f}")
         print(f"{k * every:5d} {int(done.sum()):6d} {span:7.1f} {med['rs']:8.1f} {med['nb']:8.1f} {med['book']:7.1f} "
               f"{med['fin']:7.1f} | {crit['rs']:.1f} {crit['nb']:.1f} {crit['book']:.1f} {crit['fin']:.1f}{ph}")
 
