@@ -308,7 +308,7 @@ __device__ __forceinline__ int sat_pre(const double* pre, const double* other) {
   return 0;
 }
 
-// Wall table row: corners (10) + wall-side SAT table (24) + [center x, center y, far²] (3).
+// Wall table row: corners (10) + wall-side SAT table (24) + [center x, center y, far²] (3) + cull bounds (3).
 // far² = (√2 (r_vehicle + r_wall) + 1e-6)², r = a rectangle's circumradius.  When the vehicle's
 // centre is farther than that from a wall's centre, ConvexCollision(wall, vehicle) is false for
 // certain: each rectangle has an edge normal within 45° of the centre-to-centre direction d, along
@@ -317,29 +317,80 @@ __device__ __forceinline__ int sat_pre(const double* pre, const double* other) {
 // against rounding errors below 1e-12 m at these coordinates.  Such walls skip their SAT pair
 // (the booleans, hence every planner decision, are unchanged; tests/test_oracle_hastar.py checks
 // the bound against the oracle's SAT).
-constexpr int WT = 37;
+// round 4: + the per-direction cull bounds (3) of wall_cull, so a row is 40 doubles
+constexpr int WT = 40;
 __device__ __forceinline__ double wall_far2(const HaDev& P, const double* wl) {
   const double rv = mpj_sqrt(P.L2 * P.L2 + P.W2 * P.W2), rw = mpj_sqrt(wl[3] * wl[3] + wl[4] * wl[4]);
   const double f = 1.4142135623730951 * (rv + rw) * (1 + 1e-12) + 1e-6;
   return f * f;
 }
 
-// vehicle pose q=[x,y,ψ] (rear axle) against all walls (corners wp, SAT tables wpre and centres /
-// far² wc in LDS); 1 = free
+// Per-direction SAT cull, one wall (corners wp, SAT table pre, centre c) -> cl[3]:
+//  cl[0], cl[1] = (r_vehicle + 1e-6)·|n_e|·(1 + 1e-12) for the wall's edges e = 0, 1 (n_e = the edge
+//    normal of the wall-side SAT table): when the vehicle centre's projection on n_e lies more than
+//    cl[e] beyond the wall's own projection interval [mnb, mxb], the vehicle's circumcircle -- hence
+//    every vehicle corner -- is past the wall along that axis by >= 1e-6·|n_e|, so
+//    SeparatingAxisTheorem(wall, vehicle) returns true (errors of the computed projections are
+//    ~1e-13·|n_e| at these coordinates);
+//  cl[2] = r_wall·(1 + 1e-12) + 1e-6 (r_wall = the largest corner-to-centre distance): when the wall
+//    centre lies farther than L2 + cl[2] along the vehicle's heading or W2 + cl[2] across it, every wall
+//    corner is past the vehicle's edge along that edge normal, so SeparatingAxisTheorem(vehicle, wall)
+//    returns true.
+// The booleans are the reference's either way (tests/test_oracle_hastar.py checks both bounds against
+// the oracle's SAT); the cull only skips SAT calls whose result is certain.
+__device__ __forceinline__ void wall_cull(const HaDev& P, const double* wp, const double* pre, const double* c,
+                                          double* cl) {
+  const double rv = mpj_sqrt(P.L2 * P.L2 + P.W2 * P.W2);
+  for (int e = 0; e < 2; e++) {
+    const double nx = pre[6 * e + 2], ny = pre[6 * e + 3];
+    cl[e] = (rv + 1e-6) * mpj_sqrt(nx * nx + ny * ny) * (1 + 1e-12);
+  }
+  double r2 = 0;
+  for (int j = 0; j < 4; j++) {
+    const double dx = wp[2 * j] - c[0], dy = wp[2 * j + 1] - c[1];
+    r2 = fmax(r2, dx * dx + dy * dy);
+  }
+  cl[2] = mpj_sqrt(r2) * (1 + 1e-12) + 1e-6;
+}
+// 1: SAT(wall, vehicle) is certainly true for a vehicle centred at (x, y) (wall_cull's cl[0..1])
+__device__ __forceinline__ int cull_wall_side(const double* pre, const double* cl, double x, double y) {
+  const double d0 = (x - pre[0]) * pre[2] + (y - pre[1]) * pre[3];
+  const double d1 = (x - pre[6]) * pre[8] + (y - pre[7]) * pre[9];
+  return (d0 - cl[0] > pre[5]) | (d0 + cl[0] < pre[4]) | (d1 - cl[1] > pre[11]) | (d1 + cl[1] < pre[10]);
+}
+// 1: SAT(vehicle, wall) is certainly true; (dx, dy) = vehicle centre - wall centre, (cy, sy) the
+// vehicle rectangle's heading (wall_cull's cl[2])
+__device__ __forceinline__ int cull_vehicle_side(const HaDev& P, const double* cl, double dx, double dy, double cy,
+                                                 double sy) {
+  const double u = dx * cy + dy * sy, v = dy * cy - dx * sy;
+  return (__builtin_fabs(u) > P.L2 * (1 + 1e-12) + cl[2]) | (__builtin_fabs(v) > P.W2 * (1 + 1e-12) + cl[2]);
+}
+
+// vehicle pose q=[x,y,ψ] (rear axle) against all walls (corners wp, SAT tables wpre, centres /
+// far² wc and cull bounds wcl in LDS); 1 = free
 __device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const double* wp, const double* wpre,
-                                         const double* wc, int nw) {
+                                         const double* wc, const double* wcl, int nw) {
   double sq, cq;
   mpj_sincos_bl(q[2], &sq, &cq);
   const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
   const double yaw = mpj_modpi_bl(q[2]);
   double sy = sq, cy = cq;
   if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);  // |ψ| > π: the wrapped yaw's own sin/cos
-  double vp[10];
-  rect_pts(x, y, cy, sy, P.L2, P.W2, vp);
+  // the SAT calls whose result is not certain (bit 2i: SAT(wall i, vehicle), bit 2i+1: SAT(vehicle,
+  // wall i)), collected before the rectangle is built so its corners are live only where needed
+  unsigned need = 0;
   for (int i = 0; i < nw; i++) {
     const double dx = x - wc[3 * i], dy = y - wc[3 * i + 1];
     if (dx * dx + dy * dy > wc[3 * i + 2]) continue;  // far from this wall: separated for certain
-    if (!(sat_pre(wpre + 24 * i, vp) && sat(vp, wp + 10 * i))) return 0;
+    need |= (unsigned)!cull_wall_side(wpre + 24 * i, wcl + 3 * i, x, y) << (2 * i);
+    need |= (unsigned)!cull_vehicle_side(P, wcl + 3 * i, dx, dy, cy, sy) << (2 * i + 1);
+  }
+  if (!need) return 1;
+  double vp[10];
+  rect_pts(x, y, cy, sy, P.L2, P.W2, vp);
+  for (int i = 0; i < nw; i++) {
+    if (((need >> (2 * i)) & 1) && !sat_pre(wpre + 24 * i, vp)) return 0;
+    if (((need >> (2 * i)) & 2) && !sat(vp, wp + 10 * i)) return 0;
   }
   return 1;
 }
@@ -347,15 +398,17 @@ __device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const 
 // one (wall, direction) term of pose_free: d = 0 SAT(wall, vehicle), d = 1 SAT(vehicle, wall); the pose
 // is free iff every term of every wall is 1 (ConvexCollision = SAT(wall, veh) && SAT(veh, wall))
 __device__ __forceinline__ int pose_free_part(const HaDev& P, const double* q, const double* wp, const double* wpre,
-                                              const double* wc, int w, int d) {
+                                              const double* wc, const double* wcl, int w, int d) {
   double sq, cq;
   mpj_sincos_bl(q[2], &sq, &cq);
   const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
   const double fx = x - wc[3 * w], fy = y - wc[3 * w + 1];
   if (fx * fx + fy * fy > wc[3 * w + 2]) return 1;  // far from this wall: separated for certain
+  if (d == 0 && cull_wall_side(wpre + 24 * w, wcl + 3 * w, x, y)) return 1;
   const double yaw = mpj_modpi_bl(q[2]);
   double sy = sq, cy = cq;
   if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);
+  if (d == 1 && cull_vehicle_side(P, wcl + 3 * w, fx, fy, cy, sy)) return 1;
   double vp[10];
   rect_pts(x, y, cy, sy, P.L2, P.W2, vp);
   return d == 0 ? sat_pre(wpre + 24 * w, vp) : sat(vp, wp + 10 * w);
@@ -581,6 +634,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   __shared__ double wp[MAXW * 10];
   __shared__ double wpre[MAXW * 24];
   __shared__ double wc[MAXW * 3];
+  __shared__ double wcl[MAXW * 3];
   __shared__ double cmd[15];
   __shared__ double psi_s[MAXPATH], ix_s[MAXPATH], iy_s[MAXPATH];
   __shared__ double path_s[MAXPATH * 3];
@@ -619,7 +673,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       const int w = i / WT, e = i - WT * w;
       if (e < 10) wp[10 * w + e] = v;
       else if (e < 34) wpre[24 * w + e - 10] = v;
-      else wc[3 * w + e - 34] = v;
+      else if (e < 37) wc[3 * w + e - 34] = v;
+      else wcl[3 * w + e - 37] = v;
     }
   } else {
     for (int i = tid; i < nw; i += HT) {
@@ -629,6 +684,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       wc[3 * i] = wl[0];
       wc[3 * i + 1] = wl[1];
       wc[3 * i + 2] = wall_far2(P, wl);
+      wall_cull(P, wp + 10 * i, wpre + 24 * i, wl, wcl + 3 * i);
     }
   }
   if (tid < NBG) g_free[tid] = 1;
@@ -675,7 +731,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       } else {
         transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
       }
-      const int fr = SPLIT ? pose_free_part(P, q, wp, wpre, wc, part >> 1, part & 1) : pose_free(P, q, wp, wpre, wc, nw);
+      const int fr = SPLIT ? pose_free_part(P, q, wp, wpre, wc, wcl, part >> 1, part & 1) : pose_free(P, q, wp, wpre, wc, wcl, nw);
       if (!fr) g_free[jn] = 0;  // every writer stores 0
     }
   };
@@ -931,7 +987,8 @@ int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
   return MP_OK;
 }
 
-// Block2Pts + the wall-side SAT tables (pose independent) + centre / far² once per plan: [B][nw][WT]
+// Block2Pts + the wall-side SAT tables (pose independent) + centre / far² + the cull bounds once per plan:
+// [B][nw][WT]
 __global__ __launch_bounds__(64) void ha_wall_kernel(HaDev P, int B, const double* walls, double* wtab) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= B * P.n_walls) return;
@@ -942,6 +999,7 @@ __global__ __launch_bounds__(64) void ha_wall_kernel(HaDev P, int B, const doubl
   o[34] = wl[0];
   o[35] = wl[1];
   o[36] = wall_far2(P, wl);
+  wall_cull(P, o, o + 10, wl, o + 37);
 }
 
 // ------------------------------------------------ device-resident search state

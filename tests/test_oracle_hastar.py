@@ -132,3 +132,78 @@ def test_far_wall_skip_bound():
             assert oracle.ha_convex_free(_rect(w), _rect([cx, cy, psi, L2, W2])), (w, cx, cy, psi)
             n += 1
     assert n == len(walls) * 150
+
+
+def _sat(base, other):
+    """SeparatingAxisTheorem one way (CollisionDetection/src/utils.jl:37-62), as or_hastar.c's sat()."""
+    for e in range(4):
+        bx, by = base[e]
+        nx, ny = -(base[e + 1][1] - by), base[e + 1][0] - bx
+        db = [(base[j][0] - bx) * nx + (base[j][1] - by) * ny for j in range(4)]
+        dq = [(other[j][0] - bx) * nx + (other[j][1] - by) * ny for j in range(4)]
+        if max(dq) <= min(db) or max(db) <= min(dq):
+            return True
+    return False
+
+
+def test_per_direction_sat_cull():
+    """hastar.hip's wall_cull / cull_wall_side / cull_vehicle_side (round 4) skip one SAT direction when
+    its result is certain: the vehicle's circumcircle beyond the wall's projection on a wall edge normal
+    (SAT(wall, vehicle) true), or the wall's circumcircle beyond the vehicle's half length / width along
+    the vehicle's axes (SAT(vehicle, wall) true).  Same formulas on random walls and poses concentrated
+    around the bounds; every pose the cull certifies must have that SAT direction true, and the numpy
+    SAT pair must agree with the oracle's ConvexCollision."""
+    r = np.random.default_rng(23)
+    L2, W2 = 1.5, 1.0
+    rv = math.hypot(L2, W2)
+    walls = [list(w) for w in ha.PERPENDICULAR["walls"] + ha.PARALLEL["walls"]]
+    walls += [[r.uniform(-5, 10), r.uniform(-2, 10), r.uniform(-math.pi, math.pi), r.uniform(0.2, 4), r.uniform(0.2, 2)]
+              for _ in range(30)]
+    n0 = n1 = 0
+    for w in walls:
+        wp = _rect(w)
+        pre = []
+        for e in range(2):
+            bx, by = wp[e]
+            nx, ny = -(wp[e + 1][1] - by), wp[e + 1][0] - bx
+            db = [(wp[j][0] - bx) * nx + (wp[j][1] - by) * ny for j in range(4)]
+            pre.append((bx, by, nx, ny, min(db), max(db), (rv + 1e-6) * math.sqrt(nx * nx + ny * ny) * (1 + 1e-12)))
+        rw = math.sqrt(max((wp[j][0] - w[0]) ** 2 + (wp[j][1] - w[1]) ** 2 for j in range(4))) * (1 + 1e-12) + 1e-6
+        reach = rv + math.hypot(w[3], w[4])
+        for _ in range(300):
+            ang, psi = r.uniform(-math.pi, math.pi), r.uniform(-math.pi, math.pi)
+            d = reach * r.uniform(0.3, 1.5)
+            x, y = w[0] + d * math.cos(ang), w[1] + d * math.sin(ang)
+            cy, sy = math.cos(psi), math.sin(psi)
+            vp = _rect([x, y, psi, L2, W2])
+            c0 = any(((x - bx) * nx + (y - by) * ny) - cl > mx or ((x - bx) * nx + (y - by) * ny) + cl < mn
+                     for bx, by, nx, ny, mn, mx, cl in pre)
+            dx, dy = x - w[0], y - w[1]
+            u, v = dx * cy + dy * sy, dy * cy - dx * sy
+            c1 = abs(u) > L2 * (1 + 1e-12) + rw or abs(v) > W2 * (1 + 1e-12) + rw
+            s0, s1 = _sat(wp, vp), _sat(vp, wp)
+            assert (s0 and s1) == oracle.ha_convex_free(wp, vp)
+            if c0:
+                assert s0, (w, x, y, psi)
+                n0 += 1
+            if c1:
+                assert s1, (w, x, y, psi)
+                n1 += 1
+        for _ in range(100):  # poses right at the bounds (within 1e-7 m of the certified region's edge)
+            psi = r.uniform(-math.pi, math.pi)
+            cy, sy = math.cos(psi), math.sin(psi)
+            lat, sgn = r.uniform(-1, 1), r.choice([-1.0, 1.0])
+            ext = L2 if r.random() < 0.5 else W2
+            along = sgn * (ext * (1 + 1e-12) + rw + r.uniform(1e-12, 1e-7))
+            u, v = (along, lat) if ext == L2 else (lat, along)
+            # wall centre = vehicle centre + u·(cy, sy) + v·(-sy, cy)
+            x, y = w[0] - (u * cy - v * sy), w[1] - (u * sy + v * cy)
+            assert _sat(_rect([x, y, psi, L2, W2]), wp), (w, x, y, psi)
+            bx, by, nx, ny, mn, mx, cl = pre[r.integers(2)]
+            nn = math.hypot(nx, ny)
+            t = (mx + cl + r.uniform(1e-12, 1e-7) * nn) / nn if r.random() < 0.5 else (mn - cl - r.uniform(1e-12, 1e-7) * nn) / nn
+            x, y = bx + t * nx / nn + lat * ny / nn, by + t * ny / nn - lat * nx / nn
+            if ((x - bx) * nx + (y - by) * ny) - cl > mx or ((x - bx) * nx + (y - by) * ny) + cl < mn:
+                assert _sat(wp, _rect([x, y, psi, L2, W2])), (w, x, y, psi)
+                n0 += 1
+    assert n0 > 1000 and n1 > 1000  # both bounds exercised
