@@ -352,11 +352,24 @@ __device__ __forceinline__ void wall_cull(const HaDev& P, const double* wp, cons
   }
   cl[2] = mpj_sqrt(r2) * (1 + 1e-12) + 1e-6;
 }
-// 1: SAT(wall, vehicle) is certainly true for a vehicle centred at (x, y) (wall_cull's cl[0..1])
-__device__ __forceinline__ int cull_wall_side(const double* pre, const double* cl, double x, double y) {
+// (A/B) -DHA_SAT_OVERLAP=1 enables class 2 below (proved in the oracle test; not yet measured on the GPU)
+#ifndef HA_SAT_OVERLAP
+#define HA_SAT_OVERLAP 0
+#endif
+// Wall-side class of a vehicle centred at (x, y), from its projections on the wall's edge normals 0, 1:
+//  1: SAT(wall, vehicle) is certainly true (wall_cull's cl[0..1]);
+//  2: the centre lies inside the wall, at least 1e-5 of the wall's extent from each side along both
+//     normals: the centre is then interior to both rectangles by far more than any rounding error, so
+//     on every axis the two projections overlap and both SeparatingAxisTheorem calls return false --
+//     the pose collides (tests/test_oracle_hastar.py);
+//  0: neither is certain.
+__device__ __forceinline__ int wall_side_class(const double* pre, const double* cl, double x, double y) {
   const double d0 = (x - pre[0]) * pre[2] + (y - pre[1]) * pre[3];
   const double d1 = (x - pre[6]) * pre[8] + (y - pre[7]) * pre[9];
-  return (d0 - cl[0] > pre[5]) | (d0 + cl[0] < pre[4]) | (d1 - cl[1] > pre[11]) | (d1 + cl[1] < pre[10]);
+  if ((d0 - cl[0] > pre[5]) | (d0 + cl[0] < pre[4]) | (d1 - cl[1] > pre[11]) | (d1 + cl[1] < pre[10])) return 1;
+  if (!HA_SAT_OVERLAP) return 0;
+  const double m0 = (pre[5] - pre[4]) * 1e-5, m1 = (pre[11] - pre[10]) * 1e-5;
+  return ((d0 > pre[4] + m0) & (d0 < pre[5] - m0) & (d1 > pre[10] + m1) & (d1 < pre[11] - m1)) ? 2 : 0;
 }
 // 1: SAT(vehicle, wall) is certainly true; (dx, dy) = vehicle centre - wall centre, (cy, sy) the
 // vehicle rectangle's heading (wall_cull's cl[2])
@@ -382,7 +395,11 @@ __device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const 
   for (int i = 0; i < nw; i++) {
     const double dx = x - wc[3 * i], dy = y - wc[3 * i + 1];
     if (dx * dx + dy * dy > wc[3 * i + 2]) continue;  // far from this wall: separated for certain
-    need |= (unsigned)!cull_wall_side(wpre + 24 * i, wcl + 3 * i, x, y) << (2 * i);
+    const int ws = wall_side_class(wpre + 24 * i, wcl + 3 * i, x, y);
+#if HA_SAT_OVERLAP
+    if (ws == 2) return 0;  // centre inside the wall: collides for certain
+#endif
+    need |= (unsigned)(ws != 1) << (2 * i);
     need |= (unsigned)!cull_vehicle_side(P, wcl + 3 * i, dx, dy, cy, sy) << (2 * i + 1);
   }
   if (!need) return 1;
@@ -404,7 +421,13 @@ __device__ __forceinline__ int pose_free_part(const HaDev& P, const double* q, c
   const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
   const double fx = x - wc[3 * w], fy = y - wc[3 * w + 1];
   if (fx * fx + fy * fy > wc[3 * w + 2]) return 1;  // far from this wall: separated for certain
-  if (d == 0 && cull_wall_side(wpre + 24 * w, wcl + 3 * w, x, y)) return 1;
+#if HA_SAT_OVERLAP
+  const int ws = wall_side_class(wpre + 24 * w, wcl + 3 * w, x, y);
+  if (ws == 2) return 0;  // centre inside the wall: both terms are false
+  if (d == 0 && ws == 1) return 1;
+#else
+  if (d == 0 && wall_side_class(wpre + 24 * w, wcl + 3 * w, x, y) == 1) return 1;
+#endif
   const double yaw = mpj_modpi_bl(q[2]);
   double sy = sq, cy = cq;
   if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);

@@ -159,7 +159,7 @@ def test_per_direction_sat_cull():
     walls = [list(w) for w in ha.PERPENDICULAR["walls"] + ha.PARALLEL["walls"]]
     walls += [[r.uniform(-5, 10), r.uniform(-2, 10), r.uniform(-math.pi, math.pi), r.uniform(0.2, 4), r.uniform(0.2, 2)]
               for _ in range(30)]
-    n0 = n1 = 0
+    n0 = n1 = n2 = 0
     for w in walls:
         wp = _rect(w)
         pre = []
@@ -206,4 +206,21 @@ def test_per_direction_sat_cull():
             if ((x - bx) * nx + (y - by) * ny) - cl > mx or ((x - bx) * nx + (y - by) * ny) + cl < mn:
                 assert _sat(wp, _rect([x, y, psi, L2, W2])), (w, x, y, psi)
                 n0 += 1
-    assert n0 > 1000 and n1 > 1000  # both bounds exercised
+        # wall_side_class 2: the vehicle centre inside the wall by >= 1e-5 of its extent along both
+        # normals -> both SAT directions false (the pose collides); centres drawn up to the class's edge
+        (bx0, by0, nx0, ny0, mn0, mx0, _), (bx1, by1, nx1, ny1, mn1, mx1, _) = pre
+        m0, m1 = (mx0 - mn0) * 1e-5, (mx1 - mn1) * 1e-5
+        for _ in range(100):
+            psi = r.uniform(-math.pi, math.pi)
+            a, b = r.uniform(0, 1), r.uniform(0, 1)
+            if r.random() < 0.5:
+                a = r.choice([1e-5 + 1e-9, 1 - 1e-5 - 1e-9])
+            x = wp[1][0] + a * (wp[2][0] - wp[1][0]) + b * (wp[0][0] - wp[1][0])
+            y = wp[1][1] + a * (wp[2][1] - wp[1][1]) + b * (wp[0][1] - wp[1][1])
+            d0 = (x - bx0) * nx0 + (y - by0) * ny0
+            d1 = (x - bx1) * nx1 + (y - by1) * ny1
+            if mn0 + m0 < d0 < mx0 - m0 and mn1 + m1 < d1 < mx1 - m1:
+                vp = _rect([x, y, psi, L2, W2])
+                assert not _sat(wp, vp) and not _sat(vp, wp) and not oracle.ha_convex_free(wp, vp), (w, x, y, psi)
+                n2 += 1
+    assert n0 > 1000 and n1 > 1000 and n2 > 1000  # every bound exercised
