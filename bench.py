@@ -262,6 +262,12 @@ def main():
             "kernel": "mppi_plan_kernel", "kernel_ms": kern_ms, "algorithmic_bytes": nbytes,
         },
         "valid": ok,
+        # what ran before the timed region (round-4+ headlines are timed on a warm GPU, earlier
+        # rounds' after the warmup steps only), and what the roofline's top-level fields price
+        "order": ("extras GPU legs (iLQR, Hybrid A*, tracker, closed loop), then W warmup + K timed headline "
+                  "steps, then CPU baselines") if not a.no_extras else "W warmup + K timed headline steps",
+        "roofline_note": "top-level roofline fields = the bound that binds (fp64 VALU issue when the PMC "
+                         "traffic file carries SQ_INSTS_VALU, else HBM); the HBM fraction is under roofline.hbm",
     }
     if a.share_device and world > 1:
         out["rehearsal"] = (f"--share-device: {world} ranks on one GPU over gloo; value is that one GPU's "
@@ -500,6 +506,7 @@ def hastar_shard_projection(ctx, t_all, world=8):
     from motionplanning_amd import hybrid_astar as ha
 
     out = {"workload": f"scenario_batch(256, seed=4) split {world} ways, each shard planned alone on one GPU",
+           "kind": "projection from one GPU (not a multi-GPU measurement)",
            "t256_ms": t_all * 1e3}
     for name, strided in (("contiguous", False), ("strided", True)):
         hs = ha.scenario_batch(256, seed=4)

@@ -336,6 +336,15 @@ int mp_ha_rs_connect(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double
                      const double* goal, const double* walls, uint8_t* ok, double* path,
                      int32_t* path_len);
 
+/* Whether the collision sweeps of mp_ha_expand / mp_ha_rs_connect / mp_ha_plan use their SAT culls
+ * (certain-result SeparatingAxisTheorem calls skipped, CollisionDetection/src/utils.jl:37-74) for these
+ * inputs: *active = 1 when every coordinate and length (walls[B][n_walls][5] centres + half extents,
+ * stbound, a[B][3] and b[B][3] x/y -- start or node, goal -- minR, vehicle and primitive sizes) is
+ * <= 1e6 m, the range the culls' rounding margin is proven for; 0 otherwise (every SAT call runs).
+ * Either way the booleans are the reference's.  No device work. */
+int mp_ha_sat_cull_active(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* walls, const double* a,
+                          const double* b, int32_t* active);
+
 /* allpath (ReedsSheppsCurves/src/ReedsSheppsUtils.jl:468-511) for B normalised
  * states; out: cost[B][48] (Inf where infeasible), cmds[B][48][5][3], best[B]. */
 int mp_ha_allpath(mp_ctx* ctx, int32_t B, const double* norm_states, double* cost,

@@ -572,6 +572,16 @@ function ha_rs_connect(p::HaParams, node::Matrix{Float64}, goal::Matrix{Float64}
     return ok, path, len
 end
 
+"""Whether the library's collision sweeps use their SAT culls for these inputs (coordinates <= 1e6 m)."""
+function ha_sat_cull_active(p::HaParams, walls::Array{Float64,3}, a::Matrix{Float64}, b::Matrix{Float64})
+    B = size(a, 2); on = Ref{Int32}(0)
+    c = ctx()
+    check(GC.@preserve walls a b ccall((:mp_ha_sat_cull_active, libmpgpu), Cint,
+        (Ptr{Cvoid}, Ref{HaParams}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{Int32}),
+        c, p, B, walls, a, b, on), c)
+    return on[] == 1
+end
+
 """allpath (ReedsSheppsUtils.jl:468-511) for normalised states (3, B): best (1-based), cost (48, B),
 cmds (3, 5, 48, B) (rows [distance, gear, steer] of each command)."""
 function ha_allpath(ns::Matrix{Float64})

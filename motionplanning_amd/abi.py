@@ -175,6 +175,7 @@ SIGNATURES = {
     "mp_ha_expand": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I] + [_V] * 7),
     "mp_ha_rs_connect": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I] + [_V] * 6),
     "mp_ha_allpath": (ctypes.c_int, [_V, _I, _V, _V, _V, _V]),
+    "mp_ha_sat_cull_active": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I, _V, _V, _V, _V]),
     "mp_ha_plan": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I] + [_V] * 11),
     "mp_ha_retrieve_path": (ctypes.c_int, [_V, _I, _V, _V, _V, _I] + [_V] * 8),
     "mp_ha_track": (ctypes.c_int, [_V, ctypes.POINTER(TrackParams), _I, _V, _V, _V, _I] + [_V] * 6 + [_I]),

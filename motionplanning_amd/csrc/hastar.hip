@@ -61,6 +61,7 @@ struct HaDev {
   double res[3];
   double sb[6];
   int n_walls, n_prim, n_col;
+  int cull;  // the SAT culls' rounding margins are proven for this call's coordinates (ha_cull_ok); else full SAT
 };
 
 // ------------------------------------------------------------ Reeds–Shepp
@@ -319,7 +320,19 @@ __device__ __forceinline__ int sat_pre(const double* pre, const double* other) {
 // the bound against the oracle's SAT).
 // round 4: + the per-direction cull bounds (3) of wall_cull, so a row is 40 doubles
 constexpr int WT = 40;
+// The culls' margin argument (1e-6 m, and 1e-6·|n| along an edge normal n) against the rounding of the
+// computed projections: a projection fl((p - b)·n) of a computed corner p (|p|, |b| <= X, corner rounding
+// <= 3ε(X + L)) is within ~15ε(X + L)·|n| of the exact one.  ha_cull_ok enables the culls only when every
+// input coordinate and length of the call (wall centres + extents, stbound, start, goal, minR, vehicle and
+// primitive sizes) is <= HA_CULL_MAX = 1e6 m; every swept pose then lies within ~10 HA_CULL_MAX of the
+// origin (a neighbour within expand_time of an in-bounds node, a Reeds-Shepp path within its length of
+// the popped node), so the rounding is <= 15·1.1e-16·1e7·|n| = 1.7e-8·|n|, 60x below the margin.  Beyond
+// it the culls are off (far² and the cull bounds +inf) and every SAT call runs, as the reference does.
+constexpr double HA_CULL_MAX = 1e6;
+// MAXW walls at 2 bits each in pose_free's 32-bit `need` mask
+static_assert(2 * MAXW <= 32, "pose_free's need mask holds 2 bits per wall");
 __device__ __forceinline__ double wall_far2(const HaDev& P, const double* wl) {
+  if (!P.cull) return __builtin_inf();  // never "far": every wall's SAT pair runs
   const double rv = mpj_sqrt(P.L2 * P.L2 + P.W2 * P.W2), rw = mpj_sqrt(wl[3] * wl[3] + wl[4] * wl[4]);
   const double f = 1.4142135623730951 * (rv + rw) * (1 + 1e-12) + 1e-6;
   return f * f;
@@ -340,6 +353,10 @@ __device__ __forceinline__ double wall_far2(const HaDev& P, const double* wl) {
 // the oracle's SAT); the cull only skips SAT calls whose result is certain.
 __device__ __forceinline__ void wall_cull(const HaDev& P, const double* wp, const double* pre, const double* c,
                                           double* cl) {
+  if (!P.cull) {  // no bound is certain: every SAT call runs
+    cl[0] = cl[1] = cl[2] = __builtin_inf();
+    return;
+  }
   const double rv = mpj_sqrt(P.L2 * P.L2 + P.W2 * P.W2);
   for (int e = 0; e < 2; e++) {
     const double nx = pre[6 * e + 2], ny = pre[6 * e + 3];
@@ -379,16 +396,29 @@ __device__ __forceinline__ int cull_vehicle_side(const HaDev& P, const double* c
   return (__builtin_fabs(u) > P.L2 * (1 + 1e-12) + cl[2]) | (__builtin_fabs(v) > P.W2 * (1 + 1e-12) + cl[2]);
 }
 
-// vehicle pose q=[x,y,ψ] (rear axle) against all walls (corners wp, SAT tables wpre, centres /
-// far² wc and cull bounds wcl in LDS); 1 = free
-__device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const double* wp, const double* wpre,
-                                         const double* wc, const double* wcl, int nw) {
-  double sq, cq;
-  mpj_sincos_bl(q[2], &sq, &cq);
+// The heading-only part of a pose's collision check: sin/cos of ψ (the centre offset) and of the
+// rectangle's yaw modπ(ψ) (its own sin/cos only when it differs; when yaw == ψ bit for bit the two pairs
+// are the same numbers).  A function of ψ alone, so the neighbour sweeps read it from a per-plan table
+// (ha_pose_table_kernel) when the expanded node's heading is a lattice heading.
+struct PoseTrig {
+  double sq, cq, sy, cy;
+};
+__device__ __forceinline__ PoseTrig pose_trig(double psi) {
+  PoseTrig t;
+  mpj_sincos_bl(psi, &t.sq, &t.cq);
+  const double yaw = mpj_modpi_bl(psi);
+  t.sy = t.sq;
+  t.cy = t.cq;
+  if (MPJ_ANY(yaw != psi)) mpj_sincos_bl(yaw, &t.sy, &t.cy);  // |ψ| > π: the wrapped yaw's own sin/cos
+  return t;
+}
+
+// vehicle pose q=[x,y,ψ] (rear axle) with its heading terms T against all walls (corners wp, SAT tables
+// wpre, centres / far² wc and cull bounds wcl in LDS); 1 = free
+__device__ __forceinline__ int pose_free_t(const HaDev& P, const double* q, const PoseTrig& T, const double* wp,
+                                           const double* wpre, const double* wc, const double* wcl, int nw) {
+  const double sq = T.sq, cq = T.cq, sy = T.sy, cy = T.cy;
   const double x = q[0] + P.L2 * cq, y = q[1] + P.L2 * sq;
-  const double yaw = mpj_modpi_bl(q[2]);
-  double sy = sq, cy = cq;
-  if (MPJ_ANY(yaw != q[2])) mpj_sincos_bl(yaw, &sy, &cy);  // |ψ| > π: the wrapped yaw's own sin/cos
   // the SAT calls whose result is not certain (bit 2i: SAT(wall i, vehicle), bit 2i+1: SAT(vehicle,
   // wall i)), collected before the rectangle is built so its corners are live only where needed
   unsigned need = 0;
@@ -410,6 +440,10 @@ __device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const 
     if (((need >> (2 * i)) & 2) && !sat(vp, wp + 10 * i)) return 0;
   }
   return 1;
+}
+__device__ __forceinline__ int pose_free(const HaDev& P, const double* q, const double* wp, const double* wpre,
+                                         const double* wc, const double* wcl, int nw) {
+  return pose_free_t(P, q, pose_trig(q[2]), wp, wpre, wc, wcl, nw);
 }
 
 // one (wall, direction) term of pose_free: d = 0 SAT(wall, vehicle), d = 1 SAT(vehicle, wall); the pose
@@ -434,6 +468,24 @@ __device__ __forceinline__ int pose_free_part(const HaDev& P, const double* q, c
   if (d == 1 && cull_vehicle_side(P, wcl + 3 * w, fx, fy, cy, sy)) return 1;
   double vp[10];
   rect_pts(x, y, cy, sy, P.L2, P.W2, vp);
+  return d == 0 ? sat_pre(wpre + 24 * w, vp) : sat(vp, wp + 10 * w);
+}
+// the same term with the heading terms given (the pose table)
+__device__ __forceinline__ int pose_free_part_t(const HaDev& P, const double* q, const PoseTrig& T, const double* wp,
+                                                const double* wpre, const double* wc, const double* wcl, int w, int d) {
+  const double x = q[0] + P.L2 * T.cq, y = q[1] + P.L2 * T.sq;
+  const double fx = x - wc[3 * w], fy = y - wc[3 * w + 1];
+  if (fx * fx + fy * fy > wc[3 * w + 2]) return 1;
+#if HA_SAT_OVERLAP
+  const int ws = wall_side_class(wpre + 24 * w, wcl + 3 * w, x, y);
+  if (ws == 2) return 0;
+  if (d == 0 && ws == 1) return 1;
+#else
+  if (d == 0 && wall_side_class(wpre + 24 * w, wcl + 3 * w, x, y) == 1) return 1;
+#endif
+  if (d == 1 && cull_vehicle_side(P, wcl + 3 * w, fx, fy, T.cy, T.sy)) return 1;
+  double vp[10];
+  rect_pts(x, y, T.cy, T.sy, P.L2, P.W2, vp);
   return d == 0 ? sat_pre(wpre + 24 * w, vp) : sat(vp, wp + 10 * w);
 }
 
@@ -507,6 +559,18 @@ struct IterArgs {
   long long* idx;        // [B][n_prim]
   unsigned char* fr;     // [B][n_prim]
   double* h;             // [B][n_prim]
+  // (mp_ha_plan, HA_RS_WINNER) rs_heuristic's winning Reeds-Shepp candidate (0..47) per neighbour, -1 when
+  // the group did not evaluate it; and the popped node's stored winner per scene (-1: unknown -> RS_connected
+  // runs the full 48-candidate search).  A node's states never change after its creation (FindNewNode's
+  // update branch, hybrid_astar_utils.jl:425-430, touches g/h/f/parent only), and RS_connected (:229-230)
+  // runs the same changeBasis + allpath on them as rs_heuristic (:365-366) did at the creation, so the
+  // stored candidate is RS_connected's argmin and only its word needs evaluating for the commands.
+  int* hw;               // [B][n_prim]
+  const int* node_rw;    // [B]
+  // (mp_ha_plan) the pose table: PoseTrig of every swept primitive pose (1:5:n_col) for every lattice
+  // heading m·res[2], m = pt_mlo .. pt_mlo + pt_nm - 1: [pt_nm][n_prim][pt_nsw][4]; nullptr = compute
+  const double* ptab;
+  int pt_mlo, pt_nm, pt_nsw;
 };
 
 // Agent-coherent relaxed stores / loads (global_store / global_load with the sc1 policy: they reach
@@ -571,14 +635,28 @@ static_assert(12 % HW == 0, "HA_WAVES must divide the 12 Reeds-Shepp words");
 #define HA_NBG_TAIL 4
 #endif
 constexpr int HW_TAIL = 12, NBG_TAIL = HA_NBG_TAIL;
+// (A/B) -DHA_TAIL_OVERLAP=1: the tail shape's neighbour groups evaluate rs_heuristic for all their
+// neighbours, overlapped with the sweep, instead of sweeping first and evaluating it only when a neighbour
+// needs it (as the full-width shape does).  Measured slower (r05e, lone 729-pop scenario: 29.1 vs 28.3 us
+// per iteration): with 4 neighbours per group a word fills 16 of a wave's 64 lanes, and the group's 12
+// waves (3 per SIMD) are issue-bound -- the word search takes ~10 us on every group instead of ~8.5 us on
+// the groups that need it.
+#ifndef HA_TAIL_OVERLAP
+#define HA_TAIL_OVERLAP 0
+#endif
 
 // allpath + findmin split over the block's HW waves: wave w evaluates words WPW·w+1..WPW·(w+1) for
 // its lanes' candidates (lane&3 = variant of the state in `s`), the per-wave winners are
 // combined in LDS in word order with the same total order (rs_before).  Every wave returns
 // the block-wide winner for its lanes; *best_id is the winning candidate id.
-template <bool CMD, int HWt>
+struct NoMid {
+  __device__ void operator()() const {}
+};
+// mid(): work the block does between its word loop and the cross-wave reduction (the tail shape's collision
+// sweep), so the waves' Reeds-Shepp chains and that work overlap on the SIMDs instead of following each other
+template <bool CMD, int HWt, class Mid = NoMid>
 __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* best_id, double* sh_c, int* sh_i,
-                                                double* cmd_out = nullptr) {
+                                                double* cmd_out = nullptr, const Mid& mid = Mid()) {
   constexpr int WPW = 12 / HWt;  // Reeds–Shepp words per wave
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, var = lane & 3;
   double q[3];
@@ -610,6 +688,7 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   HTIME(13);
   sh_c[tid] = bc;
   sh_i[tid] = bi;
+  mid();
   __syncthreads();
   double v = sh_c[lane];
   int ix = sh_i[lane];
@@ -645,6 +724,37 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
     }
   }
   return v;
+}
+
+// RS_connected's allpath + findmin when the winning candidate id is already known (the popped node's
+// rs_heuristic winner, IterArgs::node_rw): wave 0 evaluates only that word, lane v = variant v, and the
+// lane of the winning variant stores the commands as rs_best_split does.  The same operations on the same
+// operands as that candidate's evaluation inside the full search, so the same cost and commands.
+__device__ __forceinline__ void rs_known_cmd(const double* s, int tid, int id, double* cmd_out) {
+  if (tid >= 64) return;  // wave-uniform
+  const int lane = tid & 63, var = lane & 3;
+  double q[3];
+  rs_variant(s, var, q);
+  const RsPre R = rs_pre(q);
+  Cmd cb;
+  const double cost = rs_word(id / 4 + 1, R, &cb);
+  const int n = cost < __builtin_inf() ? cb.n : 0;  // the winner's own cost is the search's minimum
+#pragma unroll
+  for (int r = 0; r < 5; r++) {
+    double ge = 0.0, st = 0.0, tr = 0.0;
+    if (r < n) {
+      tr = cb.tr[r];
+      ge = cb.ge[r];
+      st = cb.st[r];
+      if (var == 1 || var == 3) ge = -1 * ge;
+      if (var == 2 || var == 3) st = -1 * st;
+    }
+    if (lane == (id & 3)) {
+      cmd_out[r * 3 + 0] = tr;
+      cmd_out[r * 3 + 1] = ge;
+      cmd_out[r * 3 + 2] = st;
+    }
+  }
 }
 
 // One search iteration's device work for the block (role by blockIdx: RS_connected or a
@@ -711,6 +821,9 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     }
   }
   if (tid < NBG) g_free[tid] = 1;
+  // the tail shape (threads to spare): the collision sweep splits every pose into its 2·n_walls SAT terms,
+  // one per thread, and a neighbour group evaluates rs_heuristic for all its neighbours at once
+  constexpr bool SPLIT = HWt == HW_TAIL;
   int hit = -1;  // (groups with a Dict) the neighbour's node id in the scene's Dict
   if (tid < nk) {  // transform + regulate_states + Encode of the group's neighbours (:396-405)
     const int k = k0 + tid;
@@ -718,7 +831,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     transform1(node, A.sc + 3 * k, t);
     regulate(P, t, nb);
     const long long ix = encode(P, nb);
-    if (!rs && A.dnid) hit = ix > 0 && ix < A.C ? A.dnid[(size_t)s * A.C + ix] : -1;
+    if (!rs && !(SPLIT && HA_TAIL_OVERLAP) && A.dnid) hit = ix > 0 && ix < A.C ? A.dnid[(size_t)s * A.C + ix] : -1;
     st_out(A.coherent, R.nb + 3 * k, nb[0]);
     st_out(A.coherent, R.nb + 3 * k + 1, nb[1]);
     st_out(A.coherent, R.nb + 3 * k + 2, nb[2]);
@@ -733,9 +846,14 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   HSTAMP(12);
   __syncthreads();
   const int j = lane >> 2;
-  // collision sweep: (neighbour, pose) pairs of this group, or the RS path's poses; the tail shape
-  // (threads to spare) splits every pose into its 2·n_walls SAT terms, one per thread
-  constexpr bool SPLIT = HWt == HW_TAIL;
+  // the expanded node's heading is a lattice heading m·res[2] (bit for bit; every regulated state's is):
+  // its poses' heading terms come from the pose table
+  int tabm = -1;
+  if (!rs && A.ptab) {
+    const double m = mpj_round(node[2] / P.res[2]);
+    if (__double_as_longlong(m * P.res[2]) == __double_as_longlong(node[2]) && m >= A.pt_mlo && m < A.pt_mlo + A.pt_nm)
+      tabm = (int)m - A.pt_mlo;
+  }
   auto sweep = [&](int npose) {
     double nsn = 0.0, ncs = 1.0;
     if (!rs) mpj_sincos_bl(node[2], &nsn, &ncs);
@@ -754,19 +872,33 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       } else {
         transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
       }
-      const int fr = SPLIT ? pose_free_part(P, q, wp, wpre, wc, wcl, part >> 1, part & 1) : pose_free(P, q, wp, wpre, wc, wcl, nw);
+      int fr;
+      if (tabm >= 0) {  // block-uniform
+        const double2* e =
+            reinterpret_cast<const double2*>(A.ptab + (((size_t)tabm * P.n_prim + k0 + jn) * A.pt_nsw + jp) * 4);
+        const double2 a = e[0], c = e[1];
+        const PoseTrig T{a.x, a.y, c.x, c.y};
+        fr = SPLIT ? pose_free_part_t(P, q, T, wp, wpre, wc, wcl, part >> 1, part & 1)
+                   : pose_free_t(P, q, T, wp, wpre, wc, wcl, nw);
+      } else {
+        fr = SPLIT ? pose_free_part(P, q, wp, wpre, wc, wcl, part >> 1, part & 1) : pose_free(P, q, wp, wpre, wc, wcl, nw);
+      }
       if (!fr) g_free[jn] = 0;  // every writer stores 0
     }
   };
   double cb = 0.0;
-  int best;
+  int best = -1;
   if (rs) {
     // allpath + findmin: RS_connected's optimal command from the popped node
     double ns[3];
+    const int known = A.node_rw ? A.node_rw[s] : -1;  // the popped node's stored rs_heuristic winner
     change_basis(node, goal, P.minR, ns);
     HTIME(2);
     HSTAMP(12);
-    cb = rs_best_split<true, HWt>(ns, tid, &best, red_c, red_i, cmd);
+    if (known >= 0 && known < 48)  // block-uniform
+      rs_known_cmd(ns, tid, known, cmd);
+    else
+      cb = rs_best_split<true, HWt>(ns, tid, &best, red_c, red_i, cmd);
     HSTAMP(13);
     HTIME(3);
     // createActPath (ReedsSheppsUtils.jl:440-466): 100 Euler steps per segment -- per segment the
@@ -874,6 +1006,17 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     HTIME(4);
     sweep(n > 5 ? (n - 1) / 5 + 1 : 1);  // block_collision_check on poses 1:5:end
     HTIME(5);
+  } else if (SPLIT && HA_TAIL_OVERLAP) {
+    // tail shape (latency-bound: CUs to spare, one scene's chain): rs_heuristic of every neighbour of the
+    // group, whether or not FindNewNode will read it, without waiting for the collision sweep; the sweep
+    // runs between each wave's Reeds-Shepp word and the cross-wave reduction, so the two overlap
+    double ns[3];
+    change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
+    const int npose = P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1;
+    cb = rs_best_split<false, HWt>(ns, tid, &best, red_c, red_i, nullptr, [&] { sweep(npose); });
+    HSTAMP(13);
+    HSTAMP(14);
+    HSTAMP(15);
   } else {
     // dg_cost first (primitive poses 1:5:n_col): rs_heuristic is only used for neighbours that
     // are collision-free and in bounds, so a group without one skips the 48 RS candidates.
@@ -916,6 +1059,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     const int fr = g_ix[j] != 0 && g_free[j];
     st_out(A.coherent, R.fr + k0 + j, (unsigned char)fr);
     st_out(A.coherent, R.h + k0 + j, fr ? cb * P.minR : 0.0);
+    if (A.hw) st_out(A.coherent, A.hw + (size_t)s * P.n_prim + k0 + j, fr ? best : -1);
   }
   return true;
 }
@@ -990,7 +1134,26 @@ int make_ha(mp_ctx* ctx, const mp_ha_params* p, HaDev* D) {
   D->n_walls = p->n_walls;
   D->n_prim = p->n_prim;
   D->n_col = p->n_col;
+  D->cull = 0;  // set per call by ha_cull_ok
   return MP_OK;
+}
+
+// the coordinate-magnitude guard of the SAT culls (HA_CULL_MAX above): walls [B][n_walls][5] (x, y, ψ,
+// half length, half width), a and b [B][3] (nodes / starts, goals)
+void ha_cull_ok(const mp_ctx* ctx, const mp_ha_params* p, HaDev* D, int B, const double* walls, const double* a,
+                const double* b) {
+  double m = std::max({p->minR, p->vehicle_len, p->vehicle_wid, p->expand_time, ctx->ha_prim_ext});
+  for (int i = 0; i < 6; i++) m = std::max(m, std::fabs(p->stbound[i]));
+  for (size_t i = 0; walls && i < (size_t)B * p->n_walls; i++) {
+    const double* w = walls + 5 * i;
+    m = std::max(m, std::fabs(w[0]) + std::fabs(w[3]) + std::fabs(w[4]));
+    m = std::max(m, std::fabs(w[1]) + std::fabs(w[3]) + std::fabs(w[4]));
+  }
+  for (size_t i = 0; i < 3 * (size_t)B; i++) {
+    if (a && i % 3 != 2) m = std::max(m, std::fabs(a[i]));
+    if (b && i % 3 != 2) m = std::max(m, std::fabs(b[i]));
+  }
+  D->cull = m <= HA_CULL_MAX;  // NaN: off
 }
 
 int need_prims(mp_ctx* ctx, const mp_ha_params* p) {
@@ -1012,6 +1175,23 @@ int launch_iter(mp_ctx* ctx, const HaDev& D, IterArgs& A) {
 
 // Block2Pts + the wall-side SAT tables (pose independent) + centre / far² + the cull bounds once per plan:
 // [B][nw][WT]
+// the pose table (IterArgs::ptab): thread = (m, primitive k, swept pose j); the heading m·res[2] + the
+// primitive pose's heading, as transform computes it, and its PoseTrig
+__global__ __launch_bounds__(256) void ha_pose_table_kernel(HaDev P, const double* pc, int mlo, int nm, int nsw,
+                                                            double* tab) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= nm * P.n_prim * nsw) return;
+  const int j = t % nsw, k = (t / nsw) % P.n_prim, m = t / (nsw * P.n_prim);
+  const double head = (double)(mlo + m) * P.res[2];
+  const double psi = pc[((size_t)k * P.n_col + j * 5) * 3 + 2] + head;
+  const PoseTrig T = pose_trig(psi);
+  double* o = tab + (size_t)t * 4;
+  o[0] = T.sq;
+  o[1] = T.cq;
+  o[2] = T.sy;
+  o[3] = T.cy;
+}
+
 __global__ __launch_bounds__(64) void ha_wall_kernel(HaDev P, int B, const double* walls, double* wtab) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= B * P.n_walls) return;
@@ -1063,6 +1243,9 @@ struct HaSearch {
   int* lst;              // [2][B] those scenes' indices (iteration i writes list i & 1, in any order)
   int* tk;               // [2][B] ha_step_kernel arrival tickets: neighbour groups, then (RS block, bookkeeping)
   long long* rec;        // [B][8] ha_step_kernel: the bookkeeping's record for the scene's finisher
+  int* rw;               // [B][C] per node id: rs_heuristic's winning candidate at the node's creation (-1: unknown)
+  int* orw;              // [B][C] open entries: the same, so popfirst! hands it to RS_connected with the state
+  int* node_rw;          // [2][B] popped node's winner, double-buffered like node
 };
 enum { SI_NNODES = 0, SI_NOPEN, SI_LOOP, SI_CUR, SI_ACTIVE, SI_FOUND, SI_NSTATES, SI_RSLEN, SI_N };
 
@@ -1111,7 +1294,7 @@ __device__ __forceinline__ void key_min_dpp(double& f, long long& sq, int& p) {
 constexpr int BKT = 256;
 template <int NT>
 __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int tid,
-                                       double* node_out, bool direct, long long* iw_out,
+                                       double* node_out, int* rw_out, bool direct, long long* iw_out,
                                        unsigned long long* stp = nullptr) {
   static_assert(NT % 64 == 0, "whole waves");
   __shared__ double r_f[NT / 64];
@@ -1119,6 +1302,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   __shared__ int r_p[NT / 64];
   __shared__ double r_pay[NT / 64][5];  // the wave winner's entry: g, Encode index, state
   __shared__ int r_id[NT / 64];
+  __shared__ int r_rw[NT / 64];
   const size_t base = (size_t)b * Q.C;
   if (n_open == 0 || loop >= Q.mp) return false;
   const int lane = tid & 63, wave = tid >> 6;
@@ -1126,19 +1310,20 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   // the last entry (moved into the winner's place) does not depend on the scan: loaded first
   double fl = 0.0, gl = 0.0, stl = 0.0;
   long long sl = 0, il = 0;
-  int lid = 0;
+  int lid = 0, rwl = -1;
   if (tid < 64) {
     fl = Q.of[base + last];
     gl = Q.og[base + last];
     sl = Q.oseq[base + last];
     il = Q.oix[base + last];
     lid = Q.oid[base + last];
+    rwl = Q.orw[base + last];
     if (lane < 3) stl = Q.ost[(base + last) * 3 + lane];
   }
   double bf = __builtin_inf();
   long long bs = 0x7fffffffffffffffLL;
   int bp = -1;
-  int pid = 0;
+  int pid = 0, prw = -1;
   double pg = 0.0, pix = 0.0, p0s = 0.0, p1s = 0.0, p2s = 0.0;
   for (int p0 = tid; p0 < n_open; p0 += 4 * NT) {
     double fv[4];
@@ -1159,6 +1344,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   // (no dependent load after the winner is known)
   if (bp >= 0) {
     pid = Q.oid[base + bp];
+    prw = Q.orw[base + bp];
     pg = Q.og[base + bp];
     pix = __longlong_as_double(Q.oix[base + bp]);
     p0s = Q.ost[(base + bp) * 3];
@@ -1193,6 +1379,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   if (lane == 0) { r_f[wave] = bf; r_s[wave] = bs; r_p[wave] = bp; }
   if (bp >= 0 && own == bp) {  // the one lane that scanned the wave's winning position
     r_id[wave] = pid;
+    r_rw[wave] = prw;
     r_pay[wave][0] = pg;
     r_pay[wave][1] = pix;
     r_pay[wave][2] = p0s;
@@ -1223,6 +1410,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   bp = __builtin_amdgcn_readlane(cp, 0);
   const int ww = __builtin_ctzll(__ballot(lane < NT / 64 && mine == bp));
   const int id = r_id[ww];
+  const int rww = r_rw[ww];
   const double gw = r_pay[ww][0];
   const long long iw = __double_as_longlong(r_pay[ww][1]);
   const double stw = lane < 3 ? r_pay[ww][2 + lane] : 0.0;
@@ -1233,6 +1421,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
       Q.oid[base + bp] = lid;
       Q.og[base + bp] = gl;
       Q.oix[base + bp] = il;
+      Q.orw[base + bp] = rwl;
       Q.pos[base + lid] = bp;
     }
     if (lane < 3) Q.ost[(base + bp) * 3 + lane] = stl;
@@ -1249,6 +1438,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
     }
     Q.cur_g[b] = gw;
     Q.cur_ix[b] = iw;
+    rw_out[b] = rww;
   }
   if (lane < 3) node_out[3 * b + lane] = stw;
   return true;
@@ -1269,6 +1459,7 @@ __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B
     Q.seq[base] = 0;
     Q.pos[base] = 0;
     Q.of[base] = 0.0; Q.oseq[base] = 0; Q.oid[base] = 0;
+    Q.rw[base] = -1; Q.orw[base] = -1;  // the start node: RS_connected runs the full search once
     Q.og[base] = 0.0; Q.oix[base] = si;
     for (int r = 0; r < 3; r++) Q.ost[base * 3 + r] = s0[r];
     Q.ctr[b] = 1;
@@ -1284,7 +1475,7 @@ __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B
     if (si >= 0 && si < Q.C) Q.nid[base + si] = 0;
   }
   __syncthreads();
-  const bool go = ha_pop<256>(Q, B, b, 1, 0, tid, Q.node, true, nullptr);  // node buffer 0: iteration 1 reads it
+  const bool go = ha_pop<256>(Q, B, b, 1, 0, tid, Q.node, Q.node_rw, true, nullptr);  // node buffer 0: iteration 1 reads it
   if (tid == 0) Q.sc_i[SI_ACTIVE * B + b] = go;
 }
 
@@ -1308,12 +1499,13 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   const double cur_g = Q.cur_g[b];
   const long long cidx = Q.cur_ix[b];
   long long ix = 0;
-  int frk = 0;
+  int frk = 0, hwk = -1;
   double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
   if (tid < np) {
     ix = A.idx[(size_t)b * np + tid];
     frk = A.fr[(size_t)b * np + tid];
     hk = A.h[(size_t)b * np + tid];
+    if (A.hw) hwk = A.hw[(size_t)b * np + tid];
     nb0 = A.nb[((size_t)b * np + tid) * 3];
     nb1 = A.nb[((size_t)b * np + tid) * 3 + 1];
     nb2 = A.nb[((size_t)b * np + tid) * 3 + 2];
@@ -1367,7 +1559,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   }
   int hit = -1;
   double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
-  int po = 0;
+  int po = 0, drw = -1;
   long long so0 = 0, io = 0;
   if (valid) {  // wave 0: the Dict entry of every valid lane (used by the first occurrences below)
     hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
@@ -1377,6 +1569,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
       fo_ = Q.f[base + hit];
       so0 = Q.seq[base + hit];
       io = Q.index[base + hit];
+      drw = Q.rw[base + hit];
       dst0 = Q.st[(base + hit) * 3];
       dst1 = Q.st[(base + hit) * 3 + 1];
       dst2 = Q.st[(base + hit) * 3 + 2];
@@ -1398,6 +1591,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
     long long so_ = 0;
     double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;  // the node's state and Encode index (its open entry)
     long long nix = ix;
+    int nrw = hwk;  // the node's stored rs_heuristic winner (its open entry carries it)
     if (first) {
       th = __builtin_fmax(hk, 0.0);
       if (hk != hk) th = hk;
@@ -1408,6 +1602,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
         nst1 = dst1;
         nst2 = dst2;
         nix = io;
+        nrw = drw;
         if (tg < gd) {
           if (po >= 0) {
             chg = true;
@@ -1448,6 +1643,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
         Q.st[q * 3 + 1] = nst1;
         Q.st[q * 3 + 2] = nst2;
         Q.index[q] = ix;
+        Q.rw[q] = nrw;
         if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
       }
       Q.g[q] = tg;
@@ -1462,6 +1658,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
       if (!chg) {
         Q.oid[base + p] = id;
         Q.oix[base + p] = nix;
+        Q.orw[base + p] = nrw;
         Q.ost[(base + p) * 3] = nst0;
         Q.ost[(base + p) * 3 + 1] = nst1;
         Q.ost[(base + p) * 3 + 2] = nst2;
@@ -1480,7 +1677,8 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   BTIME(6);
   const int n_open = s_nopen;
   // ---- next popfirst!
-  const bool go = ha_pop<BKT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, true, nullptr);
+  const bool go = ha_pop<BKT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B, true,
+                            nullptr);
   BTIME(7);
   if (tid == 0) {
     if (go) Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;
@@ -1545,13 +1743,14 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   const double cur_g = Q.cur_g[b];
   const long long cidx = Q.cur_ix[b];
   long long ix = 0;
-  int frk = 0;
+  int frk = 0, hwk = -1;
   double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
   if (tid < np) {
     const size_t q = (size_t)b * np + tid;
     ix = ld_ag(A.idx + q);
     frk = ld_ag(A.fr + q);
     hk = ld_ag(A.h + q);
+    if (A.hw) hwk = ld_ag(A.hw + q);
     nb0 = ld_ag(A.nb + 3 * q);
     nb1 = ld_ag(A.nb + 3 * q + 1);
     nb2 = ld_ag(A.nb + 3 * q + 2);
@@ -1575,7 +1774,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   }
   int hit = -1;
   double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
-  int po = 0;
+  int po = 0, drw = -1;
   long long so0 = 0, io = 0;
   if (valid) {
     hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
@@ -1585,6 +1784,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
       fo_ = Q.f[base + hit];
       so0 = Q.seq[base + hit];
       io = Q.index[base + hit];
+      drw = Q.rw[base + hit];
       dst0 = Q.st[(base + hit) * 3];
       dst1 = Q.st[(base + hit) * 3 + 1];
       dst2 = Q.st[(base + hit) * 3 + 2];
@@ -1605,6 +1805,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
     long long so_ = 0;
     double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;
     long long nix = ix;
+    int nrw = hwk;  // the node's stored rs_heuristic winner (its open entry carries it)
     if (first) {
       th = __builtin_fmax(hk, 0.0);
       if (hk != hk) th = hk;
@@ -1615,6 +1816,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
         nst1 = dst1;
         nst2 = dst2;
         nix = io;
+        nrw = drw;
         if (tg < gd) {
           if (po >= 0) {
             chg = true;
@@ -1653,6 +1855,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
         Q.st[q * 3 + 1] = nst1;
         Q.st[q * 3 + 2] = nst2;
         Q.index[q] = ix;
+        Q.rw[q] = nrw;
         if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
       }
       Q.g[q] = tg;
@@ -1667,6 +1870,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
       if (!chg) {
         Q.oid[base + p] = id;
         Q.oix[base + p] = nix;
+        Q.orw[base + p] = nrw;
         Q.ost[(base + p) * 3] = nst0;
         Q.ost[(base + p) * 3 + 1] = nst1;
         Q.ost[(base + p) * 3 + 2] = nst2;
@@ -1685,7 +1889,8 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   const int n_open = s_nopen;
   long long iw = 0;
   bool go;
-  go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, false, &iw, stp);
+  go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B, false,
+              &iw, stp);
   BSTAMP(8);
   BookRec br;
   br.v[RC_GO] = go;
@@ -1783,7 +1988,8 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (r == 0) return;
-  // The final ticket.  The bookkeeping block takes it before publishing anything: arriving second (the
+  // The final ticket (two arrivals: this scene's RS_connected block and its bookkeeping block, so the launch
+  // needs do_rs && do_exp -- mp_ha_plan checks it).  The bookkeeping block takes it before publishing anything: arriving second (the
   // usual case) it finishes with its own values; arriving first it publishes its record and then a
   // ready flag, which the RS_connected block, arriving second, waits for (a short wait: the bookkeeping
   // block is running and publishes without waiting on anything).
@@ -1992,6 +2198,10 @@ int mp_ha_set_primitives(mp_ctx* ctx, const mp_ha_params* p, const double* state
                         hipMemcpyHostToDevice));
   ctx->ha_n_prim = p->n_prim;
   ctx->ha_n_col = p->n_col;
+  double ext = 0;
+  for (size_t i = 0; i < 3 * (size_t)p->n_prim * p->n_col; i++)
+    if (i % 3 != 2) ext = std::max(ext, std::fabs(paths_candi[i]));
+  ctx->ha_prim_ext = ext;
   return MP_OK;
 }
 
@@ -2033,6 +2243,7 @@ int mp_ha_expand(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* no
   if ((st = need_prims(ctx, p))) return st;
   MP_CHECK(ctx, B >= 1 && node && goal && (walls || p->n_walls == 0) && nb_states && idx && free_ && h,
            "bad arguments");
+  ha_cull_ok(ctx, p, &D, B, walls, node, goal);
   MP_HIP(ctx, hipSetDevice(ctx->device));
   const size_t np = p->n_prim;
   IterArgs A{};
@@ -2068,6 +2279,7 @@ int mp_ha_rs_connect(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double
   int st = make_ha(ctx, p, &D);
   if (st) return st;
   MP_CHECK(ctx, B >= 1 && node && goal && (walls || p->n_walls == 0) && ok && path && path_len, "bad arguments");
+  ha_cull_ok(ctx, p, &D, B, walls, node, goal);
   MP_HIP(ctx, hipSetDevice(ctx->device));
   IterArgs A{};
   A.node = mp_upload(ctx, WS_IO0, node, 3 * (size_t)B, &st);
@@ -2088,6 +2300,18 @@ int mp_ha_rs_connect(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double
   if ((st = mp_download(ctx, path, (const double*)A.rs_path, (size_t)B * MAXPATH * 3))) return st;
   if ((st = mp_download(ctx, path_len, (const int32_t*)A.rs_len, (size_t)B))) return st;
   MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return MP_OK;
+}
+
+int mp_ha_sat_cull_active(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* walls, const double* a,
+                          const double* b, int32_t* active) {
+  if (!ctx) return MP_ERR_INVALID;
+  HaDev D;
+  int st = make_ha(ctx, p, &D);
+  if (st) return st;
+  MP_CHECK(ctx, B >= 1 && (walls || p->n_walls == 0) && active, "bad arguments");
+  ha_cull_ok(ctx, p, &D, B, walls, a, b);
+  *active = D.cull;
   return MP_OK;
 }
 
@@ -2176,6 +2400,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_CHECK(ctx, B >= 1 && start && goal && (walls || p->n_walls == 0) && found && pops && n_nodes && pop_seq &&
                n_states && states_out && rs_len && rs_path, "bad arguments");
   MP_CHECK(ctx, p->max_pops >= 1, "max_pops must be >= 1");
+  ha_cull_ok(ctx, p, &D, B, walls, start, goal);
   MP_CHECK(ctx, p->n_prim <= 64, "n_prim (%d) must be <= 64 (one neighbour per lane of the bookkeeping wave)",
            p->n_prim);
   MP_HIP(ctx, hipSetDevice(ctx->device));
@@ -2187,9 +2412,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_CHECK(ctx, ncell > 0 && ncell < (1LL << 26), "state lattice too large (%lld cells)", ncell);
   const size_t C = (size_t)ncell + 1, nB = (size_t)B;
   // search state: node arrays and open list indexed [scene][node / cell]
-  const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24;
+  const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + 256 * 36);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + 256 * 40);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -2223,6 +2448,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.lst = (int*)take(sizeof(int) * 2 * nB);
   Q.tk = (int*)take(sizeof(int) * 2 * nB);
   Q.rec = (long long*)take(nB * RC_N * 8);
+  Q.rw = (int*)take(nB * C * 4);
+  Q.orw = (int*)take(nB * C * 4);
+  Q.node_rw = (int*)take(nB * 8);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
@@ -2234,7 +2462,37 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.rs_ok = (unsigned char*)mp_ws(ctx, WS_IO5, nB);
   A.rs_len = (int*)mp_ws(ctx, WS_IO6, sizeof(int) * nB);
   A.rs_path = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * nB * MAXPATH * 3);
-  if (st || !A.h || !A.nb || !A.idx || !A.fr || !A.rs_ok || !A.rs_len || !A.rs_path) return st ? st : MP_ERR_NOMEM;
+  A.hw = (int*)mp_ws(ctx, WS_IO9, sizeof(int) * nB * np);
+  if (st || !A.h || !A.nb || !A.idx || !A.fr || !A.rs_ok || !A.rs_len || !A.rs_path || !A.hw)
+    return st ? st : MP_ERR_NOMEM;
+#ifndef HA_RS_WINNER
+#define HA_RS_WINNER 1
+#endif
+  // (A/B) MPGPU_HA_RS_FULL=1 (or -DHA_RS_WINNER=0): RS_connected always runs the 48-candidate search
+  static const bool rs_full = !HA_RS_WINNER || (getenv("MPGPU_HA_RS_FULL") && atoi(getenv("MPGPU_HA_RS_FULL")) == 1);
+  // the pose table (A.ptab): the neighbour sweeps' heading terms for every lattice heading -- regulated
+  // headings are round(modπ(ψ)/res)·res, so m spans round(±π/res) (one spare step each side); the few
+  // microseconds of one launch per plan.  (A/B) MPGPU_HA_NOTAB=1: every sweep evaluates its sin/cos.
+  static const bool notab = getenv("MPGPU_HA_NOTAB") && atoi(getenv("MPGPU_HA_NOTAB")) == 1;
+  {
+    const double r = p->res[2];
+    const int nsw = p->n_col > 5 ? (p->n_col - 1) / 5 + 1 : 1;
+    const double lo = std::floor(-MPJ_PI / r) - 1, hi = std::ceil(MPJ_PI / r) + 1;
+    const bool ok = !notab && r > 0 && hi - lo < 4096;
+    const int mlo = ok ? (int)lo : 0, nm = ok ? (int)(hi - lo) + 1 : 0;
+    const size_t n = (size_t)nm * np * nsw;
+    double* tab = ok ? (double*)mp_ws(ctx, WS_IO10, sizeof(double) * 4 * n) : nullptr;
+    if (ok && !tab) return MP_ERR_NOMEM;
+    if (tab) {
+      hipLaunchKernelGGL(ha_pose_table_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D,
+                         (const double*)ctx->ha_paths_candi, mlo, nm, nsw, tab);
+      MP_HIP(ctx, hipGetLastError());
+    }
+    A.ptab = tab;
+    A.pt_mlo = mlo;
+    A.pt_nm = nm;
+    A.pt_nsw = nsw;
+  }
   if (p->n_walls) {
     double* wt = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * nB * p->n_walls * WT);
     if (!wt) return MP_ERR_NOMEM;
@@ -2267,6 +2525,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.pc = ctx->ha_paths_candi;
   A.do_rs = 1;
   A.do_exp = 1;
+  // ha_step_kernel's final ticket is taken by the RS_connected block and by the scene's bookkeeping block
+  // (the last neighbour group): both roles must run, or no block finishes the iteration (and the RS block
+  // would wait for a record that never comes)
+  MP_CHECK(ctx, A.do_rs && A.do_exp, "ha_step_kernel needs both block roles");
   A.rs_path_free_only = 1;
   A.n_active = B;
   MP_HIP(ctx, hipMemsetAsync(Q.pop_seq, 0xff, nB * mp * 8, ctx->stream));  // -1 past each scene's pops
@@ -2311,6 +2573,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     A.n_live = it == 1 ? nullptr : Q.live + (it - 1);
     A.n_active = known;
     A.node = Q.node + (size_t)((it - 1) & 1) * 3 * B;  // the previous iteration's pops
+    A.node_rw = rs_full ? nullptr : Q.node_rw + (size_t)((it - 1) & 1) * B;
     const bool tail = known * per_tail <= tail_blocks;
     if (split) {
       if (tail)

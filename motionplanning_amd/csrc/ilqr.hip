@@ -2035,8 +2035,19 @@ __global__ __launch_bounds__(64) void ilqr_search_rest_kernel(IlqrDev P, int B, 
 // iteration's round 0 left pending (blocks n0.., instance-major within each 16-trial column), so
 // the rest pass's latency hides under round 0 instead of following it.  An instance's own sequence
 // of operations is unchanged (its next backward pass simply comes one launch later).
+// (A/B) ILQR_PIPE_WPE: waves per SIMD the pipelined search kernel is compiled for (0: the compiler's choice,
+// 244 VGPRs = 2 waves per SIMD -- exactly the 2,048 round-0 waves of a full-activity launch, so the rest-pass
+// waves of the same launch wait for round-0 waves to retire instead of running beside them)
+#ifndef ILQR_PIPE_WPE
+#define ILQR_PIPE_WPE 0
+#endif
+#if ILQR_PIPE_WPE
+#define ILQR_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(ILQR_PIPE_WPE)))
+#else
+#define ILQR_PIPE_ATTR
+#endif
 template <int G, int L, int L0 = L>
-__global__ __launch_bounds__(64) void ilqr_search_pipe_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
+__global__ __launch_bounds__(64) ILQR_PIPE_ATTR void ilqr_search_pipe_kernel(IlqrDev P, int B, double* X, double* U, const double* k,
                                                               const double* Kg, double* Xs, double* Us, double* Jcur,
                                                               int* active, int* iters, int* flags, int* n_active,
                                                               int* pend_new, int* mstar_new, int* npend_new,

@@ -174,8 +174,14 @@ template <class T>
 __device__ __forceinline__ T ld_ag(const T* p) {
   return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The arrival of a block's records at the scene's last block.  0 (default): each thread's records
+// acknowledged (vmcnt), then an agent-scope release fence before the relaxed ticket and an acquire fence in
+// the last block -- ordered within the HIP/HSA memory model.  1 (A/B): the records are agent-coherent stores
+// and the ticket relaxed, ordered by the per-thread vmcnt wait alone (sound on gfx94x/95x hardware, but
+// outside the language model); round 4 measured no gain from it (profiles/r04w_mppi_coherent_ha_scan_ab.txt),
+// so the fenced form is the default.
 #ifndef MPPI_COHERENT_PARTS
-#define MPPI_COHERENT_PARTS 1  // 0: the round-3 arrival (agent-scope release / acquire fences)
+#define MPPI_COHERENT_PARTS 0
 #endif
 
 // BT threads per block (4 or 8 waves); LPR lanes per rollout: 2 = lane pair (dyn_pair, the

@@ -39,6 +39,23 @@ __device__ __forceinline__ double pair_swap(double v) {
 }
 
 // ---------------------------------------------------------------- dynamics
+// The tyre chain's libm (vehicledynamics.jl:32-44: atan, sin, and sin/cos(ψ)).  Default: the FDLIBM
+// restatement of include/mp_jlmath.h -- Julia's own algorithms, bit-identical to the CPU oracle.
+// (A/B) -DMPPI_LIBM_OCML=1: ROCm's device libm (__ocml_atan_f64 / sin / sincos, ~1 ulp,
+// not Julia's bits) for the same calls, to measure what a non-FDLIBM tyre chain saves; tools/mppi_libm_ab.py
+// compares it with the oracle at north_star's tolerances.  Not a shipped mode.
+#ifndef MPPI_LIBM_OCML
+#define MPPI_LIBM_OCML 0
+#endif
+#if MPPI_LIBM_OCML
+#define TY_ATAN(x, tab) ::atan(x)
+#define TY_SIN(x) ::sin(x)
+#define TY_SINCOS(a, s, c) ::sincos((a), (s), (c))
+#else
+#define TY_ATAN(x, tab) mpj_atan_tab((x), (tab))
+#define TY_SIN(x) mpj_sin_34(x)
+#define TY_SINCOS(a, s, c) mpj_sincos_bl((a), (s), (c))
+#endif
 // VehicleDynamics for a lane pair.  side = lane & 1 (0: front tire, 1: rear).
 // atab: the mpj_atan_tab range table (LDS).
 //
@@ -69,9 +86,9 @@ __device__ __forceinline__ void dyn_pair_sc(const double* x, double sr, double a
   // front: 2*(KFZF*g - t);  rear: 2*(KFZR*g + t)   (vehicledynamics.jl:30-31); t·(∓1) is exact
   const double FZ = 2 * (pk.kfz * g + t * pk.tsg);
   // front: (v + la*r) ... - sa;  rear: (v - lb*r) ... [(-lb)*r == -(lb*r) exactly]  (:32-33)
-  const double alpha = mpj_atan_tab((v + pk.lr * r) / (ux + 0.01), atab) - (side ? 0.0 : sa);
+  const double alpha = TY_ATAN((v + pk.lr * r) / (ux + 0.01), atab) - (side ? 0.0 : sa);
   const double X1 = B * alpha;
-  const double FY = mu * FZ * 1.0 * mpj_sin_34(C * mpj_atan_tab(X1 - E * (X1 - mpj_atan_tab(X1, atab)), atab));  // (:35-38)
+  const double FY = mu * FZ * 1.0 * TY_SIN(C * TY_ATAN(X1 - E * (X1 - TY_ATAN(X1, atab)), atab));  // (:35-38)
   const double FYo = pair_swap(FY);
   const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);  // (:40-42)
   d[0] = uxc * cp - v * sp;
@@ -90,7 +107,7 @@ __device__ __forceinline__ void dyn_pair_sc(const double* x, double sr, double a
 }
 __device__ __forceinline__ void dyn_pair(const double* x, double sr, double ax, double* d, int side, const double* atab) {
   double sp, cp;
-  mpj_sincos_bl(x[4], &sp, &cp);
+  TY_SINCOS(x[4], &sp, &cp);
   dyn_pair_sc(x, sr, ax, d, side, atab, sp, cp, pair_k(side));
 }
 
@@ -106,14 +123,14 @@ __device__ __forceinline__ void dyn_lane(const double* x, double sr, double ax, 
   const double v = x[2], r = x[3], psi = x[4], ux = x[5], sa = x[6];
   const double t = (ax - r * v) * KFZX;
   const double FZf = 2 * (KFZF * g + -t), FZr = 2 * (KFZR * g + t);
-  const double af = mpj_atan_tab((v + la * r) / (ux + 0.01), atab) - sa;
-  const double ar = mpj_atan_tab((v + (-lb) * r) / (ux + 0.01), atab) - 0.0;
+  const double af = TY_ATAN((v + la * r) / (ux + 0.01), atab) - sa;
+  const double ar = TY_ATAN((v + (-lb) * r) / (ux + 0.01), atab) - 0.0;
   const double Xf = B * af, Xr = B * ar;
-  const double FY1 = mu * FZf * 1.0 * mpj_sin_34(C * mpj_atan_tab(Xf - E * (Xf - mpj_atan_tab(Xf, atab)), atab));
-  const double FY2 = mu * FZr * 1.0 * mpj_sin_34(C * mpj_atan_tab(Xr - E * (Xr - mpj_atan_tab(Xr, atab)), atab));
+  const double FY1 = mu * FZf * 1.0 * TY_SIN(C * TY_ATAN(Xf - E * (Xf - TY_ATAN(Xf, atab)), atab));
+  const double FY2 = mu * FZr * 1.0 * TY_SIN(C * TY_ATAN(Xr - E * (Xr - TY_ATAN(Xr, atab)), atab));
   const double uxc = MPJ_SEL(ux <= 0, 0.0, ux);
   double sp, cp;
-  mpj_sincos_bl(psi, &sp, &cp);
+  TY_SINCOS(psi, &sp, &cp);
   d[0] = uxc * cp - v * sp;
   d[1] = uxc * sp + v * cp;
   d[2] = (FY1 + FY2) / M - r * uxc;
@@ -331,7 +348,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
       // evaluates stage 1's and the odd lane stage 2's, then they swap (same operands, same bits)
       const double psi2 = x[4] + x[3] * P.dt;
       double sn, cs;
-      mpj_sincos_bl(side ? psi2 : x[4], &sn, &cs);
+      TY_SINCOS(side ? psi2 : x[4], &sn, &cs);
       const double so = pair_swap(sn), co = pair_swap(cs);
       dyn_pair_sc(x, u[0], u[1], k1, side, atab, side ? so : sn, side ? co : cs, pk);
 #pragma unroll

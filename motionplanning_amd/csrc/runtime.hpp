@@ -31,6 +31,7 @@ struct mp_ctx {
   double* ha_states_candi = nullptr;
   double* ha_paths_candi = nullptr;
   int ha_n_prim = 0, ha_n_col = 0;
+  double ha_prim_ext = 0;  // max |x|, |y| of the installed primitive poses (the SAT culls' coordinate guard)
   // per-scene arrival counters for the MPPI last-block combine (zero at rest)
   unsigned int* tickets = nullptr;
   int n_tickets = 0;

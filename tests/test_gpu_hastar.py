@@ -183,3 +183,41 @@ def test_bench_batch_full_size_bitexact(ctx):
         assert tr["status"] == tracker.STATUS[t["status"]] and tr["n_steps"] == t["n_steps"]
         assert np.array_equal(tr["final_state"], t["final"]) and tr["err_accumulated"] == t["err_acc"]
     assert len(found) == 169
+
+
+@pytest.mark.parametrize("shift,cull", [(1e5, 1), (1e7, 0)])
+def test_translated_scene_bitexact(ctx, shift, cull):
+    """The SAT culls' 1e-6 m rounding margin is proven for coordinates <= 1e6 m (mp_ha_sat_cull_active; the
+    library turns the culls off beyond it).  The perpendicular driver scene translated by (shift, shift) --
+    walls, stbound, start and goal -- planned on the device vs the oracle's full SAT, bit for bit: at 1e5 m
+    with the culls on, at 1e7 m with them off (CollisionDetection/src/utils.jl:37-74)."""
+    import ctypes
+
+    from motionplanning_amd.abi import ptr
+
+    st = ha.driver_settings()
+    sb = np.array(st["stbound"], float)
+    sb[:2] += shift
+    sc_ = ha.PERPENDICULAR
+    walls = [[w[0] + shift, w[1] + shift] + list(w[2:]) for w in sc_["walls"]]
+    start = [sc_["starting_real"][0] + shift, sc_["starting_real"][1] + shift, sc_["starting_real"][2]]
+    goal = [sc_["ending_real"][0] + shift, sc_["ending_real"][1] + shift, sc_["ending_real"][2]]
+    h = ha.defineHybridAstar(st["vehicle_size"], st["gear_set"], st["steer_set"], st["minR"], st["expand_time"],
+                             st["resolutions"], sb, start, goal)
+    ha.defineHybridAstarobs_(h, walls)
+    p = ha.params_of(h)
+    sc, pc = ha.install_primitives(h, ctx)
+    W = np.array(h.s.obstacle_list, float)[None]
+    a = np.array(h.s.starting_states, float)[None]
+    b = np.array(h.s.ending_states, float)[None]
+    on = ctypes.c_int32(-1)
+    ctx.check(ctx.lib.mp_ha_sat_cull_active(ctx.handle, ctypes.byref(p), 1, ptr(W), ptr(a), ptr(b), ctypes.byref(on)))
+    assert on.value == cull
+    ha.planHybridAstar_(h, ctx=ctx)
+    ref = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+    assert h.r.found == ref["found"] and h.r.loop_count == ref["pops"] and h.r.n_nodes == ref["n_nodes"]
+    assert np.array_equal(h.r.pop_sequence, ref["pop_seq"])
+    if ref["found"]:
+        assert np.array_equal(h.r.hybrid_astar_states.T, ref["states"])
+        assert np.array_equal(h.r.RSpath_final.T, ref["rs_path"])
+    assert ref["pops"] > 1
