@@ -567,6 +567,10 @@ struct IterArgs {
   // stored candidate is RS_connected's argmin and only its word needs evaluating for the commands.
   int* hw;               // [B][n_prim]
   const int* node_rw;    // [B]
+  // (tail launches of mp_ha_plan, ha_step_kernel<..., RSH = true>) rs_heuristic per neighbour in four word
+  // chunks: the chunk's best (cost, candidate id), [B][n_prim][4]; the bookkeeping combines them
+  double* hp_c;
+  int* hp_i;
   // (mp_ha_plan) the pose table: PoseTrig of every swept primitive pose (1:5:n_col) for every lattice
   // heading m·res[2], m = pt_mlo .. pt_mlo + pt_nm - 1: [pt_nm][n_prim][pt_nsw][4]; nullptr = compute
   const double* ptab;
@@ -641,6 +645,9 @@ constexpr int HW_TAIL = 12, NBG_TAIL = HA_NBG_TAIL;
 // per iteration): with 4 neighbours per group a word fills 16 of a wave's 64 lanes, and the group's 12
 // waves (3 per SIMD) are issue-bound -- the word search takes ~10 us on every group instead of ~8.5 us on
 // the groups that need it.
+#ifndef HA_TAIL_RSH
+#define HA_TAIL_RSH 1
+#endif
 #ifndef HA_TAIL_OVERLAP
 #define HA_TAIL_OVERLAP 0
 #endif
@@ -759,7 +766,7 @@ __device__ __forceinline__ void rs_known_cmd(const double* s, int tid, int id, d
 
 // One search iteration's device work for the block (role by blockIdx: RS_connected or a
 // 16-neighbour group).  Returns false (block-uniformly) when the block has nothing to do.
-template <int HWt, int NBGt>
+template <int HWt, int NBGt, bool RSH = false>
 __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, unsigned long long* hstp = nullptr) {
 // (diagnostics, -DHA_STAMP_CODE=1) phase stamps of the block's thread 0 into ha_step_kernel's slots 12..
 #define HSTAMP(i) if (HA_STAMP_CODE && hstp) __hip_atomic_store(hstp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -831,7 +838,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     transform1(node, A.sc + 3 * k, t);
     regulate(P, t, nb);
     const long long ix = encode(P, nb);
-    if (!rs && !(SPLIT && HA_TAIL_OVERLAP) && A.dnid) hit = ix > 0 && ix < A.C ? A.dnid[(size_t)s * A.C + ix] : -1;
+    if (!rs && !RSH && !(SPLIT && HA_TAIL_OVERLAP) && A.dnid) hit = ix > 0 && ix < A.C ? A.dnid[(size_t)s * A.C + ix] : -1;
     st_out(A.coherent, R.nb + 3 * k, nb[0]);
     st_out(A.coherent, R.nb + 3 * k + 1, nb[1]);
     st_out(A.coherent, R.nb + 3 * k + 2, nb[2]);
@@ -854,12 +861,12 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     if (__double_as_longlong(m * P.res[2]) == __double_as_longlong(node[2]) && m >= A.pt_mlo && m < A.pt_mlo + A.pt_nm)
       tabm = (int)m - A.pt_mlo;
   }
-  auto sweep = [&](int npose) {
+  auto sweep = [&](int npose, int nthr = 64 * HWt) {
     double nsn = 0.0, ncs = 1.0;
     if (!rs) mpj_sincos_bl(node[2], &nsn, &ncs);
     const int parts = SPLIT ? 2 * nw : 1;
     const int total = (rs ? npose : nk * npose) * parts;
-    for (int t = tid; t < total; t += HT) {
+    for (int t = tid; t < total; t += nthr) {
       const int tp = SPLIT ? t / parts : t, part = SPLIT ? t - tp * parts : 0;
       const int jn = rs ? 0 : tp / npose, jp = rs ? tp : tp - jn * npose;
       if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
@@ -1006,6 +1013,58 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     HTIME(4);
     sweep(n > 5 ? (n - 1) / 5 + 1 : 1);  // block_collision_check on poses 1:5:end
     HTIME(5);
+  } else if (RSH) {
+    // tail shape, rs_heuristic in word units (IterArgs::hp_c): waves 0 .. HWt-4 sweep the group's own
+    // neighbours; waves HWt-3 .. HWt-1 each evaluate one Reeds-Shepp word, 3c+1 .. 3c+3, for the 16 neighbours
+    // 16g .. 16g+15 (g = (item-1)/4, c = (item-1)%4; 64 lanes = 16 neighbours x 4 variants, every lane used),
+    // whatever the sweep finds.  Per SIMD at most one such wave: the word chains run side by side on the
+    // scene's 16 group CUs (a group's 12-wave word search with 16 lanes per word was issue-bound, ~8.5 us).
+    // The scene's bookkeeping combines the four word chunks of each neighbour (rs_before is a total order).
+    static_assert(HWt >= 4, "three word waves beside the sweep");
+    constexpr int SWT = 64 * (HWt - 3);
+    const int g = (item - 1) >> 2, c = (item - 1) & 3;
+    const int npose = P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1;
+    if (tid < SWT) {
+      sweep(npose, SWT);
+    } else {
+      const int w = 3 * c + ((tid - SWT) >> 6) + 1;  // wave-uniform
+      const int k = min(16 * g + (lane >> 2), P.n_prim - 1);
+      double t[3], nb[3], ns[3], q[3];
+      transform1(node, A.sc + 3 * k, t);  // the owner group's operations: the same regulated state
+      regulate(P, t, nb);
+      change_basis(nb, goal, P.minR, ns);
+      rs_variant(ns, lane & 3, q);
+      const RsPre Rp = rs_pre(q);
+      double bc = rs_word(w, Rp, nullptr);
+      int bi = 4 * (w - 1) + (lane & 3);
+#pragma unroll
+      for (int o = 2; o >= 1; o >>= 1) {
+        const double ov = __shfl_xor(bc, o);
+        const int oi = __shfl_xor(bi, o);
+        if (rs_before(ov, oi, bc, bi)) { bc = ov; bi = oi; }
+      }
+      red_c[tid] = bc;
+      red_i[tid] = bi;
+    }
+    HSTAMP(13);
+    __syncthreads();
+    if (tid >= SWT && tid < SWT + 64 && (lane & 3) == 0) {  // the chunk's three words, per neighbour
+      double v = red_c[tid];
+      int ix = red_i[tid];
+#pragma unroll
+      for (int u = 1; u < 3; u++) {
+        const double ov = red_c[tid + 64 * u];
+        const int oi = red_i[tid + 64 * u];
+        if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; }
+      }
+      const int k = 16 * g + (lane >> 2);
+      if (k < P.n_prim) {
+        st_out(A.coherent, A.hp_c + ((size_t)s * P.n_prim + k) * 4 + c, v);
+        st_out(A.coherent, A.hp_i + ((size_t)s * P.n_prim + k) * 4 + c, ix);
+      }
+    }
+    HSTAMP(14);
+    HSTAMP(15);
   } else if (SPLIT && HA_TAIL_OVERLAP) {
     // tail shape (latency-bound: CUs to spare, one scene's chain): rs_heuristic of every neighbour of the
     // group, whether or not FindNewNode will read it, without waiting for the collision sweep; the sweep
@@ -1058,8 +1117,10 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   } else if (tid < 64 && (lane & 3) == 0 && j < nk) {
     const int fr = g_ix[j] != 0 && g_free[j];
     st_out(A.coherent, R.fr + k0 + j, (unsigned char)fr);
-    st_out(A.coherent, R.h + k0 + j, fr ? cb * P.minR : 0.0);
-    if (A.hw) st_out(A.coherent, A.hw + (size_t)s * P.n_prim + k0 + j, fr ? best : -1);
+    if (!RSH) {  // (RSH: the bookkeeping forms h and the winner from the word chunks)
+      st_out(A.coherent, R.h + k0 + j, fr ? cb * P.minR : 0.0);
+      if (A.hw) st_out(A.coherent, A.hw + (size_t)s * P.n_prim + k0 + j, fr ? best : -1);
+    }
   }
   return true;
 }
@@ -1724,7 +1785,7 @@ struct BookRec {
 // FindNewNode + popfirst! for scene b on an NT-thread block (ha_book without its termination branch):
 // the neighbour records are read agent-coherently; the node count, the pop count and pop_seq go to the
 // scene's record (Q.rec) for the finisher instead of the scene's counters.
-template <int NT>
+template <int NT, bool RSH = false>
 __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& Q, const IterArgs& A, int B, int it,
                                                 int b, unsigned long long* stp = nullptr) {
 #define BSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -1749,8 +1810,25 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
     const size_t q = (size_t)b * np + tid;
     ix = ld_ag(A.idx + q);
     frk = ld_ag(A.fr + q);
-    hk = ld_ag(A.h + q);
-    if (A.hw) hwk = ld_ag(A.hw + q);
+    if (RSH) {  // rs_heuristic from its four word chunks (ha_iter_body's RSH units): the least (cost, id)
+      double cv[4];
+      int ci[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        cv[c] = ld_ag(A.hp_c + q * 4 + c);
+        ci[c] = ld_ag(A.hp_i + q * 4 + c);
+      }
+      double v = cv[0];
+      int id = ci[0];
+#pragma unroll
+      for (int c = 1; c < 4; c++)
+        if (rs_before(cv[c], ci[c], v, id)) { v = cv[c]; id = ci[c]; }
+      hk = v * P.minR;  // rs_heuristic = opt_cost * minR (:365-367), as the groups form it
+      hwk = id;
+    } else {
+      hk = ld_ag(A.h + q);
+      if (A.hw) hwk = ld_ag(A.hw + q);
+    }
     nb0 = ld_ag(A.nb + 3 * q);
     nb1 = ld_ag(A.nb + 3 * q + 1);
     nb2 = ld_ag(A.nb + 3 * q + 2);
@@ -1956,7 +2034,7 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
 #define HA_WPE_TAIL 1
 #endif
 constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 17;  // [6..11]: bookkeeping phases; [12..16]: block body phases
-template <int HWt, int NBGt>
+template <int HWt, int NBGt, bool RSH = false>
 __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == 4 ? HA_WPE_FULL : HA_WPE_TAIL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
   __shared__ int role;
   unsigned long long* stp = nullptr;
@@ -1966,7 +2044,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int per = 1 + (P.n_prim + NBGt - 1) / NBGt;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
-  if (!ha_iter_body<HWt, NBGt>(P, A, stp)) return;  // block-uniform: no work for this block (not counted)
+  if (!ha_iter_body<HWt, NBGt, RSH>(P, A, stp)) return;  // block-uniform: no work for this block (not counted)
   const int s = A.scene_of ? A.scene_of[slot] : slot;
   ha_stores_done();  // this thread's records acknowledged before the block's ticket
   __syncthreads();
@@ -1995,7 +2073,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   // block is running and publishes without waiting on anything).
   long long* rc = Q.rec + (size_t)RC_N * s;
   if (r == 1) {
-    const BookRec br = ha_book_spec<64 * HWt>(P, Q, A, B, it, s, stp);
+    const BookRec br = ha_book_spec<64 * HWt, RSH>(P, Q, A, B, it, s, stp);
     if (!HA_FIN_SHORTCUT) {  // (A/B) always publish the record first
       if (threadIdx.x == 0) {
 #pragma unroll
@@ -2554,6 +2632,14 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   for (int i = 0; i < NCK; i++) MP_HIP(ctx, hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   auto cleanup = [&] { for (int i = 0; i < NCK; i++) hipEventDestroy(ev[i]); };
   const int per = 1 + (np + NBG - 1) / NBG, per_tail = 1 + (np + NBG_TAIL - 1) / NBG_TAIL;
+  // the tail's rs_heuristic word units (ha_iter_body RSH): group g·4 + c holds neighbours 16g.. and word chunk
+  // c, so there must be a group for every (16-neighbour set, chunk) -- n_prim mod 16 in {0, 13, 14, 15} with
+  // 4 neighbours per group (62: yes).  (A/B) MPGPU_HA_TAIL_RSH=0: the groups' own word search.
+  static const bool rsh_env = !getenv("MPGPU_HA_TAIL_RSH") || atoi(getenv("MPGPU_HA_TAIL_RSH")) != 0;
+  const bool tail_rsh = HA_TAIL_RSH && rsh_env && !split && NBG_TAIL == 4 && per_tail - 1 >= 4 * ((np + 15) / 16);
+  A.hp_c = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * nB * np * 4);
+  A.hp_i = (int*)mp_ws(ctx, WS_IO12, sizeof(int) * nB * np * 4);
+  if (!A.hp_c || !A.hp_i) return MP_ERR_NOMEM;
   // iteration it >= 2 works on the compact list of scenes still live (written by the previous
   // bookkeeping launch, count on the device); the host sizes the grids by the last live count it has
   // seen (an upper bound: it only decreases) and switches to the tail shape once that many scenes
@@ -2583,8 +2669,12 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
       hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     } else if (tail) {
-      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)),
-                         dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
+      if (tail_rsh)
+        hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL, true>), dim3((unsigned)(known * per_tail)),
+                           dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
+      else
+        hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)),
+                           dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
     } else if (known * per <= mid_blocks) {
       hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG>), dim3((unsigned)(known * per)),
                          dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
