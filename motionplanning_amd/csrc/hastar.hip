@@ -125,7 +125,7 @@ __constant__ signed char kRsN[12] = {3, 3, 3, 3, 3, 4, 4, 4, 4, 4, 4, 5};
 #else
 #define RS_WORD_ATTR __forceinline__
 #endif
-__device__ RS_WORD_ATTR double rs_word(int w_, const RsPre& R, Cmd* c) {
+__device__ RS_WORD_ATTR double rs_word(int w_, const RsPre& R, Cmd* c, double* tuv = nullptr) {
   const int w = __builtin_amdgcn_readfirstlane(w_);  // wave-uniform word: scalar branches and table loads
   const double p = R.p;
   const bool useA = (w == 1) | (w == 3) | (w == 4) | (w == 5) | (w == 8) | (w == 9);
@@ -197,6 +197,11 @@ __device__ RS_WORD_ATTR double rs_word(int w_, const RsPre& R, Cmd* c) {
   else if (w <= 6) valid = rho <= 4;
   else if (w == 7) valid = (rho <= 6) && (0 <= u1) && (u1 <= 1);
   else valid = rho >= 4;
+  if (tuv) {  // the word's segment lengths: with (w, variant) they determine its commands (cmd_from_tuv)
+    tuv[0] = t;
+    tuv[1] = u;
+    tuv[2] = v;
+  }
   if (c) {
     const int wi = w - 1;
     c->n = kRsN[wi];
@@ -234,6 +239,15 @@ __device__ __forceinline__ void rs_variant(const double* s, int var, double* q) 
   else if (var == 3) { q[0] = -q[0]; q[1] = -q[1]; }  // reverse
 }
 
+// changeBasis with sin/cos of init's heading given (the lattice-heading tables)
+__device__ __forceinline__ void change_basis_sc(const double* init, const double* term, double minR, double s0,
+                                                double c0, double* out) {
+  const double p0 = init[2], pg = term[2];
+  const double dx = (term[0] - init[0]) / minR, dy = (term[1] - init[1]) / minR;
+  out[0] = dx * c0 + dy * s0;
+  out[1] = -dx * s0 + dy * c0;
+  out[2] = pg - p0;
+}
 __device__ __forceinline__ void change_basis(const double* init, const double* term, double minR, double* out) {
   const double p0 = init[2], pg = term[2];
   const double dx = (term[0] - init[0]) / minR, dy = (term[1] - init[1]) / minR;
@@ -508,20 +522,29 @@ __device__ __forceinline__ void regulate(const HaDev& P, const double* s, double
   o[2] = mpj_round(psi / P.res[2]) * P.res[2];
 }
 
-__device__ __forceinline__ long long encode(const HaDev& P, const double* s) {
+// Encode's heading index (hybrid_astar_utils.jl:316-350): a function of the heading alone
+__device__ __forceinline__ double encode_pid(const HaDev& P, double h) {
   const double* b = P.sb;
-  double x = s[0], y = s[1], psi = mpj_modpi_bl(s[2]);
+  double psi = mpj_modpi_bl(h);
+  psi = __builtin_fmax(__builtin_fmin(psi, b[5]), b[4]);
+  return mpj_round((psi - b[4]) / P.res[2]) + 1;
+}
+// Encode with the heading index given
+__device__ __forceinline__ long long encode_p(const HaDev& P, const double* s, double pid) {
+  const double* b = P.sb;
+  double x = s[0], y = s[1];
   x = __builtin_fmax(__builtin_fmin(x, b[1]), b[0]);
   y = __builtin_fmax(__builtin_fmin(y, b[3]), b[2]);
-  psi = __builtin_fmax(__builtin_fmin(psi, b[5]), b[4]);
   const double xid = mpj_round((x - b[0]) / P.res[0]) + 1;
   const double yid = mpj_round((y - b[2]) / P.res[1]) + 1;
-  const double pid = mpj_round((psi - b[4]) / P.res[2]) + 1;
   const double ynum = mpj_round((b[3] - b[2]) / P.res[1]) + 1;
   const double pnum = mpj_round((b[5] - b[4]) / P.res[2]) + 1;
   const double idx = (xid - 1) * ynum * pnum + (yid - 1) * pnum + pid;
   if (s[0] < b[0] || s[0] > b[1] || s[1] < b[2] || s[1] > b[3]) return 0;
   return (long long)idx;
+}
+__device__ __forceinline__ long long encode(const HaDev& P, const double* s) {
+  return encode_p(P, s, encode_pid(P, s[2]));
 }
 
 struct IterArgs {
@@ -571,10 +594,20 @@ struct IterArgs {
   // chunks: the chunk's best (cost, candidate id), [B][n_prim][4]; the bookkeeping combines them
   double* hp_c;
   int* hp_i;
+  double* hp_t;          // [B][n_prim][4][3] the chunk winner's (t, u, v) (its RS_connected commands)
+  const double* node_tuv;  // [B][3] the popped node's stored (t, u, v) when node_rw has RW_TUV
   // (mp_ha_plan) the pose table: PoseTrig of every swept primitive pose (1:5:n_col) for every lattice
   // heading m·res[2], m = pt_mlo .. pt_mlo + pt_nm - 1: [pt_nm][n_prim][pt_nsw][4]; nullptr = compute
   const double* ptab;
   int pt_mlo, pt_nm, pt_nsw;
+  // (mp_ha_plan) lattice-heading tables over the same m: htn [pt_nm][2] = sin, cos of m·res[2] (transform's
+  // and changeBasis's of the node); htk [pt_nm][n_prim][4] = neighbour k's regulated heading, its sin and cos
+  // (changeBasis from the neighbour), Encode's heading index -- the heading-only terms of FindNewNode's
+  // transform / regulate_states / Encode (:396-405), nullptr = compute
+  const double* htn;
+  const double* htk;
+  int no_pre;  // (A/B, MPGPU_HA_PRESCAN=0) the prescan block only marks its record stale: the bookkeeping scans
+  int no_tuv;  // (A/B, MPGPU_HA_TUV=0) nodes keep only their winner id: RS_connected evaluates its word
 };
 
 // Agent-coherent relaxed stores / loads (global_store / global_load with the sc1 policy: they reach
@@ -593,6 +626,40 @@ template <class T>
 __device__ __forceinline__ void st_out(bool coh, T* p, T v) {
   if (coh) st_ag(p, v);
   else *p = v;
+}
+
+// the lattice-heading index of heading h into the per-plan tables (IterArgs::htn), or -1 when h is not
+// m·res[2] bit for bit for a tabulated m (e.g. an unregulated start) -- then every term is computed
+__device__ __forceinline__ int lattice_m(const HaDev& P, const IterArgs& A, double h) {
+  if (!A.htn) return -1;
+  const double m = mpj_round(h / P.res[2]);
+  if (__double_as_longlong(m * P.res[2]) == __double_as_longlong(h) && m >= A.pt_mlo && m < A.pt_mlo + A.pt_nm)
+    return (int)m - A.pt_mlo;
+  return -1;
+}
+// transform + regulate_states + Encode of neighbour k of `node` (:396-405), the heading terms from the
+// lattice tables when tabm >= 0 (the same values: the tables hold what these operations give); if sn, also
+// sin / cos of the regulated heading (changeBasis from the neighbour)
+__device__ __forceinline__ long long expand_nb(const HaDev& P, const IterArgs& A, const double* node, int tabm, int k,
+                                               double* nb, double* sn = nullptr, double* cn = nullptr) {
+  double t[3];
+  if (tabm >= 0) {
+    const double* hn = A.htn + 2 * tabm;
+    const double* hk = A.htk + ((size_t)tabm * P.n_prim + k) * 4;
+    transform_cs(node, hn[1], hn[0], A.sc + 3 * k, t);
+    nb[0] = mpj_round(t[0] / P.res[0]) * P.res[0];
+    nb[1] = mpj_round(t[1] / P.res[1]) * P.res[1];
+    nb[2] = hk[0];
+    if (sn) {
+      *sn = hk[1];
+      *cn = hk[2];
+    }
+    return encode_p(P, nb, hk[3]);
+  }
+  transform1(node, A.sc + 3 * k, t);
+  regulate(P, t, nb);
+  if (sn) mpj_sincos_bl(nb[2], sn, cn);
+  return encode(P, nb);
 }
 
 // output addressing: per scene
@@ -764,6 +831,30 @@ __device__ __forceinline__ void rs_known_cmd(const double* s, int tid, int id, d
   }
 }
 
+// A node's stored RS_connected commands (IterArgs::node_rw with RW_TUV): candidate id = 4(w-1) + variant, the
+// word's (t, u, v) as rs_word computed them for that variant, ok = its cost < Inf.  The commands rs_known_cmd's
+// winning lane writes, from the word tables, without evaluating the word again.
+enum { RW_ID = 0xff, RW_TUV = 1 << 8, RW_OK = 1 << 9 };
+__device__ __forceinline__ void cmd_from_tuv(int rw, const double* tuv, double* cmd_out) {
+  const int id = rw & RW_ID, wi = id / 4, var = id & 3;
+  const int n = (rw & RW_OK) ? kRsN[wi] : 0;
+#pragma unroll
+  for (int r = 0; r < 5; r++) {
+    double ge = 0.0, st = 0.0, tr = 0.0;
+    if (r < n) {
+      const int code = kRsTr[wi][r];
+      tr = code == 0 ? tuv[0] : code == 1 ? tuv[1] : code == 2 ? tuv[2] : PI2;
+      ge = kRsGe[wi][r];
+      st = kRsSt[wi][r];
+      if (var == 1 || var == 3) ge = -1 * ge;
+      if (var == 2 || var == 3) st = -1 * st;
+    }
+    cmd_out[r * 3 + 0] = tr;
+    cmd_out[r * 3 + 1] = ge;
+    cmd_out[r * 3 + 2] = st;
+  }
+}
+
 // One search iteration's device work for the block (role by blockIdx: RS_connected or a
 // 16-neighbour group).  Returns false (block-uniformly) when the block has nothing to do.
 template <int HWt, int NBGt, bool RSH = false>
@@ -780,12 +871,14 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   __shared__ double path_s[MAXPATH * 3];
   __shared__ double red_c[HT];
   __shared__ int red_i[HT];
+  __shared__ double red_t[RSH ? 3 : 1][RSH ? 192 : 1];  // RSH units: the word waves' (t, u, v)
   __shared__ double g_nb[NBG][3];
+  __shared__ double g_sc[NBG][2];  // sin, cos of the regulated heading (changeBasis of rs_heuristic)
   __shared__ long long g_ix[NBG];
   __shared__ int g_free[NBG];
   __shared__ int g_need[NBG];
   __shared__ int sh_n;
-  const int per = 1 + (P.n_prim + NBG - 1) / NBG;
+  const int per = 1 + (P.n_prim + NBG - 1) / NBG + (RSH ? 1 : 0);  // RSH: the prescan block is the last item
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
   // the live count and the slot's scene are independent loads (slot < the grid's bound <= B keeps the
   // list read in bounds); a scene on the bookkeeping's list (n_live set) is live, so its flag is not
@@ -832,12 +925,15 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   // one per thread, and a neighbour group evaluates rs_heuristic for all its neighbours at once
   constexpr bool SPLIT = HWt == HW_TAIL;
   int hit = -1;  // (groups with a Dict) the neighbour's node id in the scene's Dict
+  // the expanded node's heading is a lattice heading m·res[2] (bit for bit; every regulated state's is): its
+  // neighbours' heading terms and its poses' come from the per-plan tables
+  const int tabm = lattice_m(P, A, node[2]);
   if (tid < nk) {  // transform + regulate_states + Encode of the group's neighbours (:396-405)
     const int k = k0 + tid;
-    double t[3], nb[3];
-    transform1(node, A.sc + 3 * k, t);
-    regulate(P, t, nb);
-    const long long ix = encode(P, nb);
+    double nb[3], sn, cn;
+    const long long ix = expand_nb(P, A, node, tabm, k, nb, &sn, &cn);
+    g_sc[tid][0] = sn;
+    g_sc[tid][1] = cn;
     if (!rs && !RSH && !(SPLIT && HA_TAIL_OVERLAP) && A.dnid) hit = ix > 0 && ix < A.C ? A.dnid[(size_t)s * A.C + ix] : -1;
     st_out(A.coherent, R.nb + 3 * k, nb[0]);
     st_out(A.coherent, R.nb + 3 * k + 1, nb[1]);
@@ -853,17 +949,16 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   HSTAMP(12);
   __syncthreads();
   const int j = lane >> 2;
-  // the expanded node's heading is a lattice heading m·res[2] (bit for bit; every regulated state's is):
-  // its poses' heading terms come from the pose table
-  int tabm = -1;
-  if (!rs && A.ptab) {
-    const double m = mpj_round(node[2] / P.res[2]);
-    if (__double_as_longlong(m * P.res[2]) == __double_as_longlong(node[2]) && m >= A.pt_mlo && m < A.pt_mlo + A.pt_nm)
-      tabm = (int)m - A.pt_mlo;
-  }
   auto sweep = [&](int npose, int nthr = 64 * HWt) {
     double nsn = 0.0, ncs = 1.0;
-    if (!rs) mpj_sincos_bl(node[2], &nsn, &ncs);
+    if (!rs) {
+      if (tabm >= 0) {
+        nsn = A.htn[2 * tabm];
+        ncs = A.htn[2 * tabm + 1];
+      } else {
+        mpj_sincos_bl(node[2], &nsn, &ncs);
+      }
+    }
     const int parts = SPLIT ? 2 * nw : 1;
     const int total = (rs ? npose : nk * npose) * parts;
     for (int t = tid; t < total; t += nthr) {
@@ -880,7 +975,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
         transform_cs(node, ncs, nsn, A.pc + ((size_t)(k0 + jn) * P.n_col + jp * 5) * 3, q);
       }
       int fr;
-      if (tabm >= 0) {  // block-uniform
+      if (!rs && tabm >= 0 && A.ptab) {  // block-uniform (the RS path's poses have their own headings)
         const double2* e =
             reinterpret_cast<const double2*>(A.ptab + (((size_t)tabm * P.n_prim + k0 + jn) * A.pt_nsw + jp) * 4);
         const double2 a = e[0], c = e[1];
@@ -899,10 +994,15 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     // allpath + findmin: RS_connected's optimal command from the popped node
     double ns[3];
     const int known = A.node_rw ? A.node_rw[s] : -1;  // the popped node's stored rs_heuristic winner
-    change_basis(node, goal, P.minR, ns);
+    if (tabm >= 0)
+      change_basis_sc(node, goal, P.minR, A.htn[2 * tabm], A.htn[2 * tabm + 1], ns);
+    else
+      change_basis(node, goal, P.minR, ns);
     HTIME(2);
     HSTAMP(12);
-    if (known >= 0 && known < 48)  // block-uniform
+    if (known >= 0 && (known & RW_TUV)) {  // block-uniform: the commands stored at the node's creation
+      if (tid == 0) cmd_from_tuv(known, A.node_tuv + 3 * s, cmd);
+    } else if (known >= 0 && known < 48)
       rs_known_cmd(ns, tid, known, cmd);
     else
       cb = rs_best_split<true, HWt>(ns, tid, &best, red_c, red_i, cmd);
@@ -1029,38 +1129,51 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     } else {
       const int w = 3 * c + ((tid - SWT) >> 6) + 1;  // wave-uniform
       const int k = min(16 * g + (lane >> 2), P.n_prim - 1);
-      double t[3], nb[3], ns[3], q[3];
-      transform1(node, A.sc + 3 * k, t);  // the owner group's operations: the same regulated state
-      regulate(P, t, nb);
-      change_basis(nb, goal, P.minR, ns);
+      double nb[3], ns[3], q[3], sn, cn;
+      expand_nb(P, A, node, tabm, k, nb, &sn, &cn);  // the owner group's operations: the same regulated state
+      change_basis_sc(nb, goal, P.minR, sn, cn, ns);
       rs_variant(ns, lane & 3, q);
       const RsPre Rp = rs_pre(q);
-      double bc = rs_word(w, Rp, nullptr);
+      double tv[3];
+      double bc = rs_word(w, Rp, nullptr, tv);
       int bi = 4 * (w - 1) + (lane & 3);
 #pragma unroll
       for (int o = 2; o >= 1; o >>= 1) {
         const double ov = __shfl_xor(bc, o);
         const int oi = __shfl_xor(bi, o);
-        if (rs_before(ov, oi, bc, bi)) { bc = ov; bi = oi; }
+        double ot[3];
+#pragma unroll
+        for (int e = 0; e < 3; e++) ot[e] = __shfl_xor(tv[e], o);
+        if (rs_before(ov, oi, bc, bi)) {
+          bc = ov;
+          bi = oi;
+#pragma unroll
+          for (int e = 0; e < 3; e++) tv[e] = ot[e];
+        }
       }
       red_c[tid] = bc;
       red_i[tid] = bi;
+#pragma unroll
+      for (int e = 0; e < 3; e++) red_t[e][tid - SWT] = tv[e];
     }
     HSTAMP(13);
     __syncthreads();
     if (tid >= SWT && tid < SWT + 64 && (lane & 3) == 0) {  // the chunk's three words, per neighbour
       double v = red_c[tid];
-      int ix = red_i[tid];
+      int ix = red_i[tid], wu = 0;
 #pragma unroll
       for (int u = 1; u < 3; u++) {
         const double ov = red_c[tid + 64 * u];
         const int oi = red_i[tid + 64 * u];
-        if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; }
+        if (rs_before(ov, oi, v, ix)) { v = ov; ix = oi; wu = u; }
       }
       const int k = 16 * g + (lane >> 2);
       if (k < P.n_prim) {
-        st_out(A.coherent, A.hp_c + ((size_t)s * P.n_prim + k) * 4 + c, v);
-        st_out(A.coherent, A.hp_i + ((size_t)s * P.n_prim + k) * 4 + c, ix);
+        const size_t q = ((size_t)s * P.n_prim + k) * 4 + c;
+        st_out(A.coherent, A.hp_c + q, v);
+        st_out(A.coherent, A.hp_i + q, ix);
+#pragma unroll
+        for (int e = 0; e < 3; e++) st_out(A.coherent, A.hp_t + 3 * q + e, red_t[e][tid - SWT + 64 * wu]);
       }
     }
     HSTAMP(14);
@@ -1070,7 +1183,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     // group, whether or not FindNewNode will read it, without waiting for the collision sweep; the sweep
     // runs between each wave's Reeds-Shepp word and the cross-wave reduction, so the two overlap
     double ns[3];
-    change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
+    const int jj = j < nk ? j : 0;
+    change_basis_sc(g_nb[jj], goal, P.minR, g_sc[jj][0], g_sc[jj][1], ns);
     const int npose = P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1;
     cb = rs_best_split<false, HWt>(ns, tid, &best, red_c, red_i, nullptr, [&] { sweep(npose); });
     HSTAMP(13);
@@ -1096,7 +1210,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     for (int q = 0; q < nk; q++) any |= (g_ix[q] != 0) & g_free[q] & g_need[q];
     if (any) {  // block-uniform
       double ns[3];
-      change_basis(g_nb[j < nk ? j : 0], goal, P.minR, ns);
+      const int jj = j < nk ? j : 0;
+      change_basis_sc(g_nb[jj], goal, P.minR, g_sc[jj][0], g_sc[jj][1], ns);
       HTIME(2);
       cb = rs_best_split<false, HWt>(ns, tid, &best, red_c, red_i);
       HSTAMP(15);
@@ -1253,6 +1368,31 @@ __global__ __launch_bounds__(256) void ha_pose_table_kernel(HaDev P, const doubl
   o[3] = T.cy;
 }
 
+// the lattice-heading tables (IterArgs::htn / htk): thread = (m, neighbour k)
+__global__ __launch_bounds__(256) void ha_head_table_kernel(HaDev P, const double* sc, int mlo, int nm, double* htn,
+                                                            double* htk) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= nm * P.n_prim) return;
+  const int k = t % P.n_prim, m = t / P.n_prim;
+  const double head = (double)(mlo + m) * P.res[2];
+  if (k == 0) {
+    double sh, ch;
+    mpj_sincos_bl(head, &sh, &ch);
+    htn[2 * m] = sh;
+    htn[2 * m + 1] = ch;
+  }
+  const double t2 = sc[3 * k + 2] + head;  // transform's heading (o[2] = q[2] + node[2])
+  const double psi = mpj_modpi_bl(t2);       // regulate_states
+  const double nb2 = mpj_round(psi / P.res[2]) * P.res[2];
+  double sn, cn;
+  mpj_sincos_bl(nb2, &sn, &cn);
+  double* o = htk + (size_t)t * 4;
+  o[0] = nb2;
+  o[1] = sn;
+  o[2] = cn;
+  o[3] = encode_pid(P, nb2);
+}
+
 __global__ __launch_bounds__(64) void ha_wall_kernel(HaDev P, int B, const double* walls, double* wtab) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   if (i >= B * P.n_walls) return;
@@ -1307,7 +1447,14 @@ struct HaSearch {
   int* rw;               // [B][C] per node id: rs_heuristic's winning candidate at the node's creation (-1: unknown)
   int* orw;              // [B][C] open entries: the same, so popfirst! hands it to RS_connected with the state
   int* node_rw;          // [2][B] popped node's winner, double-buffered like node
+  double* tuv;           // [B][C][3] per node id: the winner's (t, u, v) when rw has RW_TUV
+  double* otuv;          // [B][C][3] open entries: the same
+  double* node_tuv;      // [2][B][3] popped node's, double-buffered like node
+  long long* pre;        // [B][PRE_W] (RSH tail) the prescan's record: popfirst!'s K least entries before FindNewNode
 };
+// prescan record: [0] iteration tag, [1] kc = min(K, n_open), then K entries of 13 words: f (bits), seq, position,
+// node id, g (bits), Encode index, state (3, bits), rw, (t, u, v) (3, bits)
+constexpr int PRE_K = 4, PRE_E = 13, PRE_W = 2 + PRE_E * PRE_K;
 enum { SI_NNODES = 0, SI_NOPEN, SI_LOOP, SI_CUR, SI_ACTIVE, SI_FOUND, SI_NSTATES, SI_RSLEN, SI_N };
 
 // open-list order: a before c (Julia isless on f, then list position)
@@ -1353,9 +1500,11 @@ __device__ __forceinline__ void key_min_dpp(double& f, long long& sq, int& p) {
 // pop_seq are written here (ha_init_kernel, ha_book_kernel), else they are left to the scene's finisher
 // in ha_step_kernel and the popped Encode index is returned in *iw_out (lane 0 of wave 0).
 constexpr int BKT = 256;
-template <int NT>
+// TUV: the open entries carry the (t, u, v) of RSH-tail nodes (only the tail's launches can meet them: the shapes
+// go full width -> tail, never back)
+template <int NT, bool TUV = true>
 __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_open, int loop, int tid,
-                                       double* node_out, int* rw_out, bool direct, long long* iw_out,
+                                       double* node_out, int* rw_out, double* tuv_out, bool direct, long long* iw_out,
                                        unsigned long long* stp = nullptr) {
   static_assert(NT % 64 == 0, "whole waves");
   __shared__ double r_f[NT / 64];
@@ -1364,12 +1513,13 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   __shared__ double r_pay[NT / 64][5];  // the wave winner's entry: g, Encode index, state
   __shared__ int r_id[NT / 64];
   __shared__ int r_rw[NT / 64];
+  __shared__ double r_tuv[NT / 64][3];
   const size_t base = (size_t)b * Q.C;
   if (n_open == 0 || loop >= Q.mp) return false;
   const int lane = tid & 63, wave = tid >> 6;
   const int last = n_open - 1;
   // the last entry (moved into the winner's place) does not depend on the scan: loaded first
-  double fl = 0.0, gl = 0.0, stl = 0.0;
+  double fl = 0.0, gl = 0.0, stl = 0.0, tuvl = 0.0;
   long long sl = 0, il = 0;
   int lid = 0, rwl = -1;
   if (tid < 64) {
@@ -1379,13 +1529,16 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
     il = Q.oix[base + last];
     lid = Q.oid[base + last];
     rwl = Q.orw[base + last];
-    if (lane < 3) stl = Q.ost[(base + last) * 3 + lane];
+    if (lane < 3) {
+      stl = Q.ost[(base + last) * 3 + lane];
+      if (TUV) tuvl = Q.otuv[(base + last) * 3 + lane];
+    }
   }
   double bf = __builtin_inf();
   long long bs = 0x7fffffffffffffffLL;
   int bp = -1;
   int pid = 0, prw = -1;
-  double pg = 0.0, pix = 0.0, p0s = 0.0, p1s = 0.0, p2s = 0.0;
+  double pg = 0.0, pix = 0.0, p0s = 0.0, p1s = 0.0, p2s = 0.0, pt0 = 0.0, pt1 = 0.0, pt2 = 0.0;
   for (int p0 = tid; p0 < n_open; p0 += 4 * NT) {
     double fv[4];
     long long sv[4];
@@ -1411,6 +1564,11 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
     p0s = Q.ost[(base + bp) * 3];
     p1s = Q.ost[(base + bp) * 3 + 1];
     p2s = Q.ost[(base + bp) * 3 + 2];
+    if (TUV) {
+      pt0 = Q.otuv[(base + bp) * 3];
+      pt1 = Q.otuv[(base + bp) * 3 + 1];
+      pt2 = Q.otuv[(base + bp) * 3 + 2];
+    }
   }
   if (HA_STAMP_CODE && stp) {  // diagnostics: the scan's loads returned (the payload waited for)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1441,6 +1599,11 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   if (bp >= 0 && own == bp) {  // the one lane that scanned the wave's winning position
     r_id[wave] = pid;
     r_rw[wave] = prw;
+    if (TUV) {
+      r_tuv[wave][0] = pt0;
+      r_tuv[wave][1] = pt1;
+      r_tuv[wave][2] = pt2;
+    }
     r_pay[wave][0] = pg;
     r_pay[wave][1] = pix;
     r_pay[wave][2] = p0s;
@@ -1475,6 +1638,7 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
   const double gw = r_pay[ww][0];
   const long long iw = __double_as_longlong(r_pay[ww][1]);
   const double stw = lane < 3 ? r_pay[ww][2 + lane] : 0.0;
+  const double tuvw = TUV && lane < 3 ? r_tuv[ww][lane] : 0.0;
   if (bp != last) {
     if (lane == 0) {
       Q.of[base + bp] = fl;
@@ -1485,7 +1649,10 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
       Q.orw[base + bp] = rwl;
       Q.pos[base + lid] = bp;
     }
-    if (lane < 3) Q.ost[(base + bp) * 3 + lane] = stl;
+    if (lane < 3) {
+      Q.ost[(base + bp) * 3 + lane] = stl;
+      if (TUV) Q.otuv[(base + bp) * 3 + lane] = tuvl;
+    }
   }
   if (lane == 0) {
     Q.pos[base + id] = -1;
@@ -1501,7 +1668,10 @@ __device__ __forceinline__ bool ha_pop(const HaSearch& Q, int B, int b, int n_op
     Q.cur_ix[b] = iw;
     rw_out[b] = rww;
   }
-  if (lane < 3) node_out[3 * b + lane] = stw;
+  if (lane < 3) {
+    node_out[3 * b + lane] = stw;
+    if (TUV) tuv_out[3 * b + lane] = tuvw;
+  }
   return true;
 }
 
@@ -1536,7 +1706,7 @@ __global__ __launch_bounds__(256) void ha_init_kernel(HaDev P, HaSearch Q, int B
     if (si >= 0 && si < Q.C) Q.nid[base + si] = 0;
   }
   __syncthreads();
-  const bool go = ha_pop<256>(Q, B, b, 1, 0, tid, Q.node, Q.node_rw, true, nullptr);  // node buffer 0: iteration 1 reads it
+  const bool go = ha_pop<256>(Q, B, b, 1, 0, tid, Q.node, Q.node_rw, Q.node_tuv, true, nullptr);  // node buffer 0: iteration 1 reads it
   if (tid == 0) Q.sc_i[SI_ACTIVE * B + b] = go;
 }
 
@@ -1562,6 +1732,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   long long ix = 0;
   int frk = 0, hwk = -1;
   double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
+  double tuvk[3] = {0.0, 0.0, 0.0};
   if (tid < np) {
     ix = A.idx[(size_t)b * np + tid];
     frk = A.fr[(size_t)b * np + tid];
@@ -1621,6 +1792,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   int hit = -1;
   double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
   int po = 0, drw = -1;
+  double dtuv[3] = {0.0, 0.0, 0.0};
   long long so0 = 0, io = 0;
   if (valid) {  // wave 0: the Dict entry of every valid lane (used by the first occurrences below)
     hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
@@ -1631,6 +1803,8 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
       so0 = Q.seq[base + hit];
       io = Q.index[base + hit];
       drw = Q.rw[base + hit];
+#pragma unroll
+      for (int e = 0; e < 3; e++) dtuv[e] = 0.0;  // (no RSH units in the split shape: no node has (t, u, v))
       dst0 = Q.st[(base + hit) * 3];
       dst1 = Q.st[(base + hit) * 3 + 1];
       dst2 = Q.st[(base + hit) * 3 + 2];
@@ -1653,6 +1827,7 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
     double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;  // the node's state and Encode index (its open entry)
     long long nix = ix;
     int nrw = hwk;  // the node's stored rs_heuristic winner (its open entry carries it)
+    double nt0 = tuvk[0], nt1 = tuvk[1], nt2 = tuvk[2];
     if (first) {
       th = __builtin_fmax(hk, 0.0);
       if (hk != hk) th = hk;
@@ -1664,6 +1839,9 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
         nst2 = dst2;
         nix = io;
         nrw = drw;
+        nt0 = dtuv[0];
+        nt1 = dtuv[1];
+        nt2 = dtuv[2];
         if (tg < gd) {
           if (po >= 0) {
             chg = true;
@@ -1738,7 +1916,8 @@ __device__ void ha_book(const HaDev& P, const HaSearch& Q, const IterArgs& A, in
   BTIME(6);
   const int n_open = s_nopen;
   // ---- next popfirst!
-  const bool go = ha_pop<BKT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B, true,
+  const bool go = ha_pop<BKT, false>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B,
+                            Q.node_tuv + (size_t)(it & 1) * 3 * B, true,
                             nullptr);
   BTIME(7);
   if (tid == 0) {
@@ -1789,7 +1968,8 @@ template <int NT, bool RSH = false>
 __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& Q, const IterArgs& A, int B, int it,
                                                 int b, unsigned long long* stp = nullptr) {
 #define BSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-  __shared__ int s_nopen, s_nnew;
+  __shared__ int s_nopen, s_nnew, s_merged;
+  __shared__ long long s_iw;
   __shared__ long long s_vix[64];
   __shared__ int s_dup[4][64];
   static_assert(NT >= 256, "the duplicate check below runs on four waves");
@@ -1806,25 +1986,36 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   long long ix = 0;
   int frk = 0, hwk = -1;
   double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
+  double tuvk[3] = {0.0, 0.0, 0.0};
   if (tid < np) {
     const size_t q = (size_t)b * np + tid;
     ix = ld_ag(A.idx + q);
     frk = ld_ag(A.fr + q);
     if (RSH) {  // rs_heuristic from its four word chunks (ha_iter_body's RSH units): the least (cost, id)
-      double cv[4];
+      double cv[4], ct[4][3];
       int ci[4];
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         cv[c] = ld_ag(A.hp_c + q * 4 + c);
         ci[c] = ld_ag(A.hp_i + q * 4 + c);
+#pragma unroll
+        for (int e = 0; e < 3; e++) ct[c][e] = ld_ag(A.hp_t + (q * 4 + c) * 3 + e);
       }
       double v = cv[0];
-      int id = ci[0];
+      int id = ci[0], wc = 0;
 #pragma unroll
       for (int c = 1; c < 4; c++)
-        if (rs_before(cv[c], ci[c], v, id)) { v = cv[c]; id = ci[c]; }
+        if (rs_before(cv[c], ci[c], v, id)) { v = cv[c]; id = ci[c]; wc = c; }
       hk = v * P.minR;  // rs_heuristic = opt_cost * minR (:365-367), as the groups form it
-      hwk = id;
+      // the winner and its (t, u, v): RS_connected's commands when this neighbour becomes a node and is popped
+      hwk = A.no_tuv ? id : id | RW_TUV | (v < __builtin_inf() ? RW_OK : 0);
+#pragma unroll
+      for (int e = 0; e < 3; e++) tuvk[e] = ct[0][e];
+#pragma unroll
+      for (int c = 1; c < 4; c++)
+        if (wc == c)
+#pragma unroll
+          for (int e = 0; e < 3; e++) tuvk[e] = ct[c][e];
     } else {
       hk = ld_ag(A.h + q);
       if (A.hw) hwk = ld_ag(A.hw + q);
@@ -1832,6 +2023,26 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
     nb0 = ld_ag(A.nb + 3 * q);
     nb1 = ld_ag(A.nb + 3 * q + 1);
     nb2 = ld_ag(A.nb + 3 * q + 2);
+  }
+  // (RSH) the prescan record (wave 0, one word per lane) and the last old open entry (lane f: field f), both
+  // read now so their latency hides behind the Dict loads and FindNewNode
+  long long recw = 0, lastw = 0;
+  if (RSH && tid < 64) {
+    if (lane < PRE_W) recw = ld_ag(Q.pre + (size_t)b * PRE_W + lane);
+    if (n_open0 > 0 && lane < PRE_E) {
+      const size_t L = base + n_open0 - 1;
+      switch (lane) {
+        case 0: lastw = __double_as_longlong(Q.of[L]); break;
+        case 1: lastw = Q.oseq[L]; break;
+        case 2: lastw = L - base; break;
+        case 3: lastw = Q.oid[L]; break;
+        case 4: lastw = __double_as_longlong(Q.og[L]); break;
+        case 5: lastw = Q.oix[L]; break;
+        case 6: case 7: case 8: lastw = __double_as_longlong(Q.ost[L * 3 + lane - 6]); break;
+        case 9: lastw = Q.orw[L]; break;
+        default: lastw = __double_as_longlong(Q.otuv[L * 3 + lane - 10]); break;
+      }
+    }
   }
   // duplicates: lane k of wave 0 is neighbour k; an earlier valid lane with the same Encode index makes
   // it one (the comparisons split over four waves, as in ha_book)
@@ -1853,6 +2064,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   int hit = -1;
   double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
   int po = 0, drw = -1;
+  double dtuv[3] = {0.0, 0.0, 0.0};
   long long so0 = 0, io = 0;
   if (valid) {
     hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
@@ -1863,6 +2075,8 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
       so0 = Q.seq[base + hit];
       io = Q.index[base + hit];
       drw = Q.rw[base + hit];
+#pragma unroll
+      for (int e = 0; e < 3; e++) dtuv[e] = RSH ? Q.tuv[(base + hit) * 3 + e] : 0.0;
       dst0 = Q.st[(base + hit) * 3];
       dst1 = Q.st[(base + hit) * 3 + 1];
       dst2 = Q.st[(base + hit) * 3 + 2];
@@ -1884,6 +2098,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
     double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;
     long long nix = ix;
     int nrw = hwk;  // the node's stored rs_heuristic winner (its open entry carries it)
+    double nt0 = tuvk[0], nt1 = tuvk[1], nt2 = tuvk[2];
     if (first) {
       th = __builtin_fmax(hk, 0.0);
       if (hk != hk) th = hk;
@@ -1895,6 +2110,9 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
         nst2 = dst2;
         nix = io;
         nrw = drw;
+        nt0 = dtuv[0];
+        nt1 = dtuv[1];
+        nt2 = dtuv[2];
         if (tg < gd) {
           if (po >= 0) {
             chg = true;
@@ -1934,6 +2152,11 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
         Q.st[q * 3 + 2] = nst2;
         Q.index[q] = ix;
         Q.rw[q] = nrw;
+        if (RSH) {
+          Q.tuv[q * 3] = nt0;
+          Q.tuv[q * 3 + 1] = nt1;
+          Q.tuv[q * 3 + 2] = nt2;
+        }
         if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
       }
       Q.g[q] = tg;
@@ -1949,6 +2172,11 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
         Q.oid[base + p] = id;
         Q.oix[base + p] = nix;
         Q.orw[base + p] = nrw;
+        if (RSH) {
+          Q.otuv[(base + p) * 3] = nt0;
+          Q.otuv[(base + p) * 3 + 1] = nt1;
+          Q.otuv[(base + p) * 3 + 2] = nt2;
+        }
         Q.ost[(base + p) * 3] = nst0;
         Q.ost[(base + p) * 3 + 1] = nst1;
         Q.ost[(base + p) * 3 + 2] = nst2;
@@ -1961,14 +2189,166 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
       s_nopen = n_open;
       s_nnew = nn0 + n_new;
     }
+    if (RSH) {
+      // ---- popfirst! merged from the prescan (ha_prescan): the least of the record entries FindNewNode left
+      // alone, the changed entries (new keys, same positions) and the appended ones
+      const int tag = (int)readlane_l(recw, 0), kc = (int)readlane_l(recw, 1);
+      // this lane's own candidate: a changed or appended entry
+      const int myp = chg ? po : app ? n_open0 + __popcll(m_app & below) : -1;
+      double bf = tf;
+      long long bs = nseq;
+      int bp = myp;
+      int bl = myp >= 0 ? lane : -1;  // the lane holding the winner (-1: a record entry)
+      // the record's entries FindNewNode left alone (wave-uniform)
+      bool any_left = false;
+      double rf = 0.0;
+      long long rsq = 0;
+      int rp = -1, re = -1;
+#pragma unroll
+      for (int e = 0; e < PRE_K; e++) {
+        if (e >= kc) break;
+        const int pe = (int)readlane_l(recw, 2 + PRE_E * e + 2);
+        if (__ballot(chg && po == pe)) continue;  // changed in place: its new key is a lane candidate
+        const double fe = __longlong_as_double(readlane_l(recw, 2 + PRE_E * e));
+        const long long se = readlane_l(recw, 2 + PRE_E * e + 1);
+        any_left = true;
+        if (rp < 0 || key_before(fe, se, rf, rsq)) { rf = fe; rsq = se; rp = pe; re = e; }
+      }
+      const bool ok_merge = tag == it && (any_left || n_open0 <= kc);
+      if (ok_merge) {
+        // the lanes' minimum
+        int bpl = bp;
+        key_min_dpp<0xB1>(bf, bs, bpl);
+        key_min_dpp<0x4E>(bf, bs, bpl);
+        key_min_dpp<0x141>(bf, bs, bpl);
+        key_min_dpp<0x140>(bf, bs, bpl);
+        double wf = __longlong_as_double(readlane_l(__double_as_longlong(bf), 0));
+        long long ws = readlane_l(bs, 0);
+        int wpos = __builtin_amdgcn_readlane(bpl, 0);
+#pragma unroll
+        for (int q = 1; q < 4; q++) {
+          const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(bf), 16 * q));
+          const long long os = readlane_l(bs, 16 * q);
+          const int op = __builtin_amdgcn_readlane(bpl, 16 * q);
+          if (op >= 0 && (wpos < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wpos = op; }
+        }
+        // vs the record's least untouched entry
+        bool from_rec = false;
+        if (rp >= 0 && (wpos < 0 || key_before(rf, rsq, wf, ws))) { wpos = rp; from_rec = true; }
+        const bool go_ = !(n_open == 0 || loop >= Q.mp);
+        if (go_) {
+          // the winner's payload: id, g, Encode index, state, rw, (t, u, v)
+          int wid, wrw;
+          double wg, ws0, ws1, ws2, wt0, wt1, wt2;
+          long long wix;
+          if (from_rec) {
+            const int o = 2 + PRE_E * re;
+            wid = (int)readlane_l(recw, o + 3);
+            wg = __longlong_as_double(readlane_l(recw, o + 4));
+            wix = readlane_l(recw, o + 5);
+            ws0 = __longlong_as_double(readlane_l(recw, o + 6));
+            ws1 = __longlong_as_double(readlane_l(recw, o + 7));
+            ws2 = __longlong_as_double(readlane_l(recw, o + 8));
+            wrw = (int)readlane_l(recw, o + 9);
+            wt0 = __longlong_as_double(readlane_l(recw, o + 10));
+            wt1 = __longlong_as_double(readlane_l(recw, o + 11));
+            wt2 = __longlong_as_double(readlane_l(recw, o + 12));
+          } else {
+            const int wl = __builtin_ctzll(__ballot(myp == wpos && myp >= 0));
+            wid = __builtin_amdgcn_readlane(id, wl);
+            wg = __longlong_as_double(readlane_l(__double_as_longlong(tg), wl));
+            wix = readlane_l(nix, wl);
+            ws0 = __longlong_as_double(readlane_l(__double_as_longlong(nst0), wl));
+            ws1 = __longlong_as_double(readlane_l(__double_as_longlong(nst1), wl));
+            ws2 = __longlong_as_double(readlane_l(__double_as_longlong(nst2), wl));
+            wrw = __builtin_amdgcn_readlane(nrw, wl);
+            wt0 = __longlong_as_double(readlane_l(__double_as_longlong(nt0), wl));
+            wt1 = __longlong_as_double(readlane_l(__double_as_longlong(nt1), wl));
+            wt2 = __longlong_as_double(readlane_l(__double_as_longlong(nt2), wl));
+          }
+          // popfirst!: the last entry moves into the winner's place (ha_pop's removal)
+          const int last = n_open - 1;
+          if (wpos != last) {
+            double lf, lg, l0, l1, l2, lt0, lt1, lt2;
+            long long ls, lix;
+            int lid, lrw;
+            // the last entry is held by a lane when it was appended (the highest appended lane: appends go in
+            // lane order) or changed in place by FindNewNode; else it is the old last entry, loaded at the start
+            const unsigned long long mlast = __ballot(chg && po == last);
+            if (last >= n_open0 || mlast) {  // wave-uniform
+              const int hl = last >= n_open0 ? 63 - __builtin_clzll(m_app) : __builtin_ctzll(mlast);
+              lf = __longlong_as_double(readlane_l(__double_as_longlong(tf), hl));
+              ls = readlane_l(nseq, hl);
+              lg = __longlong_as_double(readlane_l(__double_as_longlong(tg), hl));
+              lid = __builtin_amdgcn_readlane(id, hl);
+              lix = readlane_l(nix, hl);
+              l0 = __longlong_as_double(readlane_l(__double_as_longlong(nst0), hl));
+              l1 = __longlong_as_double(readlane_l(__double_as_longlong(nst1), hl));
+              l2 = __longlong_as_double(readlane_l(__double_as_longlong(nst2), hl));
+              lrw = __builtin_amdgcn_readlane(nrw, hl);
+              lt0 = __longlong_as_double(readlane_l(__double_as_longlong(nt0), hl));
+              lt1 = __longlong_as_double(readlane_l(__double_as_longlong(nt1), hl));
+              lt2 = __longlong_as_double(readlane_l(__double_as_longlong(nt2), hl));
+            } else {  // the old last entry, untouched by FindNewNode (loaded at the start)
+              lf = __longlong_as_double(readlane_l(lastw, 0));
+              ls = readlane_l(lastw, 1);
+              lid = (int)readlane_l(lastw, 3);
+              lg = __longlong_as_double(readlane_l(lastw, 4));
+              lix = readlane_l(lastw, 5);
+              l0 = __longlong_as_double(readlane_l(lastw, 6));
+              l1 = __longlong_as_double(readlane_l(lastw, 7));
+              l2 = __longlong_as_double(readlane_l(lastw, 8));
+              lrw = (int)readlane_l(lastw, 9);
+              lt0 = __longlong_as_double(readlane_l(lastw, 10));
+              lt1 = __longlong_as_double(readlane_l(lastw, 11));
+              lt2 = __longlong_as_double(readlane_l(lastw, 12));
+            }
+            if (lane == 0) {
+              Q.of[base + wpos] = lf;
+              Q.oseq[base + wpos] = ls;
+              Q.oid[base + wpos] = lid;
+              Q.og[base + wpos] = lg;
+              Q.oix[base + wpos] = lix;
+              Q.orw[base + wpos] = lrw;
+              Q.pos[base + lid] = wpos;
+            }
+            if (lane < 3) {
+              Q.ost[(base + wpos) * 3 + lane] = lane == 0 ? l0 : lane == 1 ? l1 : l2;
+              Q.otuv[(base + wpos) * 3 + lane] = lane == 0 ? lt0 : lane == 1 ? lt1 : lt2;
+            }
+          }
+          if (lane == 0) {
+            Q.pos[base + wid] = -1;
+            Q.sc_i[SI_NOPEN * B + b] = last;
+            Q.sc_i[SI_CUR * B + b] = wid;
+            Q.cur_g[b] = wg;
+            Q.cur_ix[b] = wix;
+            Q.node_rw[(size_t)(it & 1) * B + b] = wrw;
+            s_iw = wix;
+          }
+          if (lane < 3) {
+            Q.node[(size_t)(it & 1) * 3 * B + 3 * b + lane] = lane == 0 ? ws0 : lane == 1 ? ws1 : ws2;
+            Q.node_tuv[(size_t)(it & 1) * 3 * B + 3 * b + lane] = lane == 0 ? wt0 : lane == 1 ? wt1 : wt2;
+          }
+        }
+        if (lane == 0) s_merged = go_ ? 1 : 2;  // 2: popfirst! ends the search here
+      } else if (lane == 0) {
+        s_merged = 0;
+      }
+    }
   }
   __syncthreads();  // the open-list writes of wave 0 before the block-wide scan
   BSTAMP(7);
   const int n_open = s_nopen;
   long long iw = 0;
   bool go;
-  go = ha_pop<NT>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B, false,
-              &iw, stp);
+  if (RSH && s_merged) {  // block-uniform
+    go = s_merged == 1;
+    iw = s_iw;
+  } else {
+    go = ha_pop<NT, RSH>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B,
+                    Q.node_tuv + (size_t)(it & 1) * 3 * B, false, &iw, stp);
+  }
   BSTAMP(8);
   BookRec br;
   br.v[RC_GO] = go;
@@ -2023,6 +2403,162 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
   }
 }
 
+// (RSH tail) popfirst!'s scan ahead of FindNewNode, on its own block of the scene: the PRE_K least entries of
+// the open list as this iteration starts (stream order: the previous bookkeeping's writes are complete), with
+// their payloads, into the scene's record (Q.pre).  FindNewNode then changes some entries in place and appends
+// others; the least entry after it is the least of the record's entries it left alone, the changed and the
+// appended ones -- unless it changed every record entry while more remain (the bookkeeping then scans).
+// Every entry outside the record has a key above the record's, so the merge is exact (the key order is total).
+// Per thread its PRE_K least entries (insertion), per wave PRE_K rounds of a DPP minimum, then wave 0 over the
+// waves' PRE_K each.  Returns false (block-uniform) past the live list.
+template <int NT>
+__device__ __forceinline__ bool ha_prescan(const HaSearch& Q, const IterArgs& A, int B, int it, int slot,
+                                           unsigned long long* hstp = nullptr) {
+  static_assert(NT % 64 == 0 && NT / 64 * PRE_K <= 64, "the waves' candidates fit wave 0");
+  __shared__ double c_f[NT / 64][PRE_K];
+  __shared__ long long c_s[NT / 64][PRE_K];
+  __shared__ int c_p[NT / 64][PRE_K];
+  const int n_live = A.n_live ? *A.n_live : A.n_active;
+  const int b = A.scene_of ? A.scene_of[slot] : slot;
+  if (slot >= n_live) return false;
+  if (!A.n_live && A.active && !A.active[b]) return false;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t base = (size_t)b * Q.C;
+  if (A.no_pre) {
+    if (tid == 0) st_ag(Q.pre + (size_t)b * PRE_W, -1LL);
+    return true;
+  }
+  const int n0 = Q.sc_i[SI_NOPEN * B + b];
+  HSTAMP(12);
+  double tf[PRE_K];
+  long long ts[PRE_K];
+  int tp[PRE_K];
+#pragma unroll
+  for (int e = 0; e < PRE_K; e++) { tf[e] = __builtin_inf(); ts[e] = 0x7fffffffffffffffLL; tp[e] = -1; }
+  for (int p0 = tid; p0 < n0; p0 += 2 * NT) {  // two independent entry loads in flight per thread
+    double fv[2];
+    long long sv[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int p = p0 + u * NT;
+      fv[u] = p < n0 ? Q.of[base + p] : 0.0;
+      sv[u] = p < n0 ? Q.oseq[base + p] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int p = p0 + u * NT;
+      if (p >= n0) continue;
+      // insertion into the sorted PRE_K (the key order is total: positions are distinct entries)
+      double f = fv[u];
+      long long sq = sv[u];
+      int pp = p;
+#pragma unroll
+      for (int e = 0; e < PRE_K; e++) {
+        if (tp[e] < 0 || key_before(f, sq, tf[e], ts[e])) {
+          const double f2 = tf[e];
+          const long long s2 = ts[e];
+          const int p2 = tp[e];
+          tf[e] = f; ts[e] = sq; tp[e] = pp;
+          f = f2; sq = s2; pp = p2;
+          if (pp < 0) break;
+        }
+      }
+    }
+  }
+  if (HA_STAMP_CODE && hstp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    HSTAMP(13);
+  }
+  // the wave's PRE_K least: PRE_K rounds of the minimum of the lanes' heads, the owner lane shifting its list
+#pragma unroll 1
+  for (int r = 0; r < PRE_K; r++) {
+    double bf = tf[0];
+    long long bs = ts[0];
+    int bp = tp[0];
+    key_min_dpp<0xB1>(bf, bs, bp);
+    key_min_dpp<0x4E>(bf, bs, bp);
+    key_min_dpp<0x141>(bf, bs, bp);
+    key_min_dpp<0x140>(bf, bs, bp);
+    double wf = __longlong_as_double(readlane_l(__double_as_longlong(bf), 0));
+    long long ws = readlane_l(bs, 0);
+    int wp_ = __builtin_amdgcn_readlane(bp, 0);
+#pragma unroll
+    for (int q = 1; q < 4; q++) {
+      const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(bf), 16 * q));
+      const long long os = readlane_l(bs, 16 * q);
+      const int op = __builtin_amdgcn_readlane(bp, 16 * q);
+      if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
+    }
+    if (lane == 0) { c_f[wave][r] = wf; c_s[wave][r] = ws; c_p[wave][r] = wp_; }
+    if (wp_ >= 0 && tp[0] == wp_) {  // the owner lane drops its head
+#pragma unroll
+      for (int e = 0; e + 1 < PRE_K; e++) { tf[e] = tf[e + 1]; ts[e] = ts[e + 1]; tp[e] = tp[e + 1]; }
+      tf[PRE_K - 1] = __builtin_inf(); ts[PRE_K - 1] = 0x7fffffffffffffffLL; tp[PRE_K - 1] = -1;
+    }
+  }
+  HSTAMP(14);
+  __syncthreads();
+  if (tid >= 64) return true;
+  // wave 0: the block's PRE_K least of the waves' candidates (lane = wave * PRE_K + rank)
+  double cf = __builtin_inf();
+  long long cs = 0x7fffffffffffffffLL;
+  int cp = -1;
+  if (lane < NT / 64 * PRE_K) {
+    cf = c_f[lane / PRE_K][lane % PRE_K];
+    cs = c_s[lane / PRE_K][lane % PRE_K];
+    cp = c_p[lane / PRE_K][lane % PRE_K];
+  }
+  int mine = -1;  // lane e < kc: the e-th least entry's position
+#pragma unroll 1
+  for (int r = 0; r < PRE_K; r++) {
+    double bf = cf;
+    long long bs = cs;
+    int bp = cp;
+    key_min_dpp<0xB1>(bf, bs, bp);
+    key_min_dpp<0x4E>(bf, bs, bp);
+    key_min_dpp<0x141>(bf, bs, bp);
+    key_min_dpp<0x140>(bf, bs, bp);
+    double wf = __longlong_as_double(readlane_l(__double_as_longlong(bf), 0));
+    long long ws = readlane_l(bs, 0);
+    int wp_ = __builtin_amdgcn_readlane(bp, 0);
+#pragma unroll
+    for (int q = 1; q < 4; q++) {
+      const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(bf), 16 * q));
+      const long long os = readlane_l(bs, 16 * q);
+      const int op = __builtin_amdgcn_readlane(bp, 16 * q);
+      if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
+    }
+    if (lane == r) mine = wp_;
+    if (wp_ >= 0 && cp == wp_) { cf = __builtin_inf(); cs = 0x7fffffffffffffffLL; cp = -1; }
+  }
+  const int kc = min(PRE_K, n0);
+  HSTAMP(15);
+  long long* rec = Q.pre + (size_t)b * PRE_W;
+  if (lane < kc && mine >= 0) {  // lane e: entry e and its payload
+    const size_t q = base + mine;
+    long long w[PRE_E];
+    w[0] = __double_as_longlong(Q.of[q]);
+    w[1] = Q.oseq[q];
+    w[2] = mine;
+    w[3] = Q.oid[q];
+    w[4] = __double_as_longlong(Q.og[q]);
+    w[5] = Q.oix[q];
+#pragma unroll
+    for (int e = 0; e < 3; e++) w[6 + e] = __double_as_longlong(Q.ost[q * 3 + e]);
+    w[9] = Q.orw[q];
+#pragma unroll
+    for (int e = 0; e < 3; e++) w[10 + e] = __double_as_longlong(Q.otuv[q * 3 + e]);
+#pragma unroll
+    for (int e = 0; e < PRE_E; e++) st_ag(rec + 2 + PRE_E * lane + e, w[e]);
+  }
+  if (lane == 0) {
+    st_ag(rec + 1, (long long)kc);
+    st_ag(rec + 0, (long long)it);
+  }
+  HSTAMP(16);
+  return true;
+}
+
 // Waves per SIMD each shape is compiled for.  The full-width shape (4-wave blocks, 1,280 of them at 256
 // scenes) is occupancy-bound: 133 VGPRs would allow 3 waves per SIMD; 4 costs 20 B of spills and gains
 // 0.3 ms per plan (r04zc: 29.7 vs 30.0 ms; round 4 had drifted to 169 VGPRs, 2 waves, 31.5 ms).  The
@@ -2042,9 +2578,13 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
       threadIdx.x == 0)
     stp = A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int per = 1 + (P.n_prim + NBGt - 1) / NBGt;
+  const int per = 1 + (P.n_prim + NBGt - 1) / NBGt + (RSH ? 1 : 0);
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
-  if (!ha_iter_body<HWt, NBGt, RSH>(P, A, stp)) return;  // block-uniform: no work for this block (not counted)
+  if (RSH && item == per - 1) {  // the prescan block: counted among the bookkeeping's arrivals
+    if (!ha_prescan<64 * HWt>(Q, A, B, it, slot, stp)) return;
+  } else if (!ha_iter_body<HWt, NBGt, RSH>(P, A, stp)) {
+    return;  // block-uniform: no work for this block (not counted)
+  }
   const int s = A.scene_of ? A.scene_of[slot] : slot;
   ha_stores_done();  // this thread's records acknowledged before the block's ticket
   __syncthreads();
@@ -2490,9 +3030,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_CHECK(ctx, ncell > 0 && ncell < (1LL << 26), "state lattice too large (%lld cells)", ncell);
   const size_t C = (size_t)ncell + 1, nB = (size_t)B;
   // search state: node arrays and open list indexed [scene][node / cell]
-  const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4;
+  const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + 256 * 40);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + 256 * 48);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -2529,6 +3069,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.rw = (int*)take(nB * C * 4);
   Q.orw = (int*)take(nB * C * 4);
   Q.node_rw = (int*)take(nB * 8);
+  Q.tuv = (double*)take(nB * C * 24);
+  Q.otuv = (double*)take(nB * C * 24);
+  Q.node_tuv = (double*)take(nB * 48);
+  Q.pre = (long long*)take(nB * PRE_W * 8);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
@@ -2570,6 +3114,15 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     A.pt_mlo = mlo;
     A.pt_nm = nm;
     A.pt_nsw = nsw;
+    double* htn = ok ? (double*)mp_ws(ctx, WS_IO13, sizeof(double) * (2 * (size_t)nm + 4 * (size_t)nm * np)) : nullptr;
+    if (ok && !htn) return MP_ERR_NOMEM;
+    if (htn) {
+      hipLaunchKernelGGL(ha_head_table_kernel, dim3((unsigned)((nm * np + 255) / 256)), dim3(256), 0, ctx->stream, D,
+                         (const double*)ctx->ha_states_candi, mlo, nm, htn, htn + 2 * (size_t)nm);
+      MP_HIP(ctx, hipGetLastError());
+    }
+    A.htn = htn;
+    A.htk = htn ? htn + 2 * (size_t)nm : nullptr;
   }
   if (p->n_walls) {
     double* wt = (double*)mp_ws(ctx, WS_IO8, sizeof(double) * nB * p->n_walls * WT);
@@ -2590,7 +3143,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool stamps_on = HA_STAMP_CODE && getenv("MPGPU_HA_STAMPS") && atoi(getenv("MPGPU_HA_STAMPS")) == 1;
   const int stamp_slots = std::min(mp / HA_STAMP_EVERY + 1, 40);  // iterations < 1,000
   A.stamps = nullptr;
-  A.stamp_blocks = B * (1 + (np + NBG_TAIL - 1) / NBG_TAIL);
+  A.stamp_blocks = B * (2 + (np + NBG_TAIL - 1) / NBG_TAIL);  // + the RSH tail's prescan block
   if (stamps_on) {
     A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA3, sizeof(unsigned long long) * HA_STAMP_N * (size_t)stamp_slots * A.stamp_blocks);
     if (!A.stamps) return MP_ERR_NOMEM;
@@ -2639,7 +3192,16 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   const bool tail_rsh = HA_TAIL_RSH && rsh_env && !split && NBG_TAIL == 4 && per_tail - 1 >= 4 * ((np + 15) / 16);
   A.hp_c = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * nB * np * 4);
   A.hp_i = (int*)mp_ws(ctx, WS_IO12, sizeof(int) * nB * np * 4);
-  if (!A.hp_c || !A.hp_i) return MP_ERR_NOMEM;
+  A.hp_t = (double*)mp_ws(ctx, WS_IO14, sizeof(double) * nB * np * 12);
+  // (A/B) MPGPU_HA_PRESCAN=1: the prescan block's PRE_K least entries merged into popfirst!.  Measured slower
+  // (r05j, lone 729-pop scenario: 26.6 vs 25.7 us per iteration): its PRE_K DPP rounds on 12 waves took ~6 us
+  // and the merge's readlane chains ~2.6 us, so the bookkeeping started later than it saved.  Off by default
+  // (the block then only marks its record stale and takes its ticket).
+  static const bool pre_env = getenv("MPGPU_HA_PRESCAN") && atoi(getenv("MPGPU_HA_PRESCAN")) == 1;
+  static const bool tuv_env = !getenv("MPGPU_HA_TUV") || atoi(getenv("MPGPU_HA_TUV")) != 0;
+  A.no_pre = !pre_env;
+  A.no_tuv = !tuv_env;
+  if (!A.hp_c || !A.hp_i || !A.hp_t) return MP_ERR_NOMEM;
   // iteration it >= 2 works on the compact list of scenes still live (written by the previous
   // bookkeeping launch, count on the device); the host sizes the grids by the last live count it has
   // seen (an upper bound: it only decreases) and switches to the tail shape once that many scenes
@@ -2660,6 +3222,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     A.n_active = known;
     A.node = Q.node + (size_t)((it - 1) & 1) * 3 * B;  // the previous iteration's pops
     A.node_rw = rs_full ? nullptr : Q.node_rw + (size_t)((it - 1) & 1) * B;
+    A.node_tuv = Q.node_tuv + (size_t)((it - 1) & 1) * 3 * B;
     const bool tail = known * per_tail <= tail_blocks;
     if (split) {
       if (tail)
@@ -2669,8 +3232,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
       hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     } else if (tail) {
-      if (tail_rsh)
-        hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL, true>), dim3((unsigned)(known * per_tail)),
+      if (tail_rsh)  // + the prescan block per scene
+        hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL, true>), dim3((unsigned)(known * (per_tail + 1))),
                            dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
       else
         hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)),
