@@ -607,6 +607,9 @@ struct IterArgs {
   const double* htn;
   const double* htk;
   int no_pre;  // (A/B, MPGPU_HA_PRESCAN=0) the prescan block only marks its record stale: the bookkeeping scans
+  int node_ag;  // read the node agent-coherently (written in this launch), once node_flag[s] >= node_flag_min
+  const int* node_flag;
+  int node_flag_min;
   int no_tuv;  // (A/B, MPGPU_HA_TUV=0) nodes keep only their winner id: RS_connected evaluates its word
 };
 
@@ -858,7 +861,8 @@ __device__ __forceinline__ void cmd_from_tuv(int rw, const double* tuv, double* 
 // One search iteration's device work for the block (role by blockIdx: RS_connected or a
 // 16-neighbour group).  Returns false (block-uniformly) when the block has nothing to do.
 template <int HWt, int NBGt, bool RSH = false>
-__device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, unsigned long long* hstp = nullptr) {
+__device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, unsigned long long* hstp = nullptr,
+                                             int slot_ = -1, int item_ = -1) {
 // (diagnostics, -DHA_STAMP_CODE=1) phase stamps of the block's thread 0 into ha_step_kernel's slots 12..
 #define HSTAMP(i) if (HA_STAMP_CODE && hstp) __hip_atomic_store(hstp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
   constexpr int HT = 64 * HWt, NBG = NBGt;
@@ -879,7 +883,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   __shared__ int g_need[NBG];
   __shared__ int sh_n;
   const int per = 1 + (P.n_prim + NBG - 1) / NBG + (RSH ? 1 : 0);  // RSH: the prescan block is the last item
-  const int slot = blockIdx.x / per, item = blockIdx.x % per;
+  // (ha_pipe_kernel passes its own slot / role numbering)
+  const int slot = slot_ >= 0 ? slot_ : blockIdx.x / per, item = item_ >= 0 ? item_ : blockIdx.x % per;
   // the live count and the slot's scene are independent loads (slot < the grid's bound <= B keeps the
   // list read in bounds); a scene on the bookkeeping's list (n_live set) is live, so its flag is not
   // read: the node and goal loads then follow one round trip instead of three
@@ -896,6 +901,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   const int nw = P.n_walls;
   const double* node = A.node + 3 * s;
   const double* goal = A.goal + 3 * s;
+  __shared__ double nd_s[3];
+  __shared__ int nd_go;
   const OutRef R = out_ref(A, s, P.n_prim);
   const int k0 = rs ? 0 : (item - 1) * NBG, nk = rs ? 0 : min(NBG, P.n_prim - k0);
   // wall corners (Block2Pts) and their SAT tables in LDS: precomputed once per plan
@@ -921,6 +928,19 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     }
   }
   if (tid < NBG) g_free[tid] = 1;
+  if (A.node_ag) {  // the node comes from another block of this launch (ha_pipe_kernel's bookkeeping): wait for
+    // its ready flag (the walls are staged meanwhile), then read it agent-coherently
+    if (tid == 0) {
+      int f;
+      while ((f = ld_ag(A.node_flag + s)) < A.node_flag_min) __builtin_amdgcn_s_sleep(1);
+      nd_go = f & 1;
+    }
+    __syncthreads();
+    if (!nd_go) return false;  // block-uniform: the search ended, nothing to expand
+    if (tid < 3) nd_s[tid] = ld_ag(A.node + 3 * s + tid);
+    __syncthreads();
+    node = nd_s;
+  }
   // the tail shape (threads to spare): the collision sweep splits every pose into its 2·n_walls SAT terms,
   // one per thread, and a neighbour group evaluates rs_heuristic for all its neighbours at once
   constexpr bool SPLIT = HWt == HW_TAIL;
@@ -1451,6 +1471,7 @@ struct HaSearch {
   double* otuv;          // [B][C][3] open entries: the same
   double* node_tuv;      // [2][B][3] popped node's, double-buffered like node
   long long* pre;        // [B][PRE_W] (RSH tail) the prescan's record: popfirst!'s K least entries before FindNewNode
+  int* nx;               // [B] (ha_pipe_kernel) 2·it + 2 + go once iteration it's bookkeeping has popped the next node
 };
 // prescan record: [0] iteration tag, [1] kc = min(K, n_open), then K entries of 13 words: f (bits), seq, position,
 // node id, g (bits), Encode index, state (3, bits), rw, (t, u, v) (3, bits)
@@ -2559,6 +2580,425 @@ __device__ __forceinline__ bool ha_prescan(const HaSearch& Q, const IterArgs& A,
   return true;
 }
 
+
+// ---------------------------------------------------------------- pipelined tail (ha_pipe_kernel)
+// The expansion of a node (its 62 neighbour records) is a function of the node's state alone, and the next
+// popfirst! is a function of the records, the Dict and the open list as they stand before FindNewNode writes:
+// the least of the entries FindNewNode leaves alone, the ones it changes in place (new keys) and the ones it
+// appends.  So launch it of the pipelined tail runs, per scene:
+//   item 0   RS_connected(n_it), as before;
+//   item 1   the bookkeeping: the records of n_it (expanded by the previous launch, E[it & 1]), FindNewNode's
+//            decisions, the open list scan excluding the positions it changes, the pop of n_{it+1} -- published
+//            (state, stored commands, a ready flag) before FindNewNode's writes -- then the writes, the removal,
+//            and the final ticket with RS_connected, as ha_step_kernel's bookkeeping block;
+//   items 2+ the expansion of n_{it+1} (the RSH groups and word units), into E[(it + 1) & 1] for launch it+1,
+//            started as soon as the pop is published (they spin on the flag: their blocks follow the
+//            bookkeeping's in dispatch order, so it is running or done).
+// The chain per iteration is the bookkeeping's pop decision + the expansion, instead of the expansion + the
+// whole bookkeeping.  Same operations on the same values as ha_step_kernel: the same search, bit for bit.
+// A bootstrap launch (boot = 1) expands the current nodes only, for the first pipelined launch.
+
+// E[par]: the expansion-record buffers hold two parities of [B][n_prim][...]
+__device__ __forceinline__ IterArgs e_par(const IterArgs& A, int B, int np, int par) {
+  IterArgs E = A;
+  const size_t n = (size_t)B * np * par;
+  E.idx = A.idx + n;
+  E.fr = A.fr + n;
+  E.nb = A.nb + 3 * n;
+  E.hp_c = A.hp_c + 4 * n;
+  E.hp_i = A.hp_i + 4 * n;
+  E.hp_t = A.hp_t + 12 * n;
+  return E;
+}
+
+template <int NT>
+__device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& Q, const IterArgs& E, int B, int it,
+                                                int b, unsigned long long* stp = nullptr) {
+#define PSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+  constexpr int SC = 4;  // open entries per thread held in registers (more are re-read)
+  __shared__ int s_nopen, s_nnew, s_nchg, s_go;
+  __shared__ int s_chg[64];  // positions FindNewNode changes in place
+  __shared__ long long s_vix[64];
+  __shared__ int s_dup[4][64];
+  __shared__ double r_f[NT / 64];
+  __shared__ long long r_s[NT / 64];
+  __shared__ int r_p[NT / 64];
+  __shared__ long long r_pay[NT / 64][11];  // each wave winner's payload: id, g, ix, st[3], rw, tuv[3]
+  __shared__ long long s_win[12];           // the pop's winner: payload as r_pay, position
+  static_assert(NT >= 256 && NT / 64 <= 16, "four waves for the duplicate check, the wave winners fit a row");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t base = (size_t)b * Q.C;
+  const int np = P.n_prim;
+  const int loop = Q.sc_i[SI_LOOP * B + b];
+  const int n_open0 = Q.sc_i[SI_NOPEN * B + b];
+  const int nn0 = Q.sc_i[SI_NNODES * B + b];
+  const int cur0 = Q.sc_i[SI_CUR * B + b];
+  const long long ctr = Q.ctr[b];
+  const double cur_g = Q.cur_g[b];
+  const long long cidx = Q.cur_ix[b];
+  // the open list as it stands (loads in flight while the records and the Dict come in)
+  double fv[SC];
+  long long sv[SC];
+  // (loaded before n_open0 is known: positions past it are read -- inside the scene's C entries -- and masked)
+#pragma unroll
+  for (int u = 0; u < SC; u++) {
+    const int p = tid + u * NT;
+    fv[u] = p < Q.C ? Q.of[base + p] : 0.0;
+    sv[u] = p < Q.C ? Q.oseq[base + p] : 0;
+  }
+  // n_it's neighbour records (expanded by the previous launch)
+  long long ix = 0;
+  int frk = 0, hwk = -1;
+  double hk = 0.0, nb0 = 0.0, nb1 = 0.0, nb2 = 0.0;
+  double tuvk[3] = {0.0, 0.0, 0.0};
+  if (tid < np) {
+    const size_t q = (size_t)b * np + tid;
+    ix = ld_ag(E.idx + q);
+    frk = ld_ag(E.fr + q);
+    double cv[4], ct[4][3];
+    int ci[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      cv[c] = ld_ag(E.hp_c + q * 4 + c);
+      ci[c] = ld_ag(E.hp_i + q * 4 + c);
+#pragma unroll
+      for (int e = 0; e < 3; e++) ct[c][e] = ld_ag(E.hp_t + (q * 4 + c) * 3 + e);
+    }
+    double v = cv[0];
+    int id = ci[0], wc = 0;
+#pragma unroll
+    for (int c = 1; c < 4; c++)
+      if (rs_before(cv[c], ci[c], v, id)) { v = cv[c]; id = ci[c]; wc = c; }
+    hk = v * P.minR;
+    hwk = E.no_tuv ? id : id | RW_TUV | (v < __builtin_inf() ? RW_OK : 0);
+#pragma unroll
+    for (int e = 0; e < 3; e++) tuvk[e] = ct[0][e];
+#pragma unroll
+    for (int c = 1; c < 4; c++)
+      if (wc == c)
+#pragma unroll
+        for (int e = 0; e < 3; e++) tuvk[e] = ct[c][e];
+    nb0 = ld_ag(E.nb + 3 * q);
+    nb1 = ld_ag(E.nb + 3 * q + 1);
+    nb2 = ld_ag(E.nb + 3 * q + 2);
+  }
+  const bool valid = tid < np && ix != 0 && frk;
+  if (tid < 64) s_vix[tid] = valid ? ix : 0;
+  __syncthreads();
+  if (tid < 256) {
+    const int w = tid >> 6;
+    const long long key = s_vix[lane];
+    bool d = false;
+#pragma unroll
+    for (int jj = 0; jj < 16; jj++) {
+      const int j = 16 * w + jj;
+      const long long oj = s_vix[j];
+      d = d | ((oj == key) & (j < lane) & (key != 0));
+    }
+    s_dup[w][lane] = d;
+  }
+  int hit = -1;
+  double gd = 0.0, fo_ = 0.0, dst0 = 0.0, dst1 = 0.0, dst2 = 0.0;
+  int po = 0, drw = -1;
+  double dtuv[3] = {0.0, 0.0, 0.0};
+  long long so0 = 0, io = 0;
+  if (valid) {
+    hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
+    if (hit >= 0) {
+      gd = Q.g[base + hit];
+      po = Q.pos[base + hit];
+      fo_ = Q.f[base + hit];
+      so0 = Q.seq[base + hit];
+      io = Q.index[base + hit];
+      drw = Q.rw[base + hit];
+#pragma unroll
+      for (int e = 0; e < 3; e++) dtuv[e] = Q.tuv[(base + hit) * 3 + e];
+      dst0 = Q.st[(base + hit) * 3];
+      dst1 = Q.st[(base + hit) * 3 + 1];
+      dst2 = Q.st[(base + hit) * 3 + 2];
+    }
+  }
+  __syncthreads();
+  PSTAMP(6);
+  // ---- FindNewNode's decisions (:418-446) on wave 0 (lane k = neighbour k), no writes yet
+  const double tg = cur_g + P.expand_time;
+  double th = 0.0, tf = 0.0;
+  int id = -1;
+  bool chg = false, app = false, isnew = false;
+  double nst0 = 0.0, nst1 = 0.0, nst2 = 0.0;
+  long long nix = ix, nseq = 0;
+  int nrw = hwk, myp = -1;
+  double nt0 = tuvk[0], nt1 = tuvk[1], nt2 = tuvk[2];
+  unsigned long long m_new = 0, m_chg = 0, m_app = 0;
+  int n_app = 0, n_open = n_open0;
+  if (tid < 64) {
+    const int k = lane;
+    const bool dup = s_dup[0][k] | s_dup[1][k] | s_dup[2][k] | s_dup[3][k];
+    const bool first = valid && !dup;
+    double fo = 0.0;
+    long long so_ = 0;
+    if (first) {
+      th = __builtin_fmax(hk, 0.0);
+      if (hk != hk) th = hk;
+      tf = tg + th;
+      if (hit >= 0) {
+        id = hit;
+        nst0 = dst0; nst1 = dst1; nst2 = dst2;
+        nix = io;
+        nrw = drw;
+        nt0 = dtuv[0]; nt1 = dtuv[1]; nt2 = dtuv[2];
+        if (tg < gd) {
+          if (po >= 0) { chg = true; fo = fo_; so_ = so0; }
+          else app = true;
+        }
+      } else {
+        isnew = true;
+        app = true;
+        nst0 = nb0; nst1 = nb1; nst2 = nb2;
+      }
+    }
+    m_new = __ballot(isnew);
+    m_chg = __ballot(chg);
+    m_app = __ballot(app);
+    const unsigned long long below = (1ull << k) - 1;
+    const int n_chg = __popcll(m_chg);
+    n_app = __popcll(m_app);
+    if (isnew) id = nn0 + __popcll(m_new & below);
+    int r = 0;
+    for (unsigned long long m = m_chg; m; m &= m - 1) {
+      const int j = __builtin_ctzll(m);
+      const double fj = __shfl(fo, j);
+      const long long sj = __shfl(so_, j);
+      r += chg && key_before(fj, sj, fo, so_);
+    }
+    if (chg) nseq = ctr + r;
+    else if (app) nseq = ctr + n_chg + __popcll(m_app & below);
+    myp = chg ? po : app ? n_open0 + __popcll(m_app & below) : -1;
+    if (chg) s_chg[__popcll(m_chg & below)] = po;
+    n_open = n_open0 + n_app;
+    if (lane == 0) {
+      s_nchg = n_chg;
+      s_nopen = n_open;
+      s_nnew = nn0 + __popcll(m_new);
+    }
+  }
+  __syncthreads();
+  // ---- the old entries FindNewNode leaves alone: each thread's least (positions it changes excluded)
+  const int nchg = s_nchg;
+  auto changed = [&](int p) {
+    bool c = false;
+    for (int i = 0; i < nchg; i++) c |= s_chg[i] == p;
+    return c;
+  };
+  double bf = __builtin_inf();
+  long long bs = 0x7fffffffffffffffLL;
+  int bp = -1;
+#pragma unroll
+  for (int u = 0; u < SC; u++) {
+    const int p = tid + u * NT;
+    if (p < n_open0 && !changed(p) && (bp < 0 || key_before(fv[u], sv[u], bf, bs))) { bf = fv[u]; bs = sv[u]; bp = p; }
+  }
+  for (int p = tid + SC * NT; p < n_open0; p += NT) {  // long lists: the rest re-read
+    const double f = Q.of[base + p];
+    const long long sq = Q.oseq[base + p];
+    if (!changed(p) && (bp < 0 || key_before(f, sq, bf, bs))) { bf = f; bs = sq; bp = p; }
+  }
+  // the thread's own best entry's payload, its latency behind the reductions
+  long long pay[11];
+#pragma unroll
+  for (int e = 0; e < 11; e++) pay[e] = 0;
+  if (bp >= 0) {
+    const size_t q = base + bp;
+    pay[0] = Q.oid[q];
+    pay[1] = __double_as_longlong(Q.og[q]);
+    pay[2] = Q.oix[q];
+#pragma unroll
+    for (int e = 0; e < 3; e++) pay[3 + e] = __double_as_longlong(Q.ost[q * 3 + e]);
+    pay[6] = Q.orw[q];
+#pragma unroll
+    for (int e = 0; e < 3; e++) pay[7 + e] = __double_as_longlong(Q.otuv[q * 3 + e]);
+  }
+  const int own = bp;
+  key_min_dpp<0xB1>(bf, bs, bp);
+  key_min_dpp<0x4E>(bf, bs, bp);
+  key_min_dpp<0x141>(bf, bs, bp);
+  key_min_dpp<0x140>(bf, bs, bp);
+  {
+    double wf = __longlong_as_double(readlane_l(__double_as_longlong(bf), 0));
+    long long ws = readlane_l(bs, 0);
+    int wp_ = __builtin_amdgcn_readlane(bp, 0);
+#pragma unroll
+    for (int q = 1; q < 4; q++) {
+      const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(bf), 16 * q));
+      const long long os = readlane_l(bs, 16 * q);
+      const int op = __builtin_amdgcn_readlane(bp, 16 * q);
+      if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
+    }
+    if (lane == 0) { r_f[wave] = wf; r_s[wave] = ws; r_p[wave] = wp_; }
+    if (wp_ >= 0 && own == wp_) {
+#pragma unroll
+      for (int e = 0; e < 10; e++) r_pay[wave][e] = pay[e];
+    }
+  }
+  __syncthreads();
+  PSTAMP(7);
+  // ---- popfirst! (wave 0): the least of the waves' winners (lanes < NT/64) and the lanes' changed / appended
+  // entries -- a lane offers the better of the two it holds
+  if (tid < 64) {
+    double cf = __builtin_inf();
+    long long cs = 0x7fffffffffffffffLL;
+    int cp = -1, src = -1;  // src: wave index of an old winner, 64 + lane for a lane candidate
+    if (lane < NT / 64 && r_p[lane] >= 0) { cf = r_f[lane]; cs = r_s[lane]; cp = r_p[lane]; src = lane; }
+    if (myp >= 0 && (cp < 0 || key_before(tf, nseq, cf, cs))) { cf = tf; cs = nseq; cp = myp; src = 64 + lane; }
+    const int mine = cp, msrc = src;
+    key_min_dpp<0xB1>(cf, cs, cp);
+    key_min_dpp<0x4E>(cf, cs, cp);
+    key_min_dpp<0x141>(cf, cs, cp);
+    key_min_dpp<0x140>(cf, cs, cp);
+    double wf = __longlong_as_double(readlane_l(__double_as_longlong(cf), 0));
+    long long ws = readlane_l(cs, 0);
+    int wpos = __builtin_amdgcn_readlane(cp, 0);
+#pragma unroll
+    for (int q = 1; q < 4; q++) {
+      const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(cf), 16 * q));
+      const long long os = readlane_l(cs, 16 * q);
+      const int op = __builtin_amdgcn_readlane(cp, 16 * q);
+      if (op >= 0 && (wpos < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wpos = op; }
+    }
+    const bool go = !(n_open == 0 || loop >= Q.mp);
+    // the winner's lane writes its payload to LDS (an old entry's from its wave record, a lane's own values)
+    if (go && mine == wpos && mine >= 0) {
+      if (msrc < 64) {
+#pragma unroll
+        for (int e = 0; e < 10; e++) s_win[e] = r_pay[msrc][e];
+      } else {
+        s_win[0] = id;
+        s_win[1] = __double_as_longlong(tg);
+        s_win[2] = nix;
+        s_win[3] = __double_as_longlong(nst0);
+        s_win[4] = __double_as_longlong(nst1);
+        s_win[5] = __double_as_longlong(nst2);
+        s_win[6] = nrw;
+        s_win[7] = __double_as_longlong(nt0);
+        s_win[8] = __double_as_longlong(nt1);
+        s_win[9] = __double_as_longlong(nt2);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the winner's LDS writes before the wave reads them
+    if (go) {
+      // publish the next node: state, stored commands, then the ready flag (the expansion blocks spin on it)
+      if (lane < 3) {
+        st_ag(Q.node + (size_t)(it & 1) * 3 * B + 3 * b + lane, __longlong_as_double(s_win[3 + lane]));
+        st_ag(Q.node_tuv + (size_t)(it & 1) * 3 * B + 3 * b + lane, __longlong_as_double(s_win[7 + lane]));
+      }
+      if (lane == 0) st_ag(Q.node_rw + (size_t)(it & 1) * B + b, (int)s_win[6]);
+    }
+    ha_stores_done();
+    if (lane == 0) {
+      st_ag(Q.nx + b, 2 * it + 2 + (go ? 1 : 0));
+      s_go = go;
+      s_win[10] = wpos;
+    }
+    PSTAMP(8);
+    // ---- FindNewNode's writes (as ha_book_spec)
+    if (chg || app) {
+      const size_t q = base + id;
+      if (isnew) {
+        Q.st[q * 3] = nst0;
+        Q.st[q * 3 + 1] = nst1;
+        Q.st[q * 3 + 2] = nst2;
+        Q.index[q] = ix;
+        Q.rw[q] = nrw;
+        Q.tuv[q * 3] = nt0;
+        Q.tuv[q * 3 + 1] = nt1;
+        Q.tuv[q * 3 + 2] = nt2;
+        if (ix > 0 && ix < Q.C) Q.nid[base + ix] = id;
+      }
+      Q.g[q] = tg;
+      Q.h[q] = th;
+      Q.f[q] = tf;
+      Q.parent[q] = cidx;
+      Q.seq[q] = nseq;
+      const int p = myp;
+      Q.of[base + p] = tf;
+      Q.oseq[base + p] = nseq;
+      Q.og[base + p] = tg;
+      if (!chg) {
+        Q.oid[base + p] = id;
+        Q.oix[base + p] = nix;
+        Q.orw[base + p] = nrw;
+        Q.otuv[(base + p) * 3] = nt0;
+        Q.otuv[(base + p) * 3 + 1] = nt1;
+        Q.otuv[(base + p) * 3 + 2] = nt2;
+        Q.ost[(base + p) * 3] = nst0;
+        Q.ost[(base + p) * 3 + 1] = nst1;
+        Q.ost[(base + p) * 3 + 2] = nst2;
+        Q.pos[q] = p;
+      }
+    }
+    if (lane == 0) Q.ctr[b] = ctr + __popcll(m_chg) + n_app;
+    // ---- popfirst!'s removal: the last entry moves into the winner's place (ha_pop)
+    if (go) {
+      const int last = n_open - 1;
+      const int wid = (int)s_win[0];
+      if (wpos != last) {
+        // the last entry: appended (the highest appending lane), changed in place, or the old one (lane 0)
+        const unsigned long long mlast = __ballot(chg && po == last);
+        const int hl = last >= n_open0 ? 63 - __builtin_clzll(m_app) : mlast ? __builtin_ctzll(mlast) : 0;
+        if (lane == hl) {
+          const bool own_vals = last >= n_open0 || mlast;
+          // the old last entry (read only now: off the pop's publication path)
+          double Lf = 0.0, Lg = 0.0, Ls0 = 0.0, Ls1 = 0.0, Ls2 = 0.0, Lt0 = 0.0, Lt1 = 0.0, Lt2 = 0.0;
+          long long Lsq = 0, Lix = 0;
+          int Lid = 0, Lrw = -1;
+          if (!own_vals) {
+            const size_t L = base + n_open0 - 1;
+            Lf = Q.of[L]; Lsq = Q.oseq[L]; Lid = Q.oid[L]; Lg = Q.og[L]; Lix = Q.oix[L]; Lrw = Q.orw[L];
+            Ls0 = Q.ost[L * 3]; Ls1 = Q.ost[L * 3 + 1]; Ls2 = Q.ost[L * 3 + 2];
+            Lt0 = Q.otuv[L * 3]; Lt1 = Q.otuv[L * 3 + 1]; Lt2 = Q.otuv[L * 3 + 2];
+          }
+          const double f_ = own_vals ? tf : Lf, g_ = own_vals ? tg : Lg;
+          const long long s_ = own_vals ? nseq : Lsq, x_ = own_vals ? nix : Lix;
+          const int i_ = own_vals ? id : Lid, w_ = own_vals ? nrw : Lrw;
+          const size_t d = base + wpos;
+          Q.of[d] = f_;
+          Q.oseq[d] = s_;
+          Q.oid[d] = i_;
+          Q.og[d] = g_;
+          Q.oix[d] = x_;
+          Q.orw[d] = w_;
+          Q.ost[d * 3] = own_vals ? nst0 : Ls0;
+          Q.ost[d * 3 + 1] = own_vals ? nst1 : Ls1;
+          Q.ost[d * 3 + 2] = own_vals ? nst2 : Ls2;
+          Q.otuv[d * 3] = own_vals ? nt0 : Lt0;
+          Q.otuv[d * 3 + 1] = own_vals ? nt1 : Lt1;
+          Q.otuv[d * 3 + 2] = own_vals ? nt2 : Lt2;
+          Q.pos[base + i_] = wpos;
+        }
+      }
+      if (lane == 0) {
+        Q.pos[base + wid] = -1;
+        Q.sc_i[SI_NOPEN * B + b] = last;
+        Q.sc_i[SI_CUR * B + b] = wid;
+        Q.cur_g[b] = __longlong_as_double(s_win[1]);
+        Q.cur_ix[b] = s_win[2];
+      }
+    }
+  }
+  __syncthreads();
+  BookRec br;
+  br.v[RC_GO] = s_go;
+  br.v[RC_LOOP] = loop;
+  br.v[RC_NN0] = nn0;
+  br.v[RC_NNEW] = s_nnew;
+  br.v[RC_NOPEN] = s_nopen;
+  br.v[RC_CUR] = cur0;
+  br.v[RC_IW] = s_go ? s_win[2] : 0;
+  br.v[RC_N - 1] = 0;
+#undef PSTAMP
+  return br;
+}
+
 // Waves per SIMD each shape is compiled for.  The full-width shape (4-wave blocks, 1,280 of them at 256
 // scenes) is occupancy-bound: 133 VGPRs would allow 3 waves per SIMD; 4 costs 20 B of spills and gains
 // 0.3 ms per plan (r04zc: 29.7 vs 30.0 ms; round 4 had drifted to 169 VGPRs, 2 waves, 31.5 ms).  The
@@ -2659,6 +3099,82 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   }
 }
 
+
+
+// ha_pipe_kernel: the pipelined tail's launch (see above).  Items per slot: 0 RS_connected(n_it), 1 the
+// bookkeeping, 2 .. 1 + n_groups the expansion of n_{it+1}.  boot = 1: only the expansion, of n_it itself
+// (node buffer (it - 1) & 1) into E[it & 1], for the first pipelined launch.
+template <int HWt, int NBGt>
+__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE_TAIL))) void ha_pipe_kernel(
+    HaDev P, HaSearch Q, IterArgs A, int B, int it, int boot) {
+  __shared__ int role, sh_go;
+  unsigned long long* stp = nullptr;
+  if (HA_STAMP_CODE && A.stamps && !boot && it % HA_STAMP_EVERY == 0 && it / HA_STAMP_EVERY < 40 &&
+      (int)blockIdx.x < A.stamp_blocks && threadIdx.x == 0)
+    stp = A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
+  if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int ng = (P.n_prim + NBGt - 1) / NBGt, per = 2 + ng;
+  const int slot = blockIdx.x / per, item = blockIdx.x % per;
+  const int n_live = A.n_live ? *A.n_live : A.n_active;
+  if (slot >= n_live) return;
+  const int s = A.scene_of ? A.scene_of[slot] : slot;
+  if (!A.n_live && A.active && !A.active[s]) return;
+  const int np = P.n_prim;
+  if (item >= 2) {  // the expansion of n_{it+1} (boot: of n_it) into E[(it + 1) & 1] (boot: E[it & 1])
+    IterArgs X = e_par(A, B, np, boot ? (it & 1) : ((it + 1) & 1));
+    if (!boot) {  // wait for the bookkeeping's pop (its block precedes this one in dispatch order)
+      X.node = Q.node + (size_t)(it & 1) * 3 * B;
+      X.node_ag = 1;
+      X.node_flag = Q.nx;
+      X.node_flag_min = 2 * it + 2;
+    }
+    X.do_rs = 0;
+    ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 1);
+    return;
+  }
+  if (boot) return;
+  if (item == 0) {
+    if (!ha_iter_body<HWt, NBGt, true>(P, A, stp, slot, 0)) return;
+    ha_stores_done();
+    __syncthreads();
+  }
+  if (stp) __hip_atomic_store(stp + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (stp) __hip_atomic_store(stp + 5, (unsigned long long)(item == 0 ? 2 : 1) | ((unsigned long long)s << 4) |
+                                           ((unsigned long long)(item == 0 ? 0 : 17) << 32),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the final ticket: RS_connected (item 0) and the bookkeeping (item 1), as in ha_step_kernel
+  long long* rc = Q.rec + (size_t)RC_N * s;
+  if (item == 1) {
+    const BookRec br = ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, stp);
+    if (threadIdx.x == 0) {
+      if (stp) __hip_atomic_store(stp + 3, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(Q.tk + B + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+        asm volatile("" ::: "memory");
+        st_ag(Q.tk + B + s, 0);
+        ha_finish(Q, A, B, it, s, br);
+        if (stp) __hip_atomic_store(stp + 4, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+#pragma unroll
+        for (int i = 0; i < RC_N - 1; i++) st_ag(rc + i, br.v[i]);
+        ha_stores_done();
+        st_ag(rc + RC_N - 1, 1LL);  // record ready
+      }
+    }
+    return;
+  }
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(Q.tk + B + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+    asm volatile("" ::: "memory");
+    st_ag(Q.tk + B + s, 0);
+    while (ld_ag(rc + RC_N - 1) == 0) __builtin_amdgcn_s_sleep(1);
+    BookRec br;
+#pragma unroll
+    for (int i = 0; i < RC_N - 1; i++) br.v[i] = ld_ag(rc + i);
+    st_ag(rc + RC_N - 1, 0LL);
+    ha_finish(Q, A, B, it, s, br);
+    if (stp) __hip_atomic_store(stp + 4, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 
 // ------------------------------------------------------------- path finishing
@@ -3032,7 +3548,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + 256 * 48);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 4 + 256 * 50);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -3073,14 +3589,17 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.otuv = (double*)take(nB * C * 24);
   Q.node_tuv = (double*)take(nB * 48);
   Q.pre = (long long*)take(nB * PRE_W * 8);
+  Q.nx = (int*)take(nB * 4);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
   const double* dstart = mp_upload(ctx, WS_IO0, start, 3 * nB, &st);
   A.h = (double*)mp_ws(ctx, WS_IO1, sizeof(double) * nB * np);
-  A.nb = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * nB * np * 3);
-  A.idx = (long long*)mp_ws(ctx, WS_IO3, sizeof(long long) * nB * np);
-  A.fr = (unsigned char*)mp_ws(ctx, WS_IO4, nB * np);
+  // the expansion records (nb, idx, fr, hp_*) hold two parities: ha_pipe_kernel's launch it reads E[it & 1]
+  // while its expansion blocks write E[(it + 1) & 1]; every other launch uses parity 0
+  A.nb = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * nB * np * 3 * 2);
+  A.idx = (long long*)mp_ws(ctx, WS_IO3, sizeof(long long) * nB * np * 2);
+  A.fr = (unsigned char*)mp_ws(ctx, WS_IO4, nB * np * 2);
   A.rs_ok = (unsigned char*)mp_ws(ctx, WS_IO5, nB);
   A.rs_len = (int*)mp_ws(ctx, WS_IO6, sizeof(int) * nB);
   A.rs_path = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * nB * MAXPATH * 3);
@@ -3166,6 +3685,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.live, 0, sizeof(int) * (mp + 2), ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.tk, 0, sizeof(int) * 2 * nB, ctx->stream));  // the finishers reset them
   MP_HIP(ctx, hipMemsetAsync(Q.rec, 0, sizeof(long long) * RC_N * nB, ctx->stream));  // record-ready flags
+  MP_HIP(ctx, hipMemsetAsync(Q.nx, 0, sizeof(int) * nB, ctx->stream));  // ha_pipe_kernel's pop flags
   hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
   MP_HIP(ctx, hipGetLastError());
   // The whole search loop is enqueued without host round trips: iteration i = one ha_step_kernel
@@ -3190,9 +3710,16 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // 4 neighbours per group (62: yes).  (A/B) MPGPU_HA_TAIL_RSH=0: the groups' own word search.
   static const bool rsh_env = !getenv("MPGPU_HA_TAIL_RSH") || atoi(getenv("MPGPU_HA_TAIL_RSH")) != 0;
   const bool tail_rsh = HA_TAIL_RSH && rsh_env && !split && NBG_TAIL == 4 && per_tail - 1 >= 4 * ((np + 15) / 16);
-  A.hp_c = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * nB * np * 4);
-  A.hp_i = (int*)mp_ws(ctx, WS_IO12, sizeof(int) * nB * np * 4);
-  A.hp_t = (double*)mp_ws(ctx, WS_IO14, sizeof(double) * nB * np * 12);
+  A.hp_c = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * nB * np * 4 * 2);
+  A.hp_i = (int*)mp_ws(ctx, WS_IO12, sizeof(int) * nB * np * 4 * 2);
+  A.hp_t = (double*)mp_ws(ctx, WS_IO14, sizeof(double) * nB * np * 12 * 2);
+  // (A/B) MPGPU_HA_PIPE=0: the tail keeps ha_step_kernel (expansion, then the whole bookkeeping per launch)
+  static const bool pipe_env = !getenv("MPGPU_HA_PIPE") || atoi(getenv("MPGPU_HA_PIPE")) != 0;
+  const bool tail_pipe = tail_rsh && pipe_env;
+  // the pipelined launch's expansion blocks wait for their bookkeeping on a CU each: it pays only while the
+  // whole launch is resident at once (one 12-wave block per CU); (A/B) MPGPU_HA_PIPE_BLOCKS
+  const int pipe_blocks = getenv("MPGPU_HA_PIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_PIPE_BLOCKS")) : 256;
+  bool piped = false;
   // (A/B) MPGPU_HA_PRESCAN=1: the prescan block's PRE_K least entries merged into popfirst!.  Measured slower
   // (r05j, lone 729-pop scenario: 26.6 vs 25.7 us per iteration): its PRE_K DPP rounds on 12 waves took ~6 us
   // and the merge's readlane chains ~2.6 us, so the bookkeeping started later than it saved.  Off by default
@@ -3231,6 +3758,15 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       else
         hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
       hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
+    } else if (tail && tail_pipe && known * (2 + (np + NBG_TAIL - 1) / NBG_TAIL) <= pipe_blocks) {
+      const int per_pipe = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
+      if (!piped) {  // the current nodes' expansion, for the first pipelined launch
+        hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL),
+                           0, ctx->stream, D, Q, A, B, it, 1);
+        piped = true;
+      }
+      hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), 0,
+                         ctx->stream, D, Q, A, B, it, 0);
     } else if (tail) {
       if (tail_rsh)  // + the prescan block per scene
         hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL, true>), dim3((unsigned)(known * (per_tail + 1))),

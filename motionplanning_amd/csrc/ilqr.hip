@@ -1362,8 +1362,13 @@ __global__ __launch_bounds__(64 * (1 + kFusedDW)) void ilqr_backward_fused_kerne
     // derivative wave w: tasks w, w + DW, w + 2 DW, ... of the sequence (group g, part p) = (t / 4, t % 4),
     // in order.  No deadlock: the sweep waits for the least unfinished group g0, every task of a group
     // <= g0 + RG - 1 runs without waiting for a slot, and a wave reaches its task of g0 after finishing
-    // only tasks of earlier groups.  (A shared task counter -- one lane's LDS atomic broadcast to the
-    // wave -- was miscompiled into a loop that reran a task without fetching the next: the kernel hung.)
+    // only tasks of earlier groups.  (A first version fetched tasks from a shared LDS counter -- one lane's
+    // LDS atomic broadcast to the wave -- and hung; its cause was not isolated before the static order replaced
+    // it, and the counter protocol itself is sound: tools/ubench/task_counter.hip runs it -- readfirstlane or
+    // __shfl broadcast, with and without a divergent branch before the fetch, 7 producer waves feeding a
+    // consumer wave through per-slot LDS counts as here -- 200 x 256 blocks x 200 tasks with every task run
+    // exactly once, profiles/r05j_task_counter.txt, fetch ISA in profiles/r05j_task_counter_fetch_isa.txt.
+    // So it was not a miscompile of the counter; the LDS-count hand-offs below are the ones that test runs.)
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6) - 1, lane = tid & 63;
     const int kk = lane / kQuadIPB, ci = lane % kQuadIPB;
     const int ncol = n - col0;
