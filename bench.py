@@ -499,8 +499,8 @@ def bench_hastar(ctx, world, rank, cpu=None):
 
 def hastar_shard_projection(ctx, t_all, world=8):
     """The one-GPU proxy of configs[3]'s 1->8 strong scaling: each of the 8 shards a world-8 job would
-    give one rank, planned alone on this GPU (median of 3), for the contiguous split the bench used
-    through round 3 and the strided one it uses now (distributed.shard_indices).  The 8-GPU plan time is
+    give one rank, planned alone on this GPU (median of 3), for the contiguous split (the default again
+    from round 5, distributed.HA_STRIDED) and the strided one (round 4's).  The 8-GPU plan time is
     at least the slowest shard's, so T(256) / max T(shard) projects the speed-up."""
     from motionplanning_amd import distributed as D
     from motionplanning_amd import hybrid_astar as ha

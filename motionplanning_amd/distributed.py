@@ -9,9 +9,9 @@ does exactly one all-gather at the end, the exchange step the north star names:
   the rank's block with ``scene_base = a`` (the Philox counter word), so every scene draws
   the stream it would draw on one GPU; then an all-gather of the optimal controls
   (S×H×2 f64 — 6.4 KB per rank at 8 scenes × H=50) plus the per-scene scalars;
-* Hybrid A* (configs[3]): scenarios r, r + world, r + 2 world, ... per rank (strided: every rank
-  gets the same mix of perpendicular and parallel scenes), each rank runs its own lockstep search
-  (``mp_ha_plan``); all-gather of the outcome (found, pops, nodes, RS length) back into batch order;
+* Hybrid A* (configs[3]): a contiguous block of scenarios per rank (``HA_STRIDED``), each rank runs its
+  own lockstep search (``mp_ha_plan``); all-gather of the outcome (found, pops, nodes, RS length) back
+  into batch order;
 * iLQR (configs[2]): instances [a, b) per rank (replicas of the solver); all-gather of
   J and the iteration counts.
 
@@ -58,12 +58,16 @@ def shard_bounds(n, rank, world):
     return a, a + base + (1 if rank < rem else 0)
 
 
+# Hybrid A*'s split.  Round 4 defaulted to strided (every rank the same mix of perpendicular and parallel
+# scenes); every one-GPU world-8 projection since measured the contiguous split ahead (round 5: 1.29-1.35x vs
+# 1.12-1.25x, profiles/r05*_ha_*; the strided shard that draws the 729-pop scenario also draws more long
+# searches), so round 5 returns to contiguous blocks.
+HA_STRIDED = False
+
+
 def shard_indices(n, rank, world, strided=False):
     """The units of `rank`: the contiguous block shard_bounds gives, or (strided) every world-th unit
-    from `rank` on.  Both give rank r the same number of units (the first n % world ranks one extra).
-    Hybrid A* uses the strided split: scenario_batch lists its 128 perpendicular scenes before the 128
-    parallel ones, and a contiguous split hands every long perpendicular search to the first half of
-    the ranks, while the strided split gives every rank the same mix."""
+    from `rank` on.  Both give rank r the same number of units (the first n % world ranks one extra)."""
     if strided:
         return np.arange(rank, n, world)
     a, b = shard_bounds(n, rank, world)
@@ -140,18 +144,18 @@ def hybrid_astar_sharded(searchers, planner=None, ctx=None, max_pops=5000):
 
     rank, world = _world()
     n = len(searchers)
-    mine = [searchers[i] for i in shard_indices(n, rank, world, strided=True)]
+    mine = [searchers[i] for i in shard_indices(n, rank, world, strided=HA_STRIDED)]
     if mine:
         (planner or (lambda hs: ha.plan_batch(hs, ctx=ctx, max_pops=max_pops)))(mine)
     out = np.array([[int(h.r.found), h.r.loop_count, h.r.n_nodes, h.r.RSpath_final.shape[1]] for h in mine],
                    np.int64).reshape(-1, 4)
-    g = all_gather_rows(out, n, strided=True)
+    g = all_gather_rows(out, n, strided=HA_STRIDED)
     return dict(found=g[:, 0].astype(bool), pops=g[:, 1], n_nodes=g[:, 2], rs_len=g[:, 3])
 
 
 def track_sharded(searchers, ctx=None, settings=None, runner=None):
     """retrievePath + the main_Tracker.jl loop for this rank's shard of a planned batch (the same
-    strided split as hybrid_astar_sharded, so each rank tracks what it planned).  Every rank returns
+    split as hybrid_astar_sharded, so each rank tracks what it planned).  Every rank returns
     the gathered {status, n_steps} for the whole batch.  `runner(mine)` replaces the device calls
     (the gloo tests run the oracle there)."""
     from . import hybrid_astar as ha
@@ -159,7 +163,7 @@ def track_sharded(searchers, ctx=None, settings=None, runner=None):
 
     rank, world = _world()
     n = len(searchers)
-    mine = [searchers[i] for i in shard_indices(n, rank, world, strided=True)]
+    mine = [searchers[i] for i in shard_indices(n, rank, world, strided=HA_STRIDED)]
     if mine and runner is not None:
         runner(mine)
     elif mine:
@@ -167,7 +171,7 @@ def track_sharded(searchers, ctx=None, settings=None, runner=None):
         tracker.track_batch(mine, ctx=ctx, settings=settings)
     inv = {v: k for k, v in tracker.STATUS.items()}
     out = np.array([[inv[h.r.tracking["status"]], h.r.tracking["n_steps"]] for h in mine], np.int64).reshape(-1, 2)
-    g = all_gather_rows(out, n, strided=True)
+    g = all_gather_rows(out, n, strided=HA_STRIDED)
     return dict(status=g[:, 0], n_steps=g[:, 1])
 
 
