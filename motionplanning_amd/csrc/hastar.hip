@@ -607,6 +607,7 @@ struct IterArgs {
   const double* htn;
   const double* htk;
   int no_pre;  // (A/B, MPGPU_HA_PRESCAN=0) the prescan block only marks its record stale: the bookkeeping scans
+  int rs_last;  // (A/B, MPGPU_HA_RS_LAST=1) ha_step_kernel dispatches the RS_connected blocks last
   int node_ag;  // read the node agent-coherently (written in this launch), once node_flag[s] >= node_flag_min
   const int* node_flag;
   int node_flag_min;
@@ -3019,10 +3020,15 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
     stp = A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int per = 1 + (P.n_prim + NBGt - 1) / NBGt + (RSH ? 1 : 0);
-  const int slot = blockIdx.x / per, item = blockIdx.x % per;
+  int slot = blockIdx.x / per, item = blockIdx.x % per;
+  if (!RSH && A.rs_last) {  // (A/B) the RS_connected blocks after every neighbour group in dispatch order
+    const int n = gridDim.x / per, G = per - 1, bid = blockIdx.x;
+    if (bid < n * G) { slot = bid / G; item = 1 + bid % G; }
+    else { slot = bid - n * G; item = 0; }
+  }
   if (RSH && item == per - 1) {  // the prescan block: counted among the bookkeeping's arrivals
     if (!ha_prescan<64 * HWt>(Q, A, B, it, slot, stp)) return;
-  } else if (!ha_iter_body<HWt, NBGt, RSH>(P, A, stp)) {
+  } else if (!ha_iter_body<HWt, NBGt, RSH>(P, A, stp, slot, item)) {
     return;  // block-uniform: no work for this block (not counted)
   }
   const int s = A.scene_of ? A.scene_of[slot] : slot;
@@ -3727,6 +3733,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool pre_env = getenv("MPGPU_HA_PRESCAN") && atoi(getenv("MPGPU_HA_PRESCAN")) == 1;
   static const bool tuv_env = !getenv("MPGPU_HA_TUV") || atoi(getenv("MPGPU_HA_TUV")) != 0;
   A.no_pre = !pre_env;
+  static const bool rs_last_env = getenv("MPGPU_HA_RS_LAST") && atoi(getenv("MPGPU_HA_RS_LAST")) == 1;
+  A.rs_last = rs_last_env;
   A.no_tuv = !tuv_env;
   if (!A.hp_c || !A.hp_i || !A.hp_t) return MP_ERR_NOMEM;
   // iteration it >= 2 works on the compact list of scenes still live (written by the previous
