@@ -607,10 +607,11 @@ struct IterArgs {
   const double* htn;
   const double* htk;
   int no_pre;  // (A/B, MPGPU_HA_PRESCAN=0) the prescan block only marks its record stale: the bookkeeping scans
-  int rs_last;  // (A/B, MPGPU_HA_RS_LAST=1) ha_step_kernel dispatches the RS_connected blocks last
+  int rs_last;  // ha_step_kernel dispatches the RS_connected blocks last ((A/B) MPGPU_HA_RS_LAST=0: first)
   int node_ag;  // read the node agent-coherently (written in this launch), once node_flag[s] >= node_flag_min
   const int* node_flag;
   int node_flag_min;
+  int* node_flag_err;  // the wait is bounded: past HA_SPIN_MAX polls it sets *node_flag_err and gives up
   int no_tuv;  // (A/B, MPGPU_HA_TUV=0) nodes keep only their winner id: RS_connected evaluates its word
 };
 
@@ -664,6 +665,23 @@ __device__ __forceinline__ long long expand_nb(const HaDev& P, const IterArgs& A
   regulate(P, t, nb);
   if (sn) mpj_sincos_bl(nb[2], sn, cn);
   return encode(P, nb);
+}
+
+// Bounded cross-block wait (ha_pipe_kernel, ha_persist_kernel): poll *p until it is >= v; past HA_SPIN_MAX
+// polls (~1 s) set *err and return HA_DONE (every waiter then leaves its loop: a wrong result, not a hang)
+constexpr int HA_DONE = 0x3ffffffe;  // a scene's flag once its search ended (even: no next node)
+constexpr long long HA_SPIN_MAX = 1LL << 24;
+__device__ __forceinline__ int wait_ge(const int* p, int v, int* err) {
+  int f = ld_ag(p);
+  for (long long n = 0; f < v; n++) {
+    if (n >= HA_SPIN_MAX) {
+      if (err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return HA_DONE;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    f = ld_ag(p);
+  }
+  return f;
 }
 
 // output addressing: per scene
@@ -931,11 +949,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   if (tid < NBG) g_free[tid] = 1;
   if (A.node_ag) {  // the node comes from another block of this launch (ha_pipe_kernel's bookkeeping): wait for
     // its ready flag (the walls are staged meanwhile), then read it agent-coherently
-    if (tid == 0) {
-      int f;
-      while ((f = ld_ag(A.node_flag + s)) < A.node_flag_min) __builtin_amdgcn_s_sleep(1);
-      nd_go = f & 1;
-    }
+    if (tid == 0) nd_go = wait_ge(A.node_flag + s, A.node_flag_min, A.node_flag_err) & 1;
     __syncthreads();
     if (!nd_go) return false;  // block-uniform: the search ended, nothing to expand
     if (tid < 3) nd_s[tid] = ld_ag(A.node + 3 * s + tid);
@@ -1014,7 +1028,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   if (rs) {
     // allpath + findmin: RS_connected's optimal command from the popped node
     double ns[3];
-    const int known = A.node_rw ? A.node_rw[s] : -1;  // the popped node's stored rs_heuristic winner
+    // the popped node's stored rs_heuristic winner (agent-coherently when published in this launch)
+    const int known = A.node_rw ? (A.node_ag ? ld_ag(A.node_rw + s) : A.node_rw[s]) : -1;
     if (tabm >= 0)
       change_basis_sc(node, goal, P.minR, A.htn[2 * tabm], A.htn[2 * tabm + 1], ns);
     else
@@ -1022,7 +1037,11 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     HTIME(2);
     HSTAMP(12);
     if (known >= 0 && (known & RW_TUV)) {  // block-uniform: the commands stored at the node's creation
-      if (tid == 0) cmd_from_tuv(known, A.node_tuv + 3 * s, cmd);
+      if (tid == 0) {
+        double tv[3];
+        for (int e = 0; e < 3; e++) tv[e] = A.node_ag ? ld_ag(A.node_tuv + 3 * s + e) : A.node_tuv[3 * s + e];
+        cmd_from_tuv(known, tv, cmd);
+      }
     } else if (known >= 0 && known < 48)
       rs_known_cmd(ns, tid, known, cmd);
     else
@@ -1129,7 +1148,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     __syncthreads();
     const int n = nst + 1;
     if (!A.rs_path_free_only)
-      for (int i = tid; i < 3 * n; i += HT) R.path[i] = path_s[i];
+      for (int i = tid; i < 3 * n; i += HT) st_out(A.coherent, R.path + i, path_s[i]);
     if (tid == 0) sh_n = n;
     HTIME(4);
     sweep(n > 5 ? (n - 1) / 5 + 1 : 1);  // block_collision_check on poses 1:5:end
@@ -1249,7 +1268,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       st_out(A.coherent, R.len, sh_n);
     }
     if (A.rs_path_free_only && g_free[0])  // block-uniform (after the barrier above)
-      for (int i = tid; i < 3 * sh_n; i += HT) R.path[i] = path_s[i];
+      for (int i = tid; i < 3 * sh_n; i += HT) st_out(A.coherent, R.path + i, path_s[i]);  // (read by ha_persist_kernel)
   } else if (tid < 64 && (lane & 3) == 0 && j < nk) {
     const int fr = g_ix[j] != 0 && g_free[j];
     st_out(A.coherent, R.fr + k0 + j, (unsigned char)fr);
@@ -1473,6 +1492,9 @@ struct HaSearch {
   double* node_tuv;      // [2][B][3] popped node's, double-buffered like node
   long long* pre;        // [B][PRE_W] (RSH tail) the prescan's record: popfirst!'s K least entries before FindNewNode
   int* nx;               // [B] (ha_pipe_kernel) 2·it + 2 + go once iteration it's bookkeeping has popped the next node
+  int* ex;               // [B] (ha_persist_kernel) expansions finished (neighbour groups, cumulative)
+  int* rsr;              // [B] (ha_persist_kernel) 2·it + 2 once RS_connected(n_it) has run
+  int* err;              // [1] (ha_persist_kernel) a bounded wait ran out (the search is then not trusted)
 };
 // prescan record: [0] iteration tag, [1] kc = min(K, n_open), then K entries of 13 words: f (bits), seq, position,
 // node id, g (bits), Encode index, state (3, bits), rw, (t, u, v) (3, bits)
@@ -2389,7 +2411,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
 // the scene's iteration ends (one thread): the termination of :259-271 when RS_connected found a path,
 // else the speculative pop's results published and the scene listed for the next iteration
 __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, int B, int it, int b,
-                                          const BookRec& br) {
+                                          const BookRec& br, bool list = true) {
   const long long* rc = br.v;
   const int go = (int)rc[RC_GO], loop = (int)rc[RC_LOOP];
   const int rs_ok = ld_ag(A.rs_ok + b);
@@ -2418,7 +2440,7 @@ __device__ __forceinline__ void ha_finish(const HaSearch& Q, const IterArgs& A, 
   if (go) {
     Q.sc_i[SI_LOOP * B + b] = loop + 1;
     Q.pop_seq[(size_t)b * Q.mp + loop] = rc[RC_IW];
-    Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;
+    if (list) Q.lst[(it & 1) * B + atomicAdd(Q.live + it, 1)] = b;  // (ha_persist_kernel keeps no list)
   } else {
     Q.sc_i[SI_ACTIVE * B + b] = 0;
     Q.sc_i[SI_NOPEN * B + b] = (int)rc[RC_NOPEN];
@@ -3021,7 +3043,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int per = 1 + (P.n_prim + NBGt - 1) / NBGt + (RSH ? 1 : 0);
   int slot = blockIdx.x / per, item = blockIdx.x % per;
-  if (!RSH && A.rs_last) {  // (A/B) the RS_connected blocks after every neighbour group in dispatch order
+  if (!RSH && A.rs_last) {  // the RS_connected blocks after every neighbour group in dispatch order
     const int n = gridDim.x / per, G = per - 1, bid = blockIdx.x;
     if (bid < n * G) { slot = bid / G; item = 1 + bid % G; }
     else { slot = bid - n * G; item = 0; }
@@ -3133,6 +3155,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE
       X.node_ag = 1;
       X.node_flag = Q.nx;
       X.node_flag_min = 2 * it + 2;
+      X.node_flag_err = Q.err;
     }
     X.do_rs = 0;
     ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 1);
@@ -3179,6 +3202,101 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE
     st_ag(rc + RC_N - 1, 0LL);
     ha_finish(Q, A, B, it, s, br);
     if (stp) __hip_atomic_store(stp + 4, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+
+// ha_persist_kernel: the pipelined tail as ONE launch for the rest of the search, once every block of it can be
+// resident at once (cooperative launch): per scene an RS_connected block, the bookkeeping block and the expansion
+// groups each loop over the iterations, handing over through per-scene flags instead of launch boundaries --
+// the bookkeeping publishes n_{it+1} (Q.nx, as ha_pipe_kernel), the groups expand it into E[(it+1) & 1] and
+// count themselves in (Q.ex), RS_connected(n_it) signals its verdict (Q.rsr; verdict and path in the iteration's
+// parity buffer); the bookkeeping of iteration it waits for E[it & 1] and RS_connected(n_it) and finishes the
+// iteration as ha_step_kernel's finisher.  A finished scene publishes HA_DONE: every block of it leaves its loop.
+// Same operations on the same values as ha_pipe_kernel: the same search, bit for bit.  Every wait is bounded.
+template <int HWt, int NBGt>
+__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE_TAIL))) void ha_persist_kernel(
+    HaDev P, HaSearch Q, IterArgs A, int B, int it0, double* rs_path2, unsigned char* rs_ok2, int* rs_len2) {
+  __shared__ int sh_f;
+  const int np = P.n_prim, ng = (np + NBGt - 1) / NBGt, per = 2 + ng;
+  const int slot = blockIdx.x / per, item = blockIdx.x % per;
+  const int n_live = A.n_live ? *A.n_live : A.n_active;
+  if (slot >= n_live) return;
+  const int s = A.scene_of ? A.scene_of[slot] : slot;
+  if (!A.n_live && A.active && !A.active[s]) return;
+  // RS_connected's outputs in the iteration's parity (the next iteration's may be written before the
+  // bookkeeping reads this one's)
+  auto rs_par = [&](IterArgs& X, int it) {
+    X.rs_ok = rs_ok2 + (size_t)(it & 1) * B;
+    X.rs_len = rs_len2 + (size_t)(it & 1) * B;
+    X.rs_path = rs_path2 + (size_t)(it & 1) * B * MAXPATH * 3;
+  };
+  if (item >= 2) {  // the expansion of n_{it+1}, it = it0, it0 + 1, ...
+    for (int it = it0;; it++) {
+      IterArgs X = e_par(A, B, np, (it + 1) & 1);
+      X.node = Q.node + (size_t)(it & 1) * 3 * B;
+      X.node_ag = 1;
+      X.node_flag = Q.nx;
+      X.node_flag_min = 2 * it + 2;
+      X.node_flag_err = Q.err;
+      X.do_rs = 0;
+      if (!ha_iter_body<HWt, NBGt, true>(P, X, nullptr, slot, item - 1)) return;  // the search ended
+      ha_stores_done();
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(Q.ex + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (item == 0) {  // RS_connected(n_it), it = it0, it0 + 1, ...
+    for (int it = it0;; it++) {
+      IterArgs X = A;
+      X.node = Q.node + (size_t)((it - 1) & 1) * 3 * B;
+      X.node_rw = Q.node_rw + (size_t)((it - 1) & 1) * B;
+      X.node_tuv = Q.node_tuv + (size_t)((it - 1) & 1) * 3 * B;
+      if (it > it0) {  // n_it: published by iteration it - 1's bookkeeping in this launch
+        X.node_ag = 1;
+        X.node_flag = Q.nx;
+        X.node_flag_min = 2 * (it - 1) + 2;
+        X.node_flag_err = Q.err;
+      }
+      rs_par(X, it);
+      X.do_exp = 0;
+      if (!ha_iter_body<HWt, NBGt, true>(P, X, nullptr, slot, 0)) return;
+      ha_stores_done();
+      __syncthreads();
+      if (threadIdx.x == 0) st_ag(Q.rsr + s, 2 * it + 2);
+    }
+  }
+  // item 1: the bookkeeping of iteration it, it = it0, it0 + 1, ...
+  for (int it = it0;; it++) {
+    if (it > it0) {  // E[it & 1]: every group of iteration it - 1 has expanded n_it
+      if (threadIdx.x == 0) wait_ge(Q.ex + s, ng * (it - it0), Q.err);
+      __syncthreads();
+    }
+    const BookRec br = ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s);
+    IterArgs F = A;
+    rs_par(F, it);
+    if (threadIdx.x == 0) {
+      // RS_connected(n_it) done; Q.rsr may already hold iteration it + 1's flag (that RS block starts once this
+      // iteration's pop is published), the verdict itself stays in the parity buffer until iteration it + 2
+      const int f = wait_ge(Q.rsr + s, 2 * it + 2, Q.err);
+      if (f == HA_DONE) {
+        sh_f = 2;
+      } else {
+        ha_finish(Q, F, B, it, s, br, false);
+        sh_f = ld_ag(F.rs_ok + s) ? 1 : !br.v[RC_GO] ? 2 : 0;
+      }
+    }
+    __syncthreads();
+    if (sh_f == 1) {  // RSpath_final into the canonical buffer the host reads
+      const int n = ld_ag(F.rs_len + s);
+      for (int i = threadIdx.x; i < 3 * n; i += 64 * HWt)
+        A.rs_path[(size_t)s * MAXPATH * 3 + i] = ld_ag(F.rs_path + (size_t)s * MAXPATH * 3 + i);
+    }
+    if (sh_f) {
+      if (threadIdx.x == 0) st_ag(Q.nx + s, HA_DONE);
+      return;
+    }
+    __syncthreads();
   }
 }
 
@@ -3554,7 +3672,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 4 + 256 * 50);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + 256 * 54);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -3596,6 +3714,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.node_tuv = (double*)take(nB * 48);
   Q.pre = (long long*)take(nB * PRE_W * 8);
   Q.nx = (int*)take(nB * 4);
+  Q.ex = (int*)take(nB * 4);
+  Q.rsr = (int*)take(nB * 4);
+  Q.err = (int*)take(4);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
@@ -3692,6 +3813,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.tk, 0, sizeof(int) * 2 * nB, ctx->stream));  // the finishers reset them
   MP_HIP(ctx, hipMemsetAsync(Q.rec, 0, sizeof(long long) * RC_N * nB, ctx->stream));  // record-ready flags
   MP_HIP(ctx, hipMemsetAsync(Q.nx, 0, sizeof(int) * nB, ctx->stream));  // ha_pipe_kernel's pop flags
+  MP_HIP(ctx, hipMemsetAsync(Q.ex, 0, sizeof(int) * nB, ctx->stream));  // ha_persist_kernel's flags
+  MP_HIP(ctx, hipMemsetAsync(Q.rsr, 0, sizeof(int) * nB, ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.err, 0, sizeof(int), ctx->stream));
   hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
   MP_HIP(ctx, hipGetLastError());
   // The whole search loop is enqueued without host round trips: iteration i = one ha_step_kernel
@@ -3722,6 +3846,26 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // (A/B) MPGPU_HA_PIPE=0: the tail keeps ha_step_kernel (expansion, then the whole bookkeeping per launch)
   static const bool pipe_env = !getenv("MPGPU_HA_PIPE") || atoi(getenv("MPGPU_HA_PIPE")) != 0;
   const bool tail_pipe = tail_rsh && pipe_env;
+  // the persistent tail (ha_persist_kernel): one cooperative launch for the rest of the search once every block
+  // of it fits the device at once; (A/B) MPGPU_HA_PERSIST=0 keeps one ha_pipe_kernel launch per iteration
+  static const bool persist_env = !getenv("MPGPU_HA_PERSIST") || atoi(getenv("MPGPU_HA_PERSIST")) != 0;
+  int persist_cap = 0;
+  double* rs_path2 = nullptr;
+  int* rs_i2 = nullptr;
+  if (tail_pipe && persist_env) {
+    int nbpc = 0, cus = 0, coop = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbpc, reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
+                                                     64 * HW_TAIL, 0) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
+        hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device) == hipSuccess && coop)
+      persist_cap = nbpc * cus;
+    (void)hipGetLastError();
+    if (getenv("MPGPU_HA_VERBOSE")) fprintf(stderr, "ha_persist_kernel: %d blocks co-resident\n", persist_cap);
+    rs_path2 = (double*)mp_ws(ctx, WS_IO15, sizeof(double) * 2 * nB * MAXPATH * 3);
+    rs_i2 = (int*)mp_ws(ctx, WS_IO16, sizeof(int) * 4 * nB);
+    if (!rs_path2 || !rs_i2) return MP_ERR_NOMEM;
+  }
+  bool persisted = false;
   // the pipelined launch's expansion blocks wait for their bookkeeping on a CU each: it pays only while the
   // whole launch is resident at once (one 12-wave block per CU); (A/B) MPGPU_HA_PIPE_BLOCKS
   const int pipe_blocks = getenv("MPGPU_HA_PIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_PIPE_BLOCKS")) : 256;
@@ -3733,7 +3877,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool pre_env = getenv("MPGPU_HA_PRESCAN") && atoi(getenv("MPGPU_HA_PRESCAN")) == 1;
   static const bool tuv_env = !getenv("MPGPU_HA_TUV") || atoi(getenv("MPGPU_HA_TUV")) != 0;
   A.no_pre = !pre_env;
-  static const bool rs_last_env = getenv("MPGPU_HA_RS_LAST") && atoi(getenv("MPGPU_HA_RS_LAST")) == 1;
+  static const bool rs_last_env = !getenv("MPGPU_HA_RS_LAST") || atoi(getenv("MPGPU_HA_RS_LAST")) != 0;  // r05o: -0.2 ms
   A.rs_last = rs_last_env;
   A.no_tuv = !tuv_env;
   if (!A.hp_c || !A.hp_i || !A.hp_t) return MP_ERR_NOMEM;
@@ -3772,6 +3916,20 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL),
                            0, ctx->stream, D, Q, A, B, it, 1);
         piped = true;
+      }
+      if (known * per_pipe <= persist_cap) {  // the rest of the search in one cooperative launch
+        unsigned char* rs_ok2 = reinterpret_cast<unsigned char*>(rs_i2);
+        int* rs_len2 = rs_i2 + 2 * nB;
+        int it0 = it;
+        void* args[] = {&D, &Q, &A, (void*)&B, &it0, &rs_path2, &rs_ok2, &rs_len2};
+        if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
+                                       dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), args, 0,
+                                       ctx->stream) != hipSuccess) {
+          cleanup();
+          return mp_fail(ctx, MP_ERR_HIP, "ha_persist_kernel cooperative launch failed");
+        }
+        persisted = true;
+        break;
       }
       hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), 0,
                          ctx->stream, D, Q, A, B, it, 0);
@@ -3822,6 +3980,15 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       fwrite(h.data(), 8, h.size(), f);
       fclose(f);
     }
+  }
+  if (persisted) {  // a bounded wait that ran out means the search is not trusted
+    int err = 0;
+    if (hipMemcpyAsync(&err, Q.err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+      cleanup();
+      return mp_fail(ctx, MP_ERR_HIP, "persistent search failed");
+    }
+    if (err) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "persistent search: a cross-block wait timed out"); }
   }
   // outputs: per-scene counters, then the used prefix of pop_seq / states / RS paths
   std::vector<int> si(SI_N * nB);
