@@ -612,6 +612,10 @@ struct IterArgs {
   const int* node_flag;
   int node_flag_min;
   int* node_flag_err;  // the wait is bounded: past HA_SPIN_MAX polls it sets *node_flag_err and gives up
+  // (full-width ha_pipe_kernel) the popped node's g and the scene's node count before its FindNewNode, published
+  // with the node: the Dict pre-check then runs beside FindNewNode's writes (see ha_iter_body)
+  const double* node_g;
+  const int* node_nn;
   int no_tuv;  // (A/B, MPGPU_HA_TUV=0) nodes keep only their winner id: RS_connected evaluates its word
 };
 
@@ -920,8 +924,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   const int nw = P.n_walls;
   const double* node = A.node + 3 * s;
   const double* goal = A.goal + 3 * s;
-  __shared__ double nd_s[3];
-  __shared__ int nd_go;
+  __shared__ double nd_s[3], nd_g;
+  __shared__ int nd_go, nd_nn;
   const OutRef R = out_ref(A, s, P.n_prim);
   const int k0 = rs ? 0 : (item - 1) * NBG, nk = rs ? 0 : min(NBG, P.n_prim - k0);
   // wall corners (Block2Pts) and their SAT tables in LDS: precomputed once per plan
@@ -953,6 +957,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     __syncthreads();
     if (!nd_go) return false;  // block-uniform: the search ended, nothing to expand
     if (tid < 3) nd_s[tid] = ld_ag(A.node + 3 * s + tid);
+    if (tid == 3 && A.node_g) nd_g = ld_ag(A.node_g + s);
+    if (tid == 4 && A.node_g) nd_nn = ld_ag(A.node_nn + s);
     __syncthreads();
     node = nd_s;
   }
@@ -1238,11 +1244,18 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     // The Dict at this launch is the one this iteration's FindNewNode starts from (the bookkeeping
     // that changes it runs after every neighbour group of the scene, ha_step_kernel / ha_book_kernel).
     double gd = 0.0;
-    if (hit >= 0) gd = A.dg[(size_t)s * A.C + hit];  // loaded now, used after the sweep
+    if (hit >= 0) gd = A.dg[(size_t)s * A.C + hit];  // loaded now, used after the sweep (a node newer than
+    // the pipelined launch's nn_lim below may be half-written: its g is loaded but never used)
     sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
     HTIME(4);
     HSTAMP(13);
-    if (tid < nk) g_need[tid] = !A.dnid || !(hit >= 0 && !(A.cur_g[s] + P.expand_time < gd));
+    // (full-width ha_pipe_kernel) this iteration's FindNewNode writes the Dict meanwhile: only nodes older than
+    // it (id < its starting node count) are trusted, and their g only decreases, so the g read (the old or the
+    // new value) >= the g FindNewNode(n_{it+1}) compares with: a skip stays a skip
+    const bool pub = A.node_ag && A.node_g;
+    const int nn_lim = pub ? nd_nn : 0x7fffffff;
+    if (tid < nk)  // (A.cur_g only with a Dict: mp_ha_expand has neither)
+      g_need[tid] = !A.dnid || !(hit >= 0 && hit < nn_lim && !((pub ? nd_g : A.cur_g[s]) + P.expand_time < gd));
     __syncthreads();
     HTIME(5);
     HSTAMP(14);
@@ -1491,6 +1504,8 @@ struct HaSearch {
   double* otuv;          // [B][C][3] open entries: the same
   double* node_tuv;      // [2][B][3] popped node's, double-buffered like node
   long long* pre;        // [B][PRE_W] (RSH tail) the prescan's record: popfirst!'s K least entries before FindNewNode
+  double* node_g;        // [2][B] (full-width ha_pipe_kernel) the popped node's g, double-buffered like node
+  int* node_nn;          // [2][B] the scene's node count before the FindNewNode that published the node
   int* nx;               // [B] (ha_pipe_kernel) 2·it + 2 + go once iteration it's bookkeeping has popped the next node
   int* ex;               // [B] (ha_persist_kernel) expansions finished (neighbour groups, cumulative)
   int* rsr;              // [B] (ha_persist_kernel) 2·it + 2 once RS_connected(n_it) has run
@@ -2631,10 +2646,12 @@ __device__ __forceinline__ IterArgs e_par(const IterArgs& A, int B, int np, int 
   E.hp_c = A.hp_c + 4 * n;
   E.hp_i = A.hp_i + 4 * n;
   E.hp_t = A.hp_t + 12 * n;
+  E.h = A.h + n;  // (full-width pipe) rs_heuristic and its winner per neighbour
+  E.hw = A.hw ? A.hw + n : nullptr;
   return E;
 }
 
-template <int NT>
+template <int NT, bool RSH = true>
 __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& Q, const IterArgs& E, int B, int it,
                                                 int b, unsigned long long* stp = nullptr) {
 #define PSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -2678,29 +2695,34 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
     const size_t q = (size_t)b * np + tid;
     ix = ld_ag(E.idx + q);
     frk = ld_ag(E.fr + q);
-    double cv[4], ct[4][3];
-    int ci[4];
+    if (RSH) {
+      double cv[4], ct[4][3];
+      int ci[4];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      cv[c] = ld_ag(E.hp_c + q * 4 + c);
-      ci[c] = ld_ag(E.hp_i + q * 4 + c);
+      for (int c = 0; c < 4; c++) {
+        cv[c] = ld_ag(E.hp_c + q * 4 + c);
+        ci[c] = ld_ag(E.hp_i + q * 4 + c);
 #pragma unroll
-      for (int e = 0; e < 3; e++) ct[c][e] = ld_ag(E.hp_t + (q * 4 + c) * 3 + e);
+        for (int e = 0; e < 3; e++) ct[c][e] = ld_ag(E.hp_t + (q * 4 + c) * 3 + e);
+      }
+      double v = cv[0];
+      int id = ci[0], wc = 0;
+#pragma unroll
+      for (int c = 1; c < 4; c++)
+        if (rs_before(cv[c], ci[c], v, id)) { v = cv[c]; id = ci[c]; wc = c; }
+      hk = v * P.minR;
+      hwk = E.no_tuv ? id : id | RW_TUV | (v < __builtin_inf() ? RW_OK : 0);
+#pragma unroll
+      for (int e = 0; e < 3; e++) tuvk[e] = ct[0][e];
+#pragma unroll
+      for (int c = 1; c < 4; c++)
+        if (wc == c)
+#pragma unroll
+          for (int e = 0; e < 3; e++) tuvk[e] = ct[c][e];
+    } else {  // the full-width groups' own rs_heuristic and winner (as ha_book_spec<NT, false>)
+      hk = ld_ag(E.h + q);
+      if (E.hw) hwk = ld_ag(E.hw + q);
     }
-    double v = cv[0];
-    int id = ci[0], wc = 0;
-#pragma unroll
-    for (int c = 1; c < 4; c++)
-      if (rs_before(cv[c], ci[c], v, id)) { v = cv[c]; id = ci[c]; wc = c; }
-    hk = v * P.minR;
-    hwk = E.no_tuv ? id : id | RW_TUV | (v < __builtin_inf() ? RW_OK : 0);
-#pragma unroll
-    for (int e = 0; e < 3; e++) tuvk[e] = ct[0][e];
-#pragma unroll
-    for (int c = 1; c < 4; c++)
-      if (wc == c)
-#pragma unroll
-        for (int e = 0; e < 3; e++) tuvk[e] = ct[c][e];
     nb0 = ld_ag(E.nb + 3 * q);
     nb1 = ld_ag(E.nb + 3 * q + 1);
     nb2 = ld_ag(E.nb + 3 * q + 2);
@@ -2915,6 +2937,8 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
         st_ag(Q.node_tuv + (size_t)(it & 1) * 3 * B + 3 * b + lane, __longlong_as_double(s_win[7 + lane]));
       }
       if (lane == 0) st_ag(Q.node_rw + (size_t)(it & 1) * B + b, (int)s_win[6]);
+      if (!RSH && lane == 1) st_ag(Q.node_g + (size_t)(it & 1) * B + b, __longlong_as_double(s_win[1]));
+      if (!RSH && lane == 2) st_ag(Q.node_nn + (size_t)(it & 1) * B + b, nn0);
     }
     ha_stores_done();
     if (lane == 0) {
@@ -3132,8 +3156,8 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
 // ha_pipe_kernel: the pipelined tail's launch (see above).  Items per slot: 0 RS_connected(n_it), 1 the
 // bookkeeping, 2 .. 1 + n_groups the expansion of n_{it+1}.  boot = 1: only the expansion, of n_it itself
 // (node buffer (it - 1) & 1) into E[it & 1], for the first pipelined launch.
-template <int HWt, int NBGt>
-__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE_TAIL))) void ha_pipe_kernel(
+template <int HWt, int NBGt, bool RSH = true>
+__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == 4 ? HA_WPE_FULL : HA_WPE_TAIL))) void ha_pipe_kernel(
     HaDev P, HaSearch Q, IterArgs A, int B, int it, int boot) {
   __shared__ int role, sh_go;
   unsigned long long* stp = nullptr;
@@ -3156,14 +3180,23 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE
       X.node_flag = Q.nx;
       X.node_flag_min = 2 * it + 2;
       X.node_flag_err = Q.err;
+      if (!RSH) {  // the Dict pre-check beside FindNewNode's writes (ha_iter_body)
+        X.node_g = Q.node_g + (size_t)(it & 1) * B;
+        X.node_nn = Q.node_nn + (size_t)(it & 1) * B;
+      }
     }
     X.do_rs = 0;
-    ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 1);
+    ha_iter_body<HWt, NBGt, RSH>(P, X, stp, slot, item - 1);
+    if (stp) {
+      __hip_atomic_store(stp + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(stp + 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 1) << 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
   if (boot) return;
   if (item == 0) {
-    if (!ha_iter_body<HWt, NBGt, true>(P, A, stp, slot, 0)) return;
+    if (!ha_iter_body<HWt, NBGt, RSH>(P, A, stp, slot, 0)) return;
     ha_stores_done();
     __syncthreads();
   }
@@ -3174,7 +3207,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE
   // the final ticket: RS_connected (item 0) and the bookkeeping (item 1), as in ha_step_kernel
   long long* rc = Q.rec + (size_t)RC_N * s;
   if (item == 1) {
-    const BookRec br = ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, stp);
+    const BookRec br = ha_book_pipe<64 * HWt, RSH>(P, Q, e_par(A, B, np, it & 1), B, it, s, stp);
     if (threadIdx.x == 0) {
       if (stp) __hip_atomic_store(stp + 3, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (__hip_atomic_fetch_add(Q.tk + B + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
@@ -3672,7 +3705,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + 256 * 54);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + 256 * 56);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -3717,12 +3750,14 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.ex = (int*)take(nB * 4);
   Q.rsr = (int*)take(nB * 4);
   Q.err = (int*)take(4);
+  Q.node_g = (double*)take(nB * 16);
+  Q.node_nn = (int*)take(nB * 8);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
   const double* dstart = mp_upload(ctx, WS_IO0, start, 3 * nB, &st);
-  A.h = (double*)mp_ws(ctx, WS_IO1, sizeof(double) * nB * np);
-  // the expansion records (nb, idx, fr, hp_*) hold two parities: ha_pipe_kernel's launch it reads E[it & 1]
+  A.h = (double*)mp_ws(ctx, WS_IO1, sizeof(double) * nB * np * 2);
+  // the expansion records (nb, idx, fr, h, hw, hp_*) hold two parities: ha_pipe_kernel's launch it reads E[it & 1]
   // while its expansion blocks write E[(it + 1) & 1]; every other launch uses parity 0
   A.nb = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * nB * np * 3 * 2);
   A.idx = (long long*)mp_ws(ctx, WS_IO3, sizeof(long long) * nB * np * 2);
@@ -3730,7 +3765,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   A.rs_ok = (unsigned char*)mp_ws(ctx, WS_IO5, nB);
   A.rs_len = (int*)mp_ws(ctx, WS_IO6, sizeof(int) * nB);
   A.rs_path = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * nB * MAXPATH * 3);
-  A.hw = (int*)mp_ws(ctx, WS_IO9, sizeof(int) * nB * np);
+  A.hw = (int*)mp_ws(ctx, WS_IO9, sizeof(int) * nB * np * 2);
   if (st || !A.h || !A.nb || !A.idx || !A.fr || !A.rs_ok || !A.rs_len || !A.rs_path || !A.hw)
     return st ? st : MP_ERR_NOMEM;
 #ifndef HA_RS_WINNER
@@ -3869,7 +3904,11 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // the pipelined launch's expansion blocks wait for their bookkeeping on a CU each: it pays only while the
   // whole launch is resident at once (one 12-wave block per CU); (A/B) MPGPU_HA_PIPE_BLOCKS
   const int pipe_blocks = getenv("MPGPU_HA_PIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_PIPE_BLOCKS")) : 256;
-  bool piped = false;
+  // the full-width shape pipelined the same way (ha_pipe_kernel<HW, NBG, false>: 6 four-wave blocks per scene)
+  // once its launch is resident at once (4 blocks per CU at HA_WPE_FULL = 4); (A/B) MPGPU_HA_FPIPE_BLOCKS, 0: off
+  const int fpipe_blocks = getenv("MPGPU_HA_FPIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_FPIPE_BLOCKS")) : 1024;
+  const int per_fpipe = 2 + (np + NBG - 1) / NBG;
+  int piped = 0;  // the format of the records the last launch left in E[it & 1]: 0 none, 1 full-width, 2 tail
   // (A/B) MPGPU_HA_PRESCAN=1: the prescan block's PRE_K least entries merged into popfirst!.  Measured slower
   // (r05j, lone 729-pop scenario: 26.6 vs 25.7 us per iteration): its PRE_K DPP rounds on 12 waves took ~6 us
   // and the merge's readlane chains ~2.6 us, so the bookkeeping started later than it saved.  Off by default
@@ -3912,10 +3951,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
     } else if (tail && tail_pipe && known * (2 + (np + NBG_TAIL - 1) / NBG_TAIL) <= pipe_blocks) {
       const int per_pipe = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
-      if (!piped) {  // the current nodes' expansion, for the first pipelined launch
+      if (piped != 2) {  // the current nodes' expansion, for the first pipelined launch
         hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL),
                            0, ctx->stream, D, Q, A, B, it, 1);
-        piped = true;
+        piped = 2;
       }
       if (known * per_pipe <= persist_cap) {  // the rest of the search in one cooperative launch
         unsigned char* rs_ok2 = reinterpret_cast<unsigned char*>(rs_i2);
@@ -3933,7 +3972,16 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       }
       hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), 0,
                          ctx->stream, D, Q, A, B, it, 0);
+    } else if (!tail && tail_pipe && known * per_fpipe <= fpipe_blocks) {
+      if (piped != 1) {
+        hipLaunchKernelGGL((ha_pipe_kernel<HW, NBG, false>), dim3((unsigned)(known * per_fpipe)), dim3(HT), 0,
+                           ctx->stream, D, Q, A, B, it, 1);
+        piped = 1;
+      }
+      hipLaunchKernelGGL((ha_pipe_kernel<HW, NBG, false>), dim3((unsigned)(known * per_fpipe)), dim3(HT), 0,
+                         ctx->stream, D, Q, A, B, it, 0);
     } else if (tail) {
+      piped = 0;
       if (tail_rsh)  // + the prescan block per scene
         hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL, true>), dim3((unsigned)(known * (per_tail + 1))),
                            dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
@@ -3941,9 +3989,11 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)),
                            dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
     } else if (known * per <= mid_blocks) {
+      piped = 0;
       hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG>), dim3((unsigned)(known * per)),
                          dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
     } else {
+      piped = 0;
       hipLaunchKernelGGL((ha_step_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0,
                          ctx->stream, D, Q, A, B, it);
     }
@@ -3969,6 +4019,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       }
     }
   }
+  // -1 past every scene's pops, filled while the search still runs on the device: the copy after it
+  // overwrites columns [0, max_loop) (the device's memset padded those)
+  std::fill(pop_seq, pop_seq + nB * mp, (int64_t)-1);
   if (A.stamps) {  // diagnostics: raw stamps to $MPGPU_HA_STAMPS_OUT (tools/ha_stamps.py reads them)
     std::vector<unsigned long long> h((size_t)HA_STAMP_N * stamp_slots * A.stamp_blocks);
     MP_HIP(ctx, hipMemcpyAsync(h.data(), A.stamps, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -4006,9 +4059,6 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     max_ns = std::max(max_ns, n_states[b]);
     max_rs = std::max(max_rs, rs_len[b]);
   }
-  // -1 past every scene's pops: the device copy below covers columns [0, max_loop) (its memset
-  // already padded them), the host fills the rest of each row
-  for (size_t b = 0; b < nB; b++) std::fill(pop_seq + b * mp + max_loop, pop_seq + (b + 1) * mp, (int64_t)-1);
   if (max_loop > 0)
     MP_HIP(ctx, hipMemcpy2DAsync(pop_seq, sizeof(int64_t) * mp, Q.pop_seq, sizeof(long long) * mp,
                                  sizeof(long long) * max_loop, nB, hipMemcpyDeviceToHost, ctx->stream));

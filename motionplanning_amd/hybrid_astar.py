@@ -10,6 +10,7 @@ Setup-time lattice arithmetic (regulate_states, Encode bounds) is exact IEEE
 (round-half-even, fmod), computed here.
 """
 import ctypes
+import itertools
 import math
 import time
 from dataclasses import dataclass, field
@@ -179,28 +180,40 @@ def plan_batch(searchers, ctx=None, max_pops=5000):
     B = len(searchers)
     start = f64([h.s.starting_states for h in searchers])
     goal = f64([h.s.ending_states for h in searchers])
-    walls = f64([h.s.obstacle_list for h in searchers]).reshape(B, p.n_walls, 5)
+    if any(len(h.s.obstacle_list) != p.n_walls for h in searchers):
+        raise ValueError("plan_batch: every scene needs the same number of walls")
+    walls = np.fromiter(itertools.chain.from_iterable(itertools.chain.from_iterable(h.s.obstacle_list for h in searchers)),
+                        np.float64, B * p.n_walls * 5).reshape(B, p.n_walls, 5)
     found = np.zeros(B, np.int32)
     pops = np.zeros(B, np.int32)
     n_nodes = np.zeros(B, np.int32)
-    pop_seq = np.empty((B, max_pops), np.int64)  # the library writes every entry (-1 past the pops)
     n_states = np.zeros(B, np.int32)
-    states = np.empty((B, max_pops, 3))  # rows [0, n_states) written; nothing else is read
     rs_len = np.zeros(B, np.int32)
-    rs_path = np.zeros((B, 501, 3))
+    # the large outputs live in per-context buffers reused across calls (their pages stay mapped): the library
+    # writes every pop_seq entry (-1 past the pops), the first n_states rows of states and rs_len rows of rs_path
+    key = (B, max_pops)
+    bufs = getattr(ctx, "_ha_plan_bufs", None)
+    if bufs is None or bufs[0] != key:
+        bufs = (key, np.empty((B, max_pops), np.int64), np.empty((B, max_pops, 3)), np.zeros((B, 501, 3)))
+        ctx._ha_plan_bufs = bufs
+    _, pop_seq, states, rs_path = bufs
     t0 = time.time()
     ctx.check(ctx.lib.mp_ha_plan(ctx.handle, ctypes.byref(p), B, ptr(start), ptr(goal), ptr(walls), ptr(found),
                                  ptr(pops), ptr(n_nodes), ptr(pop_seq), ptr(n_states), ptr(states), ptr(rs_len),
                                  ptr(rs_path)))
     dt = time.time() - t0
+    # one compact copy per output, each scene's result a view of it (nothing aliases the reused buffers)
+    ps = pop_seq[:, : max(int(pops.max()), 0)].copy()
+    sts = states[:, : max(int(n_states.max()), 0)].copy()
+    rsp = rs_path[:, : max(int(rs_len.max()), 0)].copy()
     for b, h in enumerate(searchers):
         r = h.r
         r.found = bool(found[b])
         r.loop_count = int(pops[b])
         r.n_nodes = int(n_nodes[b])
-        r.pop_sequence = pop_seq[b, : pops[b]].copy()
-        r.hybrid_astar_states = states[b, : n_states[b]].T.copy()
-        r.RSpath_final = rs_path[b, : rs_len[b]].T.copy()
+        r.pop_sequence = ps[b, : pops[b]]
+        r.hybrid_astar_states = sts[b, : n_states[b]].T
+        r.RSpath_final = rsp[b, : rs_len[b]].T
         r.planning_time = dt
     return searchers
 

@@ -22,6 +22,8 @@ for rep in range(5):
     pops = [h.r.loop_count for h in hs]
     print(f"plan 256: {el * 1e3:.1f} ms (library call {hs[0].r.planning_time * 1e3:.1f} ms), pops {sum(pops)}, "
           f"max pops {max(pops)}, found {sum(h.r.found for h in hs)}", flush=True)
+print("scenes still searching after iteration k: " + " ".join(
+    f"{k}:{sum(p > k for p in pops)}" for k in (50, 100, 200, 300, 400, 500, 600, 700)), flush=True)
 if "--shards" in sys.argv:
     t_all = sorted(els)[len(els) // 2]
     for name, strided in (("contiguous", False), ("strided", True)):
