@@ -616,6 +616,8 @@ struct IterArgs {
   // with the node: the Dict pre-check then runs beside FindNewNode's writes (see ha_iter_body)
   const double* node_g;
   const int* node_nn;
+  int full_tuv;  // the full-width groups store their winners' (t, u, v) (hp_t chunk 0) and the books flag them
+  unsigned long long* mirror;  // (host-coherent) launch it's first block writes (it - 1) << 32 | live(it - 1)
   int no_tuv;  // (A/B, MPGPU_HA_TUV=0) nodes keep only their winner id: RS_connected evaluates its word
 };
 
@@ -669,6 +671,15 @@ __device__ __forceinline__ long long expand_nb(const HaDev& P, const IterArgs& A
   regulate(P, t, nb);
   if (sn) mpj_sincos_bl(nb[2], sn, cn);
   return encode(P, nb);
+}
+
+// The live count of the previous iteration (final: written by the previous launch) to the host, packed with
+// the iteration, by the launch's first thread (a vector store to fine-grained host memory); mp_ha_plan sizes
+// its next launches from it instead of a stream copy every 16 iterations.
+__device__ __forceinline__ void ha_mirror(const IterArgs& A, int it) {
+  if (A.mirror && A.n_live && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(A.mirror, ((unsigned long long)(it - 1) << 32) | (unsigned)*A.n_live, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Bounded cross-block wait (ha_pipe_kernel, ha_persist_kernel): poll *p until it is >= v; past HA_SPIN_MAX
@@ -732,6 +743,11 @@ static_assert(12 % HW == 0, "HA_WAVES must divide the 12 Reeds-Shepp words");
 #define HA_NBG_TAIL 4
 #endif
 constexpr int HW_TAIL = 12, NBG_TAIL = HA_NBG_TAIL;
+// (A/B, MPGPU_HA_MID_BLOCKS > 0) the middle shape's waves per block: 16 neighbours each, 12 / HA_MID_HW
+// Reeds-Shepp words per wave
+#ifndef HA_MID_HW
+#define HA_MID_HW 6
+#endif
 // (A/B) -DHA_TAIL_OVERLAP=1: the tail shape's neighbour groups evaluate rs_heuristic for all their
 // neighbours, overlapped with the sweep, instead of sweeping first and evaluating it only when a neighbour
 // needs it (as the full-width shape does).  Measured slower (r05e, lone 729-pop scenario: 29.1 vs 28.3 us
@@ -740,6 +756,11 @@ constexpr int HW_TAIL = 12, NBG_TAIL = HA_NBG_TAIL;
 // the groups that need it.
 #ifndef HA_TAIL_RSH
 #define HA_TAIL_RSH 1
+#endif
+// (A/B build, -DHA_FULL_TUV_CODE=1 + MPGPU_HA_FULL_TUV=1) the full-width groups' winners' (t, u, v) carried
+// through the full-width bookkeeping too (see the host's ftuv_env)
+#ifndef HA_FULL_TUV_CODE
+#define HA_FULL_TUV_CODE 0
 #endif
 #ifndef HA_TAIL_OVERLAP
 #define HA_TAIL_OVERLAP 0
@@ -754,9 +775,12 @@ struct NoMid {
 };
 // mid(): work the block does between its word loop and the cross-wave reduction (the tail shape's collision
 // sweep), so the waves' Reeds-Shepp chains and that work overlap on the SIMDs instead of following each other
-template <bool CMD, int HWt, class Mid = NoMid>
+// TUV (the full-width groups): every lane also keeps its best word's (t, u, v) through the word loop and the
+// variant reduction, into tv_out; the lanes of wave (id / 4) / WPW then hold the block winner's
+template <bool CMD, int HWt, class Mid = NoMid, bool TUV = false>
 __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* best_id, double* sh_c, int* sh_i,
-                                                double* cmd_out = nullptr, const Mid& mid = Mid()) {
+                                                double* cmd_out = nullptr, const Mid& mid = Mid(),
+                                                double* tv_out = nullptr) {
   constexpr int WPW = 12 / HWt;  // Reeds–Shepp words per wave
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, var = lane & 3;
   double q[3];
@@ -770,21 +794,39 @@ __device__ __forceinline__ double rs_best_split(const double* s, int tid, int* b
   // register peak, so the winning word is evaluated again below
   constexpr bool KEEP = CMD && WPW == 1;
   Cmd cb;
+  double tb[3] = {0.0, 0.0, 0.0};
 #pragma unroll 1
   for (int w = WPW * wave + 1; w <= WPW * wave + WPW; w++) {
-    const double cost = rs_word(w, R, KEEP ? &cb : nullptr);
+    double tw[3];
+    const double cost = rs_word(w, R, KEEP ? &cb : nullptr, TUV ? tw : nullptr);
     const int id = 4 * (w - 1) + var;
     if (rs_before(cost, id, bc, bi)) {
       bc = cost;
       bi = id;
+      if (TUV)
+#pragma unroll
+        for (int e = 0; e < 3; e++) tb[e] = tw[e];
     }
   }
 #pragma unroll
   for (int o = 2; o >= 1; o >>= 1) {
     const double ov = __shfl_xor(bc, o);
     const int oi = __shfl_xor(bi, o);
-    if (rs_before(ov, oi, bc, bi)) { bc = ov; bi = oi; }
+    double ot[3];
+    if (TUV)
+#pragma unroll
+      for (int e = 0; e < 3; e++) ot[e] = __shfl_xor(tb[e], o);
+    if (rs_before(ov, oi, bc, bi)) {
+      bc = ov;
+      bi = oi;
+      if (TUV)
+#pragma unroll
+        for (int e = 0; e < 3; e++) tb[e] = ot[e];
+    }
   }
+  if (TUV)
+#pragma unroll
+    for (int e = 0; e < 3; e++) tv_out[e] = tb[e];
   HTIME(13);
   sh_c[tid] = bc;
   sh_i[tid] = bi;
@@ -1266,7 +1308,16 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       const int jj = j < nk ? j : 0;
       change_basis_sc(g_nb[jj], goal, P.minR, g_sc[jj][0], g_sc[jj][1], ns);
       HTIME(2);
-      cb = rs_best_split<false, HWt>(ns, tid, &best, red_c, red_i);
+      if (HA_FULL_TUV_CODE && A.full_tuv && A.hp_t) {  // (t, u, v) of each neighbour's winner, for RS_connected
+        double tv[3];
+        cb = rs_best_split<false, HWt, NoMid, true>(ns, tid, &best, red_c, red_i, nullptr, NoMid(), tv);
+        if ((lane & 3) == 0 && j < nk && (tid >> 6) == (best / 4) / (12 / HWt))
+#pragma unroll
+          for (int e = 0; e < 3; e++)
+            st_out(A.coherent, A.hp_t + ((size_t)s * P.n_prim + k0 + j) * 12 + e, tv[e]);
+      } else {
+        cb = rs_best_split<false, HWt>(ns, tid, &best, red_c, red_i);
+      }
       HSTAMP(15);
       HTIME(3);
     }
@@ -2078,6 +2129,11 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
     } else {
       hk = ld_ag(A.h + q);
       if (A.hw) hwk = ld_ag(A.hw + q);
+      if (A.full_tuv && hwk >= 0) {  // (the groups stored the winner's (t, u, v))
+        hwk |= RW_TUV | (hk < __builtin_inf() ? RW_OK : 0);
+#pragma unroll
+        for (int e = 0; e < 3; e++) tuvk[e] = ld_ag(A.hp_t + q * 12 + e);
+      }
     }
     nb0 = ld_ag(A.nb + 3 * q);
     nb1 = ld_ag(A.nb + 3 * q + 1);
@@ -2135,7 +2191,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
       io = Q.index[base + hit];
       drw = Q.rw[base + hit];
 #pragma unroll
-      for (int e = 0; e < 3; e++) dtuv[e] = RSH ? Q.tuv[(base + hit) * 3 + e] : 0.0;
+      for (int e = 0; e < 3; e++) dtuv[e] = (RSH || HA_FULL_TUV_CODE) ? Q.tuv[(base + hit) * 3 + e] : 0.0;
       dst0 = Q.st[(base + hit) * 3];
       dst1 = Q.st[(base + hit) * 3 + 1];
       dst2 = Q.st[(base + hit) * 3 + 2];
@@ -2211,7 +2267,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
         Q.st[q * 3 + 2] = nst2;
         Q.index[q] = ix;
         Q.rw[q] = nrw;
-        if (RSH) {
+        if (RSH || HA_FULL_TUV_CODE) {
           Q.tuv[q * 3] = nt0;
           Q.tuv[q * 3 + 1] = nt1;
           Q.tuv[q * 3 + 2] = nt2;
@@ -2231,7 +2287,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
         Q.oid[base + p] = id;
         Q.oix[base + p] = nix;
         Q.orw[base + p] = nrw;
-        if (RSH) {
+        if (RSH || HA_FULL_TUV_CODE) {
           Q.otuv[(base + p) * 3] = nt0;
           Q.otuv[(base + p) * 3 + 1] = nt1;
           Q.otuv[(base + p) * 3 + 2] = nt2;
@@ -2405,7 +2461,8 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
     go = s_merged == 1;
     iw = s_iw;
   } else {
-    go = ha_pop<NT, RSH>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B,
+    // (HA_FULL_TUV_CODE: the commands travel with the entry in both shapes, a full-width winner's rw carries RW_TUV)
+    go = ha_pop<NT, RSH || HA_FULL_TUV_CODE>(Q, B, b, n_open, loop, tid, Q.node + (size_t)(it & 1) * 3 * B, Q.node_rw + (size_t)(it & 1) * B,
                     Q.node_tuv + (size_t)(it & 1) * 3 * B, false, &iw, stp);
   }
   BSTAMP(8);
@@ -2722,6 +2779,11 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
     } else {  // the full-width groups' own rs_heuristic and winner (as ha_book_spec<NT, false>)
       hk = ld_ag(E.h + q);
       if (E.hw) hwk = ld_ag(E.hw + q);
+      if (E.full_tuv && hwk >= 0) {
+        hwk |= RW_TUV | (hk < __builtin_inf() ? RW_OK : 0);
+#pragma unroll
+        for (int e = 0; e < 3; e++) tuvk[e] = ld_ag(E.hp_t + q * 12 + e);
+      }
     }
     nb0 = ld_ag(E.nb + 3 * q);
     nb1 = ld_ag(E.nb + 3 * q + 1);
@@ -3058,13 +3120,14 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
 #endif
 constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 17;  // [6..11]: bookkeeping phases; [12..16]: block body phases
 template <int HWt, int NBGt, bool RSH = false>
-__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == 4 ? HA_WPE_FULL : HA_WPE_TAIL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
+__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == HW_TAIL ? HA_WPE_TAIL : HA_WPE_FULL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
   __shared__ int role;
   unsigned long long* stp = nullptr;
   if (HA_STAMP_CODE && A.stamps && it % HA_STAMP_EVERY == 0 && it / HA_STAMP_EVERY < 40 && (int)blockIdx.x < A.stamp_blocks &&
       threadIdx.x == 0)
     stp = A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ha_mirror(A, it);
   const int per = 1 + (P.n_prim + NBGt - 1) / NBGt + (RSH ? 1 : 0);
   int slot = blockIdx.x / per, item = blockIdx.x % per;
   if (!RSH && A.rs_last) {  // the RS_connected blocks after every neighbour group in dispatch order
@@ -3165,6 +3228,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
       (int)blockIdx.x < A.stamp_blocks && threadIdx.x == 0)
     stp = A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
   if (stp) __hip_atomic_store(stp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!boot) ha_mirror(A, it);
   const int ng = (P.n_prim + NBGt - 1) / NBGt, per = 2 + ng;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
   const int n_live = A.n_live ? *A.n_live : A.n_active;
@@ -3905,8 +3969,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // whole launch is resident at once (one 12-wave block per CU); (A/B) MPGPU_HA_PIPE_BLOCKS
   const int pipe_blocks = getenv("MPGPU_HA_PIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_PIPE_BLOCKS")) : 256;
   // the full-width shape pipelined the same way (ha_pipe_kernel<HW, NBG, false>: 6 four-wave blocks per scene)
-  // once its launch is resident at once (4 blocks per CU at HA_WPE_FULL = 4); (A/B) MPGPU_HA_FPIPE_BLOCKS, 0: off
-  const int fpipe_blocks = getenv("MPGPU_HA_FPIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_FPIPE_BLOCKS")) : 1024;
+  // once its launch is resident at once (4 blocks per CU at HA_WPE_FULL = 4).  (A/B) MPGPU_HA_FPIPE_BLOCKS=1024;
+  // off by default: measured 0.4-0.9 ms slower per 256-plan (r05u/r05v), its bookkeeping publishes the pop
+  // ~10 us after its start, so pop + expansion is no shorter than expansion + the whole bookkeeping (~8 us)
+  const int fpipe_blocks = getenv("MPGPU_HA_FPIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_FPIPE_BLOCKS")) : 0;
   const int per_fpipe = 2 + (np + NBG - 1) / NBG;
   int piped = 0;  // the format of the records the last launch left in E[it & 1]: 0 none, 1 full-width, 2 tail
   // (A/B) MPGPU_HA_PRESCAN=1: the prescan block's PRE_K least entries merged into popfirst!.  Measured slower
@@ -3919,6 +3985,11 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool rs_last_env = !getenv("MPGPU_HA_RS_LAST") || atoi(getenv("MPGPU_HA_RS_LAST")) != 0;  // r05o: -0.2 ms
   A.rs_last = rs_last_env;
   A.no_tuv = !tuv_env;
+  // (A/B, MPGPU_HA_FULL_TUV=1) the full-width groups' winners' (t, u, v) too, so a node popped there also skips
+  // RS_connected's word evaluation (RS search phase 6-9 -> 1.2 us) -- neutral per plan (r05u: RS_connected is
+  // not the full-width chain) and 10 more spilled VGPRs, so off
+  static const bool ftuv_env = getenv("MPGPU_HA_FULL_TUV") && atoi(getenv("MPGPU_HA_FULL_TUV")) == 1;
+  A.full_tuv = HA_FULL_TUV_CODE && tuv_env && ftuv_env && !split;
   if (!A.hp_c || !A.hp_i || !A.hp_t) return MP_ERR_NOMEM;
   // iteration it >= 2 works on the compact list of scenes still live (written by the previous
   // bookkeeping launch, count on the device); the host sizes the grids by the last live count it has
@@ -3934,7 +4005,38 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   int known = B;
   int chunk = 0, checked = 0;
   bool finished = false;
+  // (A/B, MPGPU_HA_MIRROR=1) the live-count mirror (ha_mirror): the host stays at most MIRROR_AHEAD launches
+  // ahead of the device and sizes each launch from the count of the latest one started, instead of a stream
+  // copy of the count every CH iterations read up to two chunks late.  Measured 1.1-1.4 ms slower per 256-plan
+  // (r05u/r05v): each launch's system-scope store to host memory delays its end, and the prompter shape
+  // switches gain nothing
+  static const bool mirror_env = getenv("MPGPU_HA_MIRROR") && atoi(getenv("MPGPU_HA_MIRROR")) == 1;
+  static const int mirror_ahead = getenv("MPGPU_HA_MIRROR_AHEAD") ? std::max(2, atoi(getenv("MPGPU_HA_MIRROR_AHEAD"))) : 6;
+  volatile unsigned long long* hm = nullptr;
+  A.mirror = nullptr;
+  if (mirror_env && !split) {
+    unsigned long long* dm = nullptr;
+    hm = mp_mapped(ctx, &dm);
+    if (hm) {
+      *hm = 0;
+      A.mirror = dm;
+    }
+  }
   for (int it = 1; it <= mp && !finished; it++) {
+    if (hm && it > 1) {  // the latest count the device has published; wait while too far ahead of it
+      unsigned long long v = *hm;
+      long long spins = 0;
+      while ((int)(v >> 32) < it - mirror_ahead) {
+        // a stream that has gone idle without reaching the iteration: a launch failed -- stop waiting
+        if ((++spins & 1023) == 0 && hipStreamQuery(ctx->stream) != hipErrorNotReady) break;
+        v = *hm;
+      }
+      const int mit = (int)(v >> 32), ml = (int)(v & 0xffffffffu);
+      if (mit >= 1) {
+        if (ml == 0) break;  // every search has ended
+        known = std::min(known, ml);
+      }
+    }
     A.scene_of = it == 1 ? nullptr : Q.lst + ((it - 1) & 1) * B;
     A.n_live = it == 1 ? nullptr : Q.live + (it - 1);
     A.n_active = known;
@@ -3990,15 +4092,15 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                            dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
     } else if (known * per <= mid_blocks) {
       piped = 0;
-      hipLaunchKernelGGL((ha_step_kernel<HW_TAIL, NBG>), dim3((unsigned)(known * per)),
-                         dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it);
+      hipLaunchKernelGGL((ha_step_kernel<HA_MID_HW, NBG>), dim3((unsigned)(known * per)),
+                         dim3(64 * HA_MID_HW), 0, ctx->stream, D, Q, A, B, it);
     } else {
       piped = 0;
       hipLaunchKernelGGL((ha_step_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0,
                          ctx->stream, D, Q, A, B, it);
     }
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
-    if (it % CH == 0 || it == mp) {
+    if (!hm && (it % CH == 0 || it == mp)) {
       const int slot = chunk % NCK;
       if (hipMemcpyAsync(hl + slot, Q.live + it, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
           hipEventRecord(ev[slot], ctx->stream) != hipSuccess) {

@@ -95,6 +95,22 @@ void* mp_pinned(mp_ctx* ctx, size_t bytes) {
   return ctx->pinned;
 }
 
+unsigned long long* mp_mapped(mp_ctx* ctx, unsigned long long** dev) {
+  if (!ctx->mapped) {
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      hipHostFree(h);
+      return nullptr;
+    }
+    ctx->mapped = static_cast<unsigned long long*>(h);
+    ctx->mapped_dev = static_cast<unsigned long long*>(d);
+  }
+  *dev = ctx->mapped_dev;
+  return ctx->mapped;
+}
+
 void mp_sync_all(mp_ctx* ctx) {
   hipStreamSynchronize(ctx->stream);
   if (ctx->side) hipStreamSynchronize(ctx->side);
@@ -218,6 +234,7 @@ int mp_ctx_destroy(mp_ctx* ctx) {
   for (void* p : ctx->ws_ptr)
     if (p) hipFree(p);
   if (ctx->pinned) hipHostFree(ctx->pinned);
+  if (ctx->mapped) hipHostFree(ctx->mapped);
   if (ctx->tickets) hipFree(ctx->tickets);
   if (ctx->flags) hipFree(ctx->flags);
   for (hipEvent_t e : ctx->ev_pool) hipEventDestroy(e);

@@ -27,6 +27,9 @@ struct mp_ctx {
   // pinned host staging
   void* pinned = nullptr;
   size_t pinned_size = 0;
+  // a few words of fine-grained (coherent) host memory the device writes while a plan runs (mp_mapped)
+  unsigned long long* mapped = nullptr;
+  unsigned long long* mapped_dev = nullptr;
   // Hybrid A* primitive table (device)
   double* ha_states_candi = nullptr;
   double* ha_paths_candi = nullptr;
@@ -118,6 +121,8 @@ size_t mp_ws_size(mp_ctx* ctx, int slot);
 bool mp_ws_affordable(mp_ctx* ctx, int slot, size_t bytes, double frac);
 int mp_ticket_reserve(mp_ctx* ctx, int n);
 void* mp_pinned(mp_ctx* ctx, size_t bytes);
+// 8 words of coherent host memory (host pointer; *dev = the device's address of it), nullptr on failure
+unsigned long long* mp_mapped(mp_ctx* ctx, unsigned long long** dev);
 
 #define MP_HIP(ctx, call)                                                                \
   do {                                                                                   \
