@@ -743,8 +743,8 @@ static_assert(12 % HW == 0, "HA_WAVES must divide the 12 Reeds-Shepp words");
 #define HA_NBG_TAIL 4
 #endif
 constexpr int HW_TAIL = 12, NBG_TAIL = HA_NBG_TAIL;
-// (A/B, MPGPU_HA_MID_BLOCKS > 0) the middle shape's waves per block: 16 neighbours each, 12 / HA_MID_HW
-// Reeds-Shepp words per wave
+// the middle shape's waves per block (MPGPU_HA_MID_BLOCKS): 16 neighbours each, 12 / HA_MID_HW Reeds-Shepp
+// words per wave (12-wave blocks measured 38 ms per 256-plan at MID 1024, r05q; 6-wave ones 24.9, r05x)
 #ifndef HA_MID_HW
 #define HA_MID_HW 6
 #endif
@@ -3996,12 +3996,18 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // seen (an upper bound: it only decreases) and switches to the tail shape once that many scenes
   // fit in about two blocks per CU
 #ifndef HA_TAIL_BLOCKS
-#define HA_TAIL_BLOCKS 512
+#define HA_TAIL_BLOCKS 256
 #endif
-  // (A/B) MPGPU_HA_TAIL_BLOCKS overrides the tail threshold; MPGPU_HA_MID_BLOCKS > 0 adds a middle shape
-  // (12-wave blocks, 16 neighbours each: 5 blocks per scene) once known * 5 fits in that many blocks
+#ifndef HA_MID_BLOCKS
+#define HA_MID_BLOCKS 512
+#endif
+  // (A/B) MPGPU_HA_TAIL_BLOCKS overrides the tail threshold; MPGPU_HA_MID_BLOCKS the middle shape's
+  // (HA_MID_HW-wave blocks, 16 neighbours each: 5 blocks per scene, once known * 5 fits in that many blocks;
+  // 0: off).  r05x: the 6-wave middle shape for 16..102 live scenes and the tail from 15 (its pipelined /
+  // persistent forms from 14) -- 256-plan 25.6 -> 24.9 ms, the largest strided / contiguous shard 21.0 ->
+  // 19.2 / 17.9 -> 17.6 ms (the 12-wave tail step from 30 live scenes, round 4's threshold, and no middle)
   const int tail_blocks = getenv("MPGPU_HA_TAIL_BLOCKS") ? atoi(getenv("MPGPU_HA_TAIL_BLOCKS")) : HA_TAIL_BLOCKS;
-  const int mid_blocks = getenv("MPGPU_HA_MID_BLOCKS") ? atoi(getenv("MPGPU_HA_MID_BLOCKS")) : 0;
+  const int mid_blocks = getenv("MPGPU_HA_MID_BLOCKS") ? atoi(getenv("MPGPU_HA_MID_BLOCKS")) : HA_MID_BLOCKS;
   int known = B;
   int chunk = 0, checked = 0;
   bool finished = false;
