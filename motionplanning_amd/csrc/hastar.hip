@@ -4069,9 +4069,19 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         int* rs_len2 = rs_i2 + 2 * nB;
         int it0 = it;
         void* args[] = {&D, &Q, &A, (void*)&B, &it0, &rs_path2, &rs_ok2, &rs_len2};
-        if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
-                                       dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), args, 0,
-                                       ctx->stream) != hipSuccess) {
+        // (MPGPU_HA_COOP=0: an ordinary launch of the same grid, co-resident by the occupancy check alone --
+        // for rocprofv3 runs: the profiler's exit handlers crash in a process that made a cooperative launch)
+        static const bool coop_env = !getenv("MPGPU_HA_COOP") || atoi(getenv("MPGPU_HA_COOP")) != 0;
+        hipError_t le;
+        if (coop_env) {
+          le = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
+                                          dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), args, 0, ctx->stream);
+        } else {
+          hipLaunchKernelGGL((ha_persist_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)),
+                             dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it0, rs_path2, rs_ok2, rs_len2);
+          le = hipGetLastError();
+        }
+        if (le != hipSuccess) {
           cleanup();
           return mp_fail(ctx, MP_ERR_HIP, "ha_persist_kernel cooperative launch failed");
         }
