@@ -310,7 +310,9 @@ typedef struct mp_ha_params {
 
 /* neighbor_origin (hybrid_astar_utils.jl:483-503) computed by the library (FDLIBM sin/cos,
  * Euler Δt = 1e-2, n_col = floor(expand_time/Δt)), returned and installed in the context:
- * states_candi[n_gear*n_steer][3], paths_candi[n_gear*n_steer][n_col][3]. */
+ * states_candi[n_gear*n_steer][3], paths_candi[n_gear*n_steer][n_col][3] (either may be NULL: not
+ * returned).  A repeat call with the same settings as the installed table returns its copies without
+ * recomputing or re-uploading it (mp_ha_set_primitives clears that memo). */
 int mp_ha_neighbor_origin(mp_ctx* ctx, const mp_ha_params* p, int32_t n_steer, const double* steer_set,
                           int32_t n_gear, const double* gear_set, double* states_candi, double* paths_candi);
 

@@ -3544,6 +3544,7 @@ int mp_ha_set_primitives(mp_ctx* ctx, const mp_ha_params* p, const double* state
   if (st) return st;
   MP_CHECK(ctx, states_candi && paths_candi, "required pointer is NULL");
   MP_HIP(ctx, hipSetDevice(ctx->device));
+  ctx->ha_prim_key.clear();  // a caller-given table: mp_ha_neighbor_origin recomputes next time
   if (ctx->ha_states_candi) { hipFree(ctx->ha_states_candi); ctx->ha_states_candi = nullptr; }
   if (ctx->ha_paths_candi) { hipFree(ctx->ha_paths_candi); ctx->ha_paths_candi = nullptr; }
   MP_HIP(ctx, hipMalloc(&ctx->ha_states_candi, sizeof(double) * 3 * p->n_prim));
@@ -3568,6 +3569,18 @@ int mp_ha_neighbor_origin(mp_ctx* ctx, const mp_ha_params* p, int32_t n_steer, c
   const double dt = 1e-2;
   const int ncol = (int)std::floor(p->expand_time / dt);
   MP_CHECK(ctx, ncol == p->n_col, "n_col (%d) != floor(expand_time/0.01) (%d)", p->n_col, ncol);
+  // the same settings as the installed table: hand back its host copies (each plan_batch call lands here)
+  std::vector<double> key = {(double)n_steer, (double)n_gear, p->expand_time, (double)p->n_col, (double)p->n_prim};
+  key.insert(key.end(), steer_set, steer_set + n_steer);
+  key.insert(key.end(), gear_set, gear_set + n_gear);
+  if (!ctx->ha_prim_key.empty() && ctx->ha_prim_key.size() == key.size() &&
+      std::equal(key.begin(), key.end(), ctx->ha_prim_key.begin(),
+                 [](double a, double b) { return __builtin_memcmp(&a, &b, sizeof a) == 0; }) &&
+      ctx->ha_states_candi && ctx->ha_n_prim == p->n_prim && ctx->ha_n_col == p->n_col) {
+    if (states_candi) std::copy(ctx->ha_sc_host.begin(), ctx->ha_sc_host.end(), states_candi);
+    if (paths_candi) std::copy(ctx->ha_pc_host.begin(), ctx->ha_pc_host.end(), paths_candi);
+    return MP_OK;
+  }
   std::vector<double> sc(3 * (size_t)p->n_prim), pc(3 * (size_t)p->n_prim * ncol);
   // hybrid_astar_utils.jl:483-503 (FDLIBM sin/cos on the host: setup-time, 62 x 250 steps)
   for (int g = 0; g < n_gear; g++)
@@ -3586,7 +3599,13 @@ int mp_ha_neighbor_origin(mp_ctx* ctx, const mp_ha_params* p, int32_t n_steer, c
     }
   if (states_candi) std::copy(sc.begin(), sc.end(), states_candi);
   if (paths_candi) std::copy(pc.begin(), pc.end(), paths_candi);
-  return mp_ha_set_primitives(ctx, p, sc.data(), pc.data());
+  const int st = mp_ha_set_primitives(ctx, p, sc.data(), pc.data());  // (clears the key)
+  if (st == MP_OK) {
+    ctx->ha_prim_key = std::move(key);
+    ctx->ha_sc_host = std::move(sc);
+    ctx->ha_pc_host = std::move(pc);
+  }
+  return st;
 }
 
 int mp_ha_expand(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* node, const double* goal,

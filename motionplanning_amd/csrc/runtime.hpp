@@ -35,6 +35,9 @@ struct mp_ctx {
   double* ha_paths_candi = nullptr;
   int ha_n_prim = 0, ha_n_col = 0;
   double ha_prim_ext = 0;  // max |x|, |y| of the installed primitive poses (the SAT culls' coordinate guard)
+  // mp_ha_neighbor_origin's inputs for the installed table (empty: installed by mp_ha_set_primitives) and
+  // its host copies, so a repeat call with the same settings neither recomputes nor re-uploads
+  std::vector<double> ha_prim_key, ha_sc_host, ha_pc_host;
   // per-scene arrival counters for the MPPI last-block combine (zero at rest)
   unsigned int* tickets = nullptr;
   int n_tickets = 0;

@@ -176,7 +176,9 @@ def plan_batch(searchers, ctx=None, max_pops=5000):
     ctx = ctx or default_context()
     h0 = searchers[0]
     p = params_of(h0, max_pops)
-    install_primitives(h0, ctx)
+    # the primitive table (the library keeps it while the settings stay the same; no copies back)
+    ctx.check(ctx.lib.mp_ha_neighbor_origin(ctx.handle, ctypes.byref(params_of(h0)), h0.s.num_steer, ptr(h0.s.steer_set),
+                                            h0.s.num_gear, ptr(h0.s.gear_set), None, None))
     B = len(searchers)
     start = f64([h.s.starting_states for h in searchers])
     goal = f64([h.s.ending_states for h in searchers])
