@@ -30,7 +30,21 @@ struct IlqrDev {
   int N, variant, max_iter, max_ls;
   double dT, eps, alpha_floor, tol;
   int ls_cap;  // last trial index the halving loop can reach (max_ls - 1, or the alpha_floor stop)
+  // (mp_ilqr_solve, MPGPU_ILQR_MIRROR) the backward pass's first kernel reports the previous search's
+  // counts -- (seq << 32) | active, (seq << 32) | pending -- to host memory (ilqr_mirror)
+  unsigned long long* mirror;
+  int mirror_seq;
 };
+
+// the first thread of a backward pass's first kernel: n_dev = the list count the previous iteration's search
+// wrote (final: that launch is complete), n_dev[-1] its pending count; vector stores to fine-grained host memory
+__device__ __forceinline__ void ilqr_mirror(const IlqrDev& P, const int* n_dev) {
+  if (P.mirror && n_dev && blockIdx.x == 0 && threadIdx.x == 0) {
+    const unsigned long long q = (unsigned long long)(unsigned)P.mirror_seq << 32;
+    __hip_atomic_store(P.mirror + 1, q | (unsigned)n_dev[-1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(P.mirror, q | (unsigned)n_dev[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 
 // ILQR.jl:76-83 break tests after trial m (alpha is then 2^-(m+1)): the floor test first
 // (Parking_ILQR), then the max_ls safety cap.
@@ -466,6 +480,7 @@ __device__ __forceinline__ void knot_cost_derivs(const IlqrDev& P, const double*
 // (the grid is sized for nmax >= n by a host that has not waited for the count), else n = nmax.
 __global__ __launch_bounds__(256) void ilqr_deriv_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                          const int* list, const int* n_dev, int nmax, double* D) {
+  ilqr_mirror(P, n_dev);
   const int n = n_dev ? *n_dev : nmax;
   const long long Bn = (long long)n * (P.N - 1);
   if ((long long)blockIdx.x * blockDim.x >= Bn) return;  // block-uniform: past the live records
@@ -538,6 +553,7 @@ __device__ __forceinline__ void knot_derivs_part(const IlqrDev& P, const double*
 // leaves most of the chip idle.
 __global__ __launch_bounds__(256) void ilqr_deriv4_kernel(IlqrDev P, int B, const double* X, const double* U,
                                                           const int* list, const int* n_dev, int nmax, double* D) {
+  ilqr_mirror(P, n_dev);
   const int n = n_dev ? *n_dev : nmax;
   const long long Bn = (long long)n * (P.N - 1);
   if ((long long)blockIdx.x * 64 >= Bn) return;  // block-uniform: past the live records
@@ -1347,6 +1363,7 @@ struct QuadFetchRing {
 __global__ __launch_bounds__(64 * (1 + kFusedDW)) void ilqr_backward_fused_kernel(
     IlqrDev P, int B, const double* X, const double* U, const int* list, const int* n_dev, int nmax, double* kout,
     double* Kout) {
+  ilqr_mirror(P, n_dev);
   extern __shared__ double ring[];  // [RG][GK][ND][IPB]
   __shared__ int ready[kFusedRG];
   __shared__ int consumed;
@@ -2079,8 +2096,11 @@ __global__ __launch_bounds__(64) void ilqr_search_finish_kernel(IlqrDev P, int B
                                                                 const double* Xs2, const double* Us2, const double* Jt,
                                                                 int* winm, double* Jcur, int* active, int* iters,
                                                                 int* flags, int* n_active, int first, size_t T2,
-                                                                int reset = 0) {
+                                                                int reset = 0, int* zero_next = nullptr) {
   const size_t b = blockIdx.x;
+  // the counts (pending, active) of the next iteration's list buffer, instead of a memset launch: that
+  // buffer's list was read by this iteration's backward pass and its counts by the last host poll
+  if (zero_next && b == 0 && threadIdx.x < 2) zero_next[threadIdx.x] = 0;
   if (pending[b]) {
     const size_t N = P.N;
     const int mw = winm[b];
@@ -2167,6 +2187,8 @@ int make_ilqr(mp_ctx* ctx, const mp_ilqr_params* p, int B, IlqrDev* D) {
   D->max_iter = p->max_iter > 0 ? p->max_iter : 1000;
   D->max_ls = p->max_ls > 0 ? p->max_ls : 200;
   D->ls_cap = D->max_ls - 1;
+  D->mirror = nullptr;
+  D->mirror_seq = 0;
   for (int m = 0; m < D->max_ls - 1; m++)
     if (floor_stop(*D, m)) {
       D->ls_cap = m;
@@ -2370,13 +2392,17 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   double* dXn = (double*)mp_ws(ctx, WS_IO4, sizeof(double) * 4 * N * B * G);
   double* dUn = (double*)mp_ws(ctx, WS_IO5, sizeof(double) * 2 * N * B * G);
   double* dJ = (double*)mp_ws(ctx, WS_IO6, sizeof(double) * B);
-  int* dint = (int*)mp_ws(ctx, WS_IO7, sizeof(int) * (4 * (size_t)B + 2));
+  int* dint = (int*)mp_ws(ctx, WS_IO7, sizeof(int) * (5 * (size_t)B + 4));
   if (st || !dk || !dK || !dXn || !dUn || !dJ || !dint) return st ? st : MP_ERR_NOMEM;
   int* dact = dint;
   int* dit = dint + B;
   int* dfl = dint + 2 * B;
-  int* dnp = dint + 3 * B;   // instances the last pipelined round 0 left pending (host poll, with dn[0])
-  int* dn = dnp + 1;         // [0] active count, [1..B] their compact list (search_accept)
+  // two list buffers, [0] instances the pipelined round 0 left pending, [1] active count, [2 ..] their compact
+  // list (search_accept): iteration q's backward pass reads par[(q + 1) & 1], its search writes par[q & 1],
+  // whose counts the finish kernel of iteration q - 1 zeroed (a memset only after a path without one)
+  int* par[2] = {dint + 3 * (size_t)B, dint + 3 * (size_t)B + (2 + (size_t)B)};
+  int* dnp = par[0];
+  int* dn = dnp + 1;
   // trials G..ls_cap in one pass for the instances still searching after round 0 (G = kSearchG only),
   // while their slots fit in 8 GiB, in half of the free device memory and in the context's
   // workspace cap.  Otherwise -- or when allocating them fails -- the G-wide kernel runs its
@@ -2402,7 +2428,9 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     }
   }
   const dim3 g1((B + 63) / 64), b1(64);
-  hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl, dn + 1);
+  MP_HIP(ctx, hipMemsetAsync(par[0], 0, 2 * sizeof(int), ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(par[1], 0, 2 * sizeof(int), ctx->stream));
+  hipLaunchKernelGGL(ilqr_init_kernel, g1, b1, 0, ctx->stream, D, B, dX, dU, dJ, dact, dit, dfl, par[1] + 2);
   MP_HIP(ctx, hipGetLastError());
   int* hn = (int*)mp_pinned(ctx, 4 * sizeof(int));
   if (!hn) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
@@ -2422,10 +2450,35 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   int n_act = B;  // upper bound on the active count of the iteration being enqueued
   // hn[2q] = instances left pending by the pipelined round 0 (their rest pass runs in the next
   // launch, then they rejoin the list), hn[2q + 1] = the list count: their sum bounds the next list
+  // the counts come from host memory the next backward pass's first kernel writes (ilqr_mirror) instead of a
+  // stream copy + event per iteration: 0.3-0.5 ms per 4096-instance solve (r05zd); (A/B) MPGPU_ILQR_MIRROR=0
+  static const bool imirror_env = !getenv("MPGPU_ILQR_MIRROR") || atoi(getenv("MPGPU_ILQR_MIRROR")) != 0;
+  volatile unsigned long long* hmr = nullptr;
+  unsigned long long* dmr = nullptr;
+  if (imirror_env) {
+    hmr = mp_mapped(ctx, &dmr);
+    if (hmr) hmr[0] = hmr[1] = 0;
+  }
   auto poll = [&](int outer, bool* stop) -> int {
+    *stop = false;
+    if (hmr) {  // the counts of iteration outer - 1's search, reported by this iteration's backward pass
+      if (outer == 0) return MP_OK;
+      const unsigned long long want = (unsigned long long)(unsigned)(outer - 1 + 1);  // seq = iteration + 1
+      unsigned long long a = hmr[0], pd = hmr[1];  // (each word carries its seq: no order between them)
+      long long spins = 0;
+      while ((a >> 32) < want || (pd >> 32) < want) {
+        if ((++spins & 1023) == 0 && hipStreamQuery(ctx->stream) != hipErrorNotReady)
+          return mp_fail(ctx, MP_ERR_HIP, "iLQR count mirror never arrived");
+        a = hmr[0];
+        pd = hmr[1];
+      }
+      const int nprev = (int)(a & 0xffffffffu) + (int)(pd & 0xffffffffu);
+      if (nprev == 0) *stop = true;
+      else n_act = nprev;
+      return MP_OK;
+    }
     MP_HIP(ctx, hipMemcpyAsync(hn + 2 * (outer & 1), dnp, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     MP_HIP(ctx, hipEventRecord(evp.e[outer & 1], ctx->stream));
-    *stop = false;
     if (outer == 0) return MP_OK;
     MP_HIP(ctx, hipEventSynchronize(evp.e[(outer - 1) & 1]));
     const int nprev = hn[2 * ((outer - 1) & 1)] + hn[2 * ((outer - 1) & 1) + 1];
@@ -2444,10 +2497,23 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   bool onepass_armed = false;  // winm of the one-pass search set (then reset by its finish kernels)
   // (an instance in a rest pass sits one launch out, so the pipelined loop may take more launches
   // than max_iter + 2; each instance still stops at its own max_iter)
+  bool w_zeroed = true;  // this iteration's list buffer's counts are zero (initially: the memsets above)
+  // (A/B) MPGPU_ILQR_MEMSET=1: a memset launch per iteration instead of the finish kernel's zeroing
+  static const bool memset_env = getenv("MPGPU_ILQR_MEMSET") && atoi(getenv("MPGPU_ILQR_MEMSET")) == 1;
   for (int outer = 0; outer <= 2 * (D.max_iter + 2); outer++) {
-    // the derivative and sweep launches cover the active instances only (compact list dn[1..])
-    if ((st = run_backward(ctx, D, B, dX, dU, dn + 1, dn, n_act, dk, dK))) return st;
-    MP_HIP(ctx, hipMemsetAsync(dnp, 0, 2 * sizeof(int), ctx->stream));
+    int* rd = par[(outer + 1) & 1];  // the list the previous iteration wrote (or the init kernel)
+    dnp = par[outer & 1];
+    dn = dnp + 1;
+    int* zn = memset_env ? nullptr : rd;  // zeroed by this iteration's finish kernel, for the next iteration
+    // the derivative and sweep launches cover the active instances only (compact list)
+    IlqrDev Dm = D;  // (the mirror: the previous iteration's counts, seq = outer; 0 = none yet)
+    if (hmr && outer > 0) {
+      Dm.mirror = dmr;
+      Dm.mirror_seq = outer;
+    }
+    if ((st = run_backward(ctx, Dm, B, dX, dU, rd + 2, rd + 1, n_act, dk, dK))) return st;
+    if (!w_zeroed) MP_HIP(ctx, hipMemsetAsync(dnp, 0, 2 * sizeof(int), ctx->stream));
+    w_zeroed = false;
     mp_time_begin(ctx);
     // The switch to the one-pass search is terminal (once armed it stays, whatever later polls
     // say).  Instances the last pipelined launch left pending keep their active flag and their
@@ -2462,8 +2528,9 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
                          B, dX, dU, dk, dK, dJ, dact, ms1, dXs2, dUs2, dJt, winm1, 0, T2);
       MP_HIP(ctx, hipGetLastError());
       hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dact,
-                         ms1, dXs2, dUs2, dJt, winm1, dJ, dact, dit, dfl, dn, 0, T2, 2);
+                         ms1, dXs2, dUs2, dJt, winm1, dJ, dact, dit, dfl, dn, 0, T2, 2, zn);
       MP_HIP(ctx, hipGetLastError());
+      w_zeroed = zn != nullptr;
       mp_time_end(ctx);
       bool stop;
       if ((st = poll(outer, &stop))) return st;
@@ -2488,8 +2555,9 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
                          pend_o, ms_o, dXs2, dUs2, dJt, winm_o, T2, (int)gs.x);
       MP_HIP(ctx, hipGetLastError());
       hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, pend_o,
-                         ms_o, dXs2, dUs2, dJt, winm_o, dJ, dact, dit, dfl, dn, kSearchG, T2, 3);
+                         ms_o, dXs2, dUs2, dJt, winm_o, dJ, dact, dit, dfl, dn, kSearchG, T2, 3, zn);
       MP_HIP(ctx, hipGetLastError());
+      w_zeroed = zn != nullptr;
       mp_time_end(ctx);
       bool stop;
       if ((st = poll(outer, &stop))) return st;
@@ -2516,8 +2584,9 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
                          T2);
       MP_HIP(ctx, hipGetLastError());
       hipLaunchKernelGGL(ilqr_search_finish_kernel<kSearchG>, dim3((unsigned)B), b1, 0, ctx->stream, D, B, dX, dU, dpw, dpw + 2 * B,
-                         dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, kSearchG, T2);
+                         dXs2, dUs2, dJt, dpw + B, dJ, dact, dit, dfl, dn, kSearchG, T2, 0, zn);
       MP_HIP(ctx, hipGetLastError());
+      w_zeroed = zn != nullptr;
     }
     mp_time_end(ctx);
     bool stop;

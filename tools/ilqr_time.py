@@ -61,6 +61,8 @@ with torch.cuda.stream(stream):
             ctx.synchronize()
             ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
             print(f"forward {label}: {ms.value / reps:.3f} ms kernel", flush=True)
-t0 = time.perf_counter()
-Xs, Us, Js, it, ok = ilqr.ilqr_solve(ilqr.params(N=N, max_iter=60), X, U, ctx=ctx)
-print(f"solve: {(time.perf_counter() - t0) * 1e3:.1f} ms, iterations max {it.max()} mean {it.mean():.1f}, ok {ok}")
+for rep in range(int(sys.argv[sys.argv.index("--solve-reps") + 1]) if "--solve-reps" in sys.argv else 1):  # (the first includes workspace allocation)
+    t0 = time.perf_counter()
+    Xs, Us, Js, it, ok = ilqr.ilqr_solve(ilqr.params(N=N, max_iter=60), X, U, ctx=ctx)
+    print(f"solve: {(time.perf_counter() - t0) * 1e3:.1f} ms, iterations max {it.max()} mean {it.mean():.1f}, ok {ok}",
+          flush=True)
