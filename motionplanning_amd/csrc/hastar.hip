@@ -618,6 +618,16 @@ struct IterArgs {
   const int* node_nn;
   int full_tuv;  // the full-width groups store their winners' (t, u, v) (hp_t chunk 0) and the books flag them
   unsigned long long* mirror;  // (host-coherent) launch it's first block writes (it - 1) << 32 | live(it - 1)
+  // [B][n_prim][HA_DREC] (full-width / middle step launches) each neighbour's Dict entry as the group found it:
+  // cell's node id, then its g, pos, f, seq, Encode index, rs winner, state -- the bookkeeping reads them with
+  // the other records instead of looking them up after them
+  long long* drec;
+  const int* dpos;
+  const double* df;
+  const long long* dseq;
+  const long long* dindex;
+  const int* drw;
+  const double* dst;
   int no_tuv;  // (A/B, MPGPU_HA_TUV=0) nodes keep only their winner id: RS_connected evaluates its word
 };
 
@@ -681,6 +691,8 @@ __device__ __forceinline__ void ha_mirror(const IterArgs& A, int it) {
     __hip_atomic_store(A.mirror, ((unsigned long long)(it - 1) << 32) | (unsigned)*A.n_live, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+constexpr int HA_DREC = 10;
 
 // Bounded cross-block wait (ha_pipe_kernel, ha_persist_kernel): poll *p until it is >= v; past HA_SPIN_MAX
 // polls (~1 s) set *err and return HA_DONE (every waiter then leaves its loop: a wrong result, not a hang)
@@ -1288,7 +1300,30 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     double gd = 0.0;
     if (hit >= 0) gd = A.dg[(size_t)s * A.C + hit];  // loaded now, used after the sweep (a node newer than
     // the pipelined launch's nn_lim below may be half-written: its g is loaded but never used)
+    // (step launches) the rest of the neighbour's Dict entry for the bookkeeping, loaded beside gd and stored
+    // after the sweep (the Dict is the one this iteration's FindNewNode starts from: it runs after every group)
+    const bool drec = A.drec && A.dnid && !A.node_ag && tid < nk;
+    long long dv[HA_DREC - 2];
+    if (drec && hit >= 0) {
+      const size_t q = (size_t)s * A.C + hit;
+      dv[0] = A.dpos[q];
+      dv[1] = __double_as_longlong(A.df[q]);
+      dv[2] = A.dseq[q];
+      dv[3] = A.dindex[q];
+      dv[4] = A.drw[q];
+#pragma unroll
+      for (int e = 0; e < 3; e++) dv[5 + e] = __double_as_longlong(A.dst[q * 3 + e]);
+    }
     sweep(P.n_col > 5 ? (P.n_col - 1) / 5 + 1 : 1);
+    if (drec) {
+      long long* o = A.drec + ((size_t)s * P.n_prim + k0 + tid) * HA_DREC;
+      st_out(A.coherent, o, (long long)hit);
+      if (hit >= 0) {
+        st_out(A.coherent, o + 1, __double_as_longlong(gd));
+#pragma unroll
+        for (int e = 0; e < HA_DREC - 2; e++) st_out(A.coherent, o + 2 + e, dv[e]);
+      }
+    }
     HTIME(4);
     HSTAMP(13);
     // (full-width ha_pipe_kernel) this iteration's FindNewNode writes the Dict meanwhile: only nodes older than
@@ -2181,7 +2216,24 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   int po = 0, drw = -1;
   double dtuv[3] = {0.0, 0.0, 0.0};
   long long so0 = 0, io = 0;
-  if (valid) {
+  if (valid && !RSH && A.drec && A.dnid) {  // the groups' copies of the Dict entries (one round trip)
+    const long long* r = A.drec + ((size_t)b * np + tid) * HA_DREC;
+    long long w[HA_DREC];
+#pragma unroll
+    for (int e = 0; e < HA_DREC; e++) w[e] = ld_ag(r + e);
+    hit = (int)w[0];
+    if (hit >= 0) {
+      gd = __longlong_as_double(w[1]);
+      po = (int)w[2];
+      fo_ = __longlong_as_double(w[3]);
+      so0 = w[4];
+      io = w[5];
+      drw = (int)w[6];
+      dst0 = __longlong_as_double(w[7]);
+      dst1 = __longlong_as_double(w[8]);
+      dst2 = __longlong_as_double(w[9]);
+    }
+  } else if (valid) {
     hit = (ix >= 0 && ix < Q.C) ? Q.nid[base + ix] : -1;
     if (hit >= 0) {
       gd = Q.g[base + hit];
@@ -2708,9 +2760,11 @@ __device__ __forceinline__ IterArgs e_par(const IterArgs& A, int B, int np, int 
   return E;
 }
 
-template <int NT, bool RSH = true>
+// pre_wait (ha_persist_kernel): the wait for this iteration's expansion records, run after the open list's loads
+// are issued (the list stands as the previous iteration's bookkeeping left it) so they land meanwhile
+template <int NT, bool RSH = true, class Wait = NoMid>
 __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& Q, const IterArgs& E, int B, int it,
-                                                int b, unsigned long long* stp = nullptr) {
+                                                int b, unsigned long long* stp = nullptr, const Wait& pre_wait = Wait()) {
 #define PSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
   constexpr int SC = 4;  // open entries per thread held in registers (more are re-read)
   __shared__ int s_nopen, s_nnew, s_nchg, s_go;
@@ -2743,6 +2797,7 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
     fv[u] = p < Q.C ? Q.of[base + p] : 0.0;
     sv[u] = p < Q.C ? Q.oseq[base + p] : 0;
   }
+  pre_wait();
   // n_it's neighbour records (expanded by the previous launch)
   long long ix = 0;
   int frk = 0, hwk = -1;
@@ -3365,11 +3420,20 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE
   }
   // item 1: the bookkeeping of iteration it, it = it0, it0 + 1, ...
   for (int it = it0;; it++) {
-    if (it > it0) {  // E[it & 1]: every group of iteration it - 1 has expanded n_it
-      if (threadIdx.x == 0) wait_ge(Q.ex + s, ng * (it - it0), Q.err);
-      __syncthreads();
-    }
-    const BookRec br = ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s);
+    // E[it & 1]: every group of iteration it - 1 has expanded n_it (waited for inside, the open list's loads
+    // in flight)
+    const auto wait_exp = [&] {
+      if (it > it0) {
+        if (threadIdx.x == 0) wait_ge(Q.ex + s, ng * (it - it0), Q.err);
+        __syncthreads();
+      }
+    };
+#ifndef HA_PREWAIT
+#define HA_PREWAIT 1
+#endif
+    if (!HA_PREWAIT) wait_exp();  // (A/B build -DHA_PREWAIT=0: the wait before the bookkeeping's first load)
+    const BookRec br = HA_PREWAIT ? ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, nullptr, wait_exp)
+                                  : ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s);
     IterArgs F = A;
     rs_par(F, it);
     if (threadIdx.x == 0) {
@@ -3902,6 +3966,15 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool noskip = getenv("MPGPU_HA_NOSKIP") && atoi(getenv("MPGPU_HA_NOSKIP")) == 1;
   A.dnid = noskip ? nullptr : Q.nid;
   A.dg = Q.g;
+  // (A/B) MPGPU_HA_DREC=0: the bookkeeping looks the Dict entries up itself
+  static const bool drec_env = !getenv("MPGPU_HA_DREC") || atoi(getenv("MPGPU_HA_DREC")) != 0;
+  A.drec = drec_env ? (long long*)mp_ws(ctx, WS_HA4, sizeof(long long) * nB * np * HA_DREC) : nullptr;
+  A.dpos = Q.pos;
+  A.df = Q.f;
+  A.dseq = Q.seq;
+  A.dindex = Q.index;
+  A.drw = Q.rw;
+  A.dst = Q.st;
   A.cur_g = Q.cur_g;
   A.C = (int)C;
   static const bool stamps_on = HA_STAMP_CODE && getenv("MPGPU_HA_STAMPS") && atoi(getenv("MPGPU_HA_STAMPS")) == 1;

@@ -104,6 +104,7 @@ enum {
   WS_HA1,
   WS_HA2,
   WS_HA3,  // Hybrid A* diagnostics (MPGPU_HA_STAMPS)
+  WS_HA4,  // Hybrid A* neighbour groups' Dict records (IterArgs::drec)
   WS_FIN0,  // MPPI final-rollout snapshots, MP_FIN_RING slots
   WS_FIN_END = WS_FIN0 + MP_FIN_RING - 1,
   WS_SHARD_SEND,  // mp_mppi_plan_sharded: this rank's packed per-scene results
