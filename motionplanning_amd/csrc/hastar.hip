@@ -693,6 +693,12 @@ __device__ __forceinline__ void ha_mirror(const IterArgs& A, int it) {
 }
 
 constexpr int HA_DREC = 10;
+// (A/B build -DHA_DREC_CODE=1 + MPGPU_HA_DREC=1) the step launches' groups copy their neighbours' Dict entries
+// into the records: bit-exact but 0.3-0.5 ms slower per 256-plan (r05zf: the groups' extra loads / stores and
+// registers cost more than the bookkeeping's saved round trip), so compiled out by default
+#ifndef HA_DREC_CODE
+#define HA_DREC_CODE 0
+#endif
 
 // Bounded cross-block wait (ha_pipe_kernel, ha_persist_kernel): poll *p until it is >= v; past HA_SPIN_MAX
 // polls (~1 s) set *err and return HA_DONE (every waiter then leaves its loop: a wrong result, not a hang)
@@ -1302,7 +1308,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     // the pipelined launch's nn_lim below may be half-written: its g is loaded but never used)
     // (step launches) the rest of the neighbour's Dict entry for the bookkeeping, loaded beside gd and stored
     // after the sweep (the Dict is the one this iteration's FindNewNode starts from: it runs after every group)
-    const bool drec = A.drec && A.dnid && !A.node_ag && tid < nk;
+    const bool drec = HA_DREC_CODE && A.drec && A.dnid && !A.node_ag && tid < nk;
     long long dv[HA_DREC - 2];
     if (drec && hit >= 0) {
       const size_t q = (size_t)s * A.C + hit;
@@ -2216,7 +2222,7 @@ __device__ __forceinline__ BookRec ha_book_spec(const HaDev& P, const HaSearch& 
   int po = 0, drw = -1;
   double dtuv[3] = {0.0, 0.0, 0.0};
   long long so0 = 0, io = 0;
-  if (valid && !RSH && A.drec && A.dnid) {  // the groups' copies of the Dict entries (one round trip)
+  if (HA_DREC_CODE && valid && !RSH && A.drec && A.dnid) {  // the groups' copies of the Dict entries
     const long long* r = A.drec + ((size_t)b * np + tid) * HA_DREC;
     long long w[HA_DREC];
 #pragma unroll
@@ -3367,7 +3373,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
 // iteration as ha_step_kernel's finisher.  A finished scene publishes HA_DONE: every block of it leaves its loop.
 // Same operations on the same values as ha_pipe_kernel: the same search, bit for bit.  Every wait is bounded.
 template <int HWt, int NBGt>
-__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HA_WPE_TAIL))) void ha_persist_kernel(
+__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == HW_TAIL ? HA_WPE_TAIL : 3))) void ha_persist_kernel(
     HaDev P, HaSearch Q, IterArgs A, int B, int it0, double* rs_path2, unsigned char* rs_ok2, int* rs_len2) {
   __shared__ int sh_f;
   const int np = P.n_prim, ng = (np + NBGt - 1) / NBGt, per = 2 + ng;
@@ -3966,8 +3972,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool noskip = getenv("MPGPU_HA_NOSKIP") && atoi(getenv("MPGPU_HA_NOSKIP")) == 1;
   A.dnid = noskip ? nullptr : Q.nid;
   A.dg = Q.g;
-  // (A/B) MPGPU_HA_DREC=0: the bookkeeping looks the Dict entries up itself
-  static const bool drec_env = !getenv("MPGPU_HA_DREC") || atoi(getenv("MPGPU_HA_DREC")) != 0;
+  // (A/B, HA_DREC_CODE builds) MPGPU_HA_DREC=1: the groups' Dict records
+  static const bool drec_env = HA_DREC_CODE && getenv("MPGPU_HA_DREC") && atoi(getenv("MPGPU_HA_DREC")) == 1;
   A.drec = drec_env ? (long long*)mp_ws(ctx, WS_HA4, sizeof(long long) * nB * np * HA_DREC) : nullptr;
   A.dpos = Q.pos;
   A.df = Q.f;
@@ -4041,12 +4047,17 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // of it fits the device at once; (A/B) MPGPU_HA_PERSIST=0 keeps one ha_pipe_kernel launch per iteration
   static const bool persist_env = !getenv("MPGPU_HA_PERSIST") || atoi(getenv("MPGPU_HA_PERSIST")) != 0;
   int persist_cap = 0;
+  // the persistent kernel's block: 6 waves (two blocks per CU, so 28 scenes fit one launch; the groups' sweep on
+  // 3 waves beside the 3 word waves) or, (A/B) MPGPU_HA_PERSIST_HW=12, the pipelined shape's 12 (one per CU, 14
+  // scenes).  r05zg: 256-plan 24.7 -> 24.0 ms, the lone 729-pop scenario 18.7 -> 18.9 us per iteration
+  static const int phw = getenv("MPGPU_HA_PERSIST_HW") && atoi(getenv("MPGPU_HA_PERSIST_HW")) == 12 ? HW_TAIL : 6;
+  const void* persist_fn = phw == 6 ? reinterpret_cast<const void*>(ha_persist_kernel<6, NBG_TAIL>)
+                                    : reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>);
   double* rs_path2 = nullptr;
   int* rs_i2 = nullptr;
   if (tail_pipe && persist_env) {
     int nbpc = 0, cus = 0, coop = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbpc, reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
-                                                     64 * HW_TAIL, 0) == hipSuccess &&
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbpc, persist_fn, 64 * phw, 0) == hipSuccess &&
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
         hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device) == hipSuccess && coop)
       persist_cap = nbpc * cus;
@@ -4149,36 +4160,35 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       else
         hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
       hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
+    } else if (tail_pipe && known * (2 + (np + NBG_TAIL - 1) / NBG_TAIL) <= persist_cap) {
+      // the rest of the search in one cooperative launch, after the current nodes' expansion (bootstrap)
+      const int per_pipe = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
+      if (piped != 2)
+        hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL),
+                           0, ctx->stream, D, Q, A, B, it, 1);
+      unsigned char* rs_ok2 = reinterpret_cast<unsigned char*>(rs_i2);
+      int* rs_len2 = rs_i2 + 2 * nB;
+      int it0 = it;
+      void* args[] = {&D, &Q, &A, (void*)&B, &it0, &rs_path2, &rs_ok2, &rs_len2};
+      // (MPGPU_HA_COOP=0: an ordinary launch of the same grid, co-resident by the occupancy check alone -- for
+      // rocprofv3 runs: the profiler's exit handlers crash in a process that made a cooperative launch)
+      static const bool coop_env = !getenv("MPGPU_HA_COOP") || atoi(getenv("MPGPU_HA_COOP")) != 0;
+      const hipError_t le =
+          coop_env ? hipLaunchCooperativeKernel(persist_fn, dim3((unsigned)(known * per_pipe)), dim3(64 * phw), args, 0,
+                                                ctx->stream)
+                   : hipLaunchKernel(persist_fn, dim3((unsigned)(known * per_pipe)), dim3(64 * phw), args, 0, ctx->stream);
+      if (le != hipSuccess) {
+        cleanup();
+        return mp_fail(ctx, MP_ERR_HIP, "ha_persist_kernel launch failed");
+      }
+      persisted = true;
+      break;
     } else if (tail && tail_pipe && known * (2 + (np + NBG_TAIL - 1) / NBG_TAIL) <= pipe_blocks) {
       const int per_pipe = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
       if (piped != 2) {  // the current nodes' expansion, for the first pipelined launch
         hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL),
                            0, ctx->stream, D, Q, A, B, it, 1);
         piped = 2;
-      }
-      if (known * per_pipe <= persist_cap) {  // the rest of the search in one cooperative launch
-        unsigned char* rs_ok2 = reinterpret_cast<unsigned char*>(rs_i2);
-        int* rs_len2 = rs_i2 + 2 * nB;
-        int it0 = it;
-        void* args[] = {&D, &Q, &A, (void*)&B, &it0, &rs_path2, &rs_ok2, &rs_len2};
-        // (MPGPU_HA_COOP=0: an ordinary launch of the same grid, co-resident by the occupancy check alone --
-        // for rocprofv3 runs: the profiler's exit handlers crash in a process that made a cooperative launch)
-        static const bool coop_env = !getenv("MPGPU_HA_COOP") || atoi(getenv("MPGPU_HA_COOP")) != 0;
-        hipError_t le;
-        if (coop_env) {
-          le = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
-                                          dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), args, 0, ctx->stream);
-        } else {
-          hipLaunchKernelGGL((ha_persist_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)),
-                             dim3(64 * HW_TAIL), 0, ctx->stream, D, Q, A, B, it0, rs_path2, rs_ok2, rs_len2);
-          le = hipGetLastError();
-        }
-        if (le != hipSuccess) {
-          cleanup();
-          return mp_fail(ctx, MP_ERR_HIP, "ha_persist_kernel cooperative launch failed");
-        }
-        persisted = true;
-        break;
       }
       hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), 0,
                          ctx->stream, D, Q, A, B, it, 0);
