@@ -4049,10 +4049,14 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   int persist_cap = 0;
   // the persistent kernel's block: 6 waves (two blocks per CU, so 28 scenes fit one launch; the groups' sweep on
   // 3 waves beside the 3 word waves) or, (A/B) MPGPU_HA_PERSIST_HW=12, the pipelined shape's 12 (one per CU, 14
-  // scenes).  r05zg: 256-plan 24.7 -> 24.0 ms, the lone 729-pop scenario 18.7 -> 18.9 us per iteration
-  static const int phw = getenv("MPGPU_HA_PERSIST_HW") && atoi(getenv("MPGPU_HA_PERSIST_HW")) == 12 ? HW_TAIL : 6;
-  const void* persist_fn = phw == 6 ? reinterpret_cast<const void*>(ha_persist_kernel<6, NBG_TAIL>)
-                                    : reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>);
+  // scenes), or MPGPU_HA_PERSIST_HW=4 (three per CU, 42 scenes: the sweep on one wave).  r05zg: 256-plan 24.7 ->
+  // 24.0 ms with 6 (lone 729-pop scenario 18.7 -> 18.9 us per iteration); r05zh: 4 plans the 256 batch in the
+  // same time, its 32-scene shards faster (strided shard 0 18.4 -> 16.4 ms), the lone scenario slower (20.4 us)
+  static const int phw_env = getenv("MPGPU_HA_PERSIST_HW") ? atoi(getenv("MPGPU_HA_PERSIST_HW")) : 6;
+  static const int phw = phw_env == 12 ? HW_TAIL : phw_env == 4 ? 4 : 6;
+  const void* persist_fn = phw == 6   ? reinterpret_cast<const void*>(ha_persist_kernel<6, NBG_TAIL>)
+                           : phw == 4 ? reinterpret_cast<const void*>(ha_persist_kernel<4, NBG_TAIL>)
+                                      : reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>);
   double* rs_path2 = nullptr;
   int* rs_i2 = nullptr;
   if (tail_pipe && persist_env) {
