@@ -221,3 +221,27 @@ def test_translated_scene_bitexact(ctx, shift, cull):
         assert np.array_equal(h.r.hybrid_astar_states.T, ref["states"])
         assert np.array_equal(h.r.RSpath_final.T, ref["rs_path"])
     assert ref["pops"] > 1
+
+
+def test_primitive_table_memo(ctx):
+    """mp_ha_neighbor_origin keeps the installed table while the settings repeat (plan_batch calls it every
+    time): a repeat returns the same table, different settings install their own (each vs the oracle), and a
+    plan after a settings change plans with the new table (bit-exact vs the oracle)."""
+    import copy
+
+    h, p, sc, pc = _setup(ctx)
+    sc2, pc2 = ha.install_primitives(h, ctx)  # memo hit
+    assert np.array_equal(sc2, sc) and np.array_equal(pc2, pc)
+    h3 = copy.deepcopy(h)
+    h3.s.steer_set = h.s.steer_set * 0.5  # other primitives, same shapes
+    sc3, pc3 = ha.install_primitives(h3, ctx)
+    sco, pco = oracle.ha_neighbor_origin(h3.s.expand_time, h3.s.steer_set, h3.s.gear_set)
+    assert np.array_equal(sc3, sco) and np.array_equal(pc3, pco) and not np.array_equal(pc3, pc)
+    hs = ha.scenario_batch(4, seed=7)
+    ha.plan_batch(hs, ctx=ctx)  # its own settings again: reinstalled, then planned
+    h0 = hs[0]
+    scb, pcb = oracle.ha_neighbor_origin(h0.s.expand_time, h0.s.steer_set, h0.s.gear_set)
+    pb = ha.params_of(h0)
+    for h4 in hs:
+        ref = oracle.ha_plan(pb, h4.s.starting_states, h4.s.ending_states, np.array(h4.s.obstacle_list), scb, pcb)
+        assert h4.r.loop_count == ref["pops"] and np.array_equal(h4.r.pop_sequence, ref["pop_seq"])
