@@ -609,6 +609,11 @@ struct IterArgs {
   int no_pre;  // (A/B, MPGPU_HA_PRESCAN=0) the prescan block only marks its record stale: the bookkeeping scans
   int rs_last;  // ha_step_kernel dispatches the RS_connected blocks last ((A/B) MPGPU_HA_RS_LAST=0: first)
   int node_ag;  // read the node agent-coherently (written in this launch), once node_flag[s] >= node_flag_min
+  // (tail pipe / persistent launches) the node as tagged granules instead: [B][HA_NGR] of {tag, 32-bit value},
+  // this parity's, complete once every tag equals ngr_tag (see ha_publish_node)
+  const unsigned long long* ngr;
+  unsigned ngr_tag;
+  int ngr_pub;  // the tail's bookkeeping publishes granules (else the node buffers + a drained flag); (A/B) MPGPU_HA_NGR
   const int* node_flag;
   int node_flag_min;
   int* node_flag_err;  // the wait is bounded: past HA_SPIN_MAX polls it sets *node_flag_err and gives up
@@ -715,6 +720,56 @@ __device__ __forceinline__ int wait_ge(const int* p, int v, int* err) {
     f = ld_ag(p);
   }
   return f;
+}
+
+// The popped node handed to the expansion and RS_connected blocks of the same launch as tagged granules (the
+// data IS the flag): 14 one-word {tag = iteration + 1, value} records -- the state's and the stored commands'
+// six double halves each, the winner word, the go bit -- each written by ONE agent-scope 8-byte store of its
+// own lane, so the bookkeeping neither drains its stores nor raises a separate flag, and a consumer wave polls
+// the 14 words until every tag matches (one round trip instead of flag + node).  HA_NGR_DONE in the go word:
+// the scene's search ended.
+constexpr int HA_NGR = 16;
+constexpr unsigned HA_NGR_DONE = 0xffffffffu;
+__device__ __forceinline__ void ha_publish_node(unsigned long long* g, unsigned tag, int lane, const long long* w,
+                                                bool go) {
+  if (lane >= 14) return;
+  unsigned v;
+  if (lane < 6) v = (unsigned)((unsigned long long)w[3 + (lane >> 1)] >> (32 * (lane & 1)));  // state
+  else if (lane < 12) v = (unsigned)((unsigned long long)w[7 + ((lane - 6) >> 1)] >> (32 * (lane & 1)));  // tuv
+  else if (lane == 12) v = (unsigned)(int)w[6];  // rs winner word
+  else v = go;
+  __hip_atomic_store(g + lane, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// wave 0 of a consumer block; returns go (0: the search ended or the wait ran out), the node in st / tuv / rw
+__device__ __forceinline__ int ha_consume_node(const unsigned long long* g, unsigned tag, int lane, double* st,
+                                               double* tuv, int* rw, int* err) {
+  unsigned long long x = 0;
+  for (long long n = 0;; n++) {
+    x = lane < 14 ? __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const unsigned t = (unsigned)(x >> 32);
+    const unsigned tg = __shfl(t, 13);
+    if (tg == HA_NGR_DONE) return 0;
+    if (__all(lane >= 14 || t == tag)) break;
+    if (n >= HA_SPIN_MAX) {
+      if (lane == 0 && err) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  const unsigned v = (unsigned)x;
+  const int go = (int)__shfl(v, 13);
+#pragma unroll
+  for (int e = 0; e < 3; e++) {
+    const unsigned lo = __shfl(v, 2 * e), hi = __shfl(v, 2 * e + 1);
+    const unsigned tlo = __shfl(v, 6 + 2 * e), thi = __shfl(v, 7 + 2 * e);
+    if (lane == 0) {
+      st[e] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+      tuv[e] = __longlong_as_double((long long)(((unsigned long long)thi << 32) | tlo));
+    }
+  }
+  const int w = (int)__shfl(v, 12);
+  if (lane == 0) *rw = w;
+  return go;
 }
 
 // output addressing: per scene
@@ -984,8 +1039,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   const int nw = P.n_walls;
   const double* node = A.node + 3 * s;
   const double* goal = A.goal + 3 * s;
-  __shared__ double nd_s[3], nd_g;
-  __shared__ int nd_go, nd_nn;
+  __shared__ double nd_s[3], nd_g, nd_tuv[3];
+  __shared__ int nd_go, nd_nn, nd_rw;
   const OutRef R = out_ref(A, s, P.n_prim);
   const int k0 = rs ? 0 : (item - 1) * NBG, nk = rs ? 0 : min(NBG, P.n_prim - k0);
   // wall corners (Block2Pts) and their SAT tables in LDS: precomputed once per plan
@@ -1013,13 +1068,23 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   if (tid < NBG) g_free[tid] = 1;
   if (A.node_ag) {  // the node comes from another block of this launch (ha_pipe_kernel's bookkeeping): wait for
     // its ready flag (the walls are staged meanwhile), then read it agent-coherently
-    if (tid == 0) nd_go = wait_ge(A.node_flag + s, A.node_flag_min, A.node_flag_err) & 1;
-    __syncthreads();
-    if (!nd_go) return false;  // block-uniform: the search ended, nothing to expand
-    if (tid < 3) nd_s[tid] = ld_ag(A.node + 3 * s + tid);
-    if (tid == 3 && A.node_g) nd_g = ld_ag(A.node_g + s);
-    if (tid == 4 && A.node_g) nd_nn = ld_ag(A.node_nn + s);
-    __syncthreads();
+    if (A.ngr) {  // tagged granules: the node and its ready state in one poll (ha_consume_node)
+      if (tid < 64) {
+        const int go = ha_consume_node(A.ngr + (size_t)s * HA_NGR, A.ngr_tag, tid, nd_s, nd_tuv, &nd_rw,
+                                       A.node_flag_err);
+        if (tid == 0) nd_go = go;
+      }
+      __syncthreads();
+      if (!nd_go) return false;  // block-uniform: the search ended, nothing to expand
+    } else {
+      if (tid == 0) nd_go = wait_ge(A.node_flag + s, A.node_flag_min, A.node_flag_err) & 1;
+      __syncthreads();
+      if (!nd_go) return false;  // block-uniform: the search ended, nothing to expand
+      if (tid < 3) nd_s[tid] = ld_ag(A.node + 3 * s + tid);
+      if (tid == 3 && A.node_g) nd_g = ld_ag(A.node_g + s);
+      if (tid == 4 && A.node_g) nd_nn = ld_ag(A.node_nn + s);
+      __syncthreads();
+    }
     node = nd_s;
   }
   // the tail shape (threads to spare): the collision sweep splits every pose into its 2·n_walls SAT terms,
@@ -1095,7 +1160,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     // allpath + findmin: RS_connected's optimal command from the popped node
     double ns[3];
     // the popped node's stored rs_heuristic winner (agent-coherently when published in this launch)
-    const int known = A.node_rw ? (A.node_ag ? ld_ag(A.node_rw + s) : A.node_rw[s]) : -1;
+    const int known =
+        A.node_rw ? (A.node_ag ? (A.ngr ? nd_rw : ld_ag(A.node_rw + s)) : A.node_rw[s]) : -1;
     if (tabm >= 0)
       change_basis_sc(node, goal, P.minR, A.htn[2 * tabm], A.htn[2 * tabm + 1], ns);
     else
@@ -1105,7 +1171,8 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
     if (known >= 0 && (known & RW_TUV)) {  // block-uniform: the commands stored at the node's creation
       if (tid == 0) {
         double tv[3];
-        for (int e = 0; e < 3; e++) tv[e] = A.node_ag ? ld_ag(A.node_tuv + 3 * s + e) : A.node_tuv[3 * s + e];
+        for (int e = 0; e < 3; e++)
+          tv[e] = A.node_ag ? (A.ngr ? nd_tuv[e] : ld_ag(A.node_tuv + 3 * s + e)) : A.node_tuv[3 * s + e];
         cmd_from_tuv(known, tv, cmd);
       }
     } else if (known >= 0 && known < 48)
@@ -1598,6 +1665,7 @@ struct HaSearch {
   long long* pre;        // [B][PRE_W] (RSH tail) the prescan's record: popfirst!'s K least entries before FindNewNode
   double* node_g;        // [2][B] (full-width ha_pipe_kernel) the popped node's g, double-buffered like node
   int* node_nn;          // [2][B] the scene's node count before the FindNewNode that published the node
+  unsigned long long* ngr;  // [2][B][HA_NGR] the popped node as tagged granules (ha_publish_node), by parity
   int* nx;               // [B] (ha_pipe_kernel) 2·it + 2 + go once iteration it's bookkeeping has popped the next node
   int* ex;               // [B] (ha_persist_kernel) expansions finished (neighbour groups, cumulative)
   int* rsr;              // [B] (ha_persist_kernel) 2·it + 2 once RS_connected(n_it) has run
@@ -3053,19 +3121,33 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the winner's LDS writes before the wave reads them
-    if (go) {
-      // publish the next node: state, stored commands, then the ready flag (the expansion blocks spin on it)
-      if (lane < 3) {
-        st_ag(Q.node + (size_t)(it & 1) * 3 * B + 3 * b + lane, __longlong_as_double(s_win[3 + lane]));
-        st_ag(Q.node_tuv + (size_t)(it & 1) * 3 * B + 3 * b + lane, __longlong_as_double(s_win[7 + lane]));
+    if (RSH && E.ngr_pub) {
+      // publish the next node as tagged granules (ha_publish_node): no drain, no separate flag; the node
+      // buffers too, for the next launch's RS_connected (a launch boundary orders those)
+      long long wv[10];
+#pragma unroll
+      for (int e = 0; e < 10; e++) wv[e] = go ? s_win[e] : 0;
+      ha_publish_node(Q.ngr + ((size_t)(it & 1) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv, go);
+      if (go && lane < 3) {
+        Q.node[(size_t)(it & 1) * 3 * B + 3 * b + lane] = __longlong_as_double(s_win[3 + lane]);
+        Q.node_tuv[(size_t)(it & 1) * 3 * B + 3 * b + lane] = __longlong_as_double(s_win[7 + lane]);
       }
-      if (lane == 0) st_ag(Q.node_rw + (size_t)(it & 1) * B + b, (int)s_win[6]);
-      if (!RSH && lane == 1) st_ag(Q.node_g + (size_t)(it & 1) * B + b, __longlong_as_double(s_win[1]));
-      if (!RSH && lane == 2) st_ag(Q.node_nn + (size_t)(it & 1) * B + b, nn0);
+      if (go && lane == 0) Q.node_rw[(size_t)(it & 1) * B + b] = (int)s_win[6];
+    } else {
+      if (go) {
+        // publish the next node: state, stored commands, then the ready flag (the expansion blocks spin on it)
+        if (lane < 3) {
+          st_ag(Q.node + (size_t)(it & 1) * 3 * B + 3 * b + lane, __longlong_as_double(s_win[3 + lane]));
+          st_ag(Q.node_tuv + (size_t)(it & 1) * 3 * B + 3 * b + lane, __longlong_as_double(s_win[7 + lane]));
+        }
+        if (lane == 0) st_ag(Q.node_rw + (size_t)(it & 1) * B + b, (int)s_win[6]);
+        if (!RSH && lane == 1) st_ag(Q.node_g + (size_t)(it & 1) * B + b, __longlong_as_double(s_win[1]));
+        if (!RSH && lane == 2) st_ag(Q.node_nn + (size_t)(it & 1) * B + b, nn0);
+      }
+      ha_stores_done();
+      if (lane == 0) st_ag(Q.nx + b, 2 * it + 2 + (go ? 1 : 0));
     }
-    ha_stores_done();
     if (lane == 0) {
-      st_ag(Q.nx + b, 2 * it + 2 + (go ? 1 : 0));
       s_go = go;
       s_win[10] = wpos;
     }
@@ -3308,6 +3390,9 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
       if (!RSH) {  // the Dict pre-check beside FindNewNode's writes (ha_iter_body)
         X.node_g = Q.node_g + (size_t)(it & 1) * B;
         X.node_nn = Q.node_nn + (size_t)(it & 1) * B;
+      } else if (A.ngr_pub) {  // the node as tagged granules
+        X.ngr = Q.ngr + (size_t)(it & 1) * B * HA_NGR;
+        X.ngr_tag = (unsigned)it + 1;
       }
     }
     X.do_rs = 0;
@@ -3389,6 +3474,17 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
     X.rs_len = rs_len2 + (size_t)(it & 1) * B;
     X.rs_path = rs_path2 + (size_t)(it & 1) * B * MAXPATH * 3;
   };
+  // (HA_STAMP_CODE builds, MPGPU_HA_STAMPS=1) this block's stamp record for iteration it, as ha_step_kernel's
+  auto pst = [&](int it) -> unsigned long long* {
+    if (!HA_STAMP_CODE || !A.stamps || it % HA_STAMP_EVERY || it / HA_STAMP_EVERY >= 40 ||
+        (int)blockIdx.x >= A.stamp_blocks || threadIdx.x)
+      return nullptr;
+    return A.stamps + ((size_t)(it / HA_STAMP_EVERY) * A.stamp_blocks + blockIdx.x) * HA_STAMP_N;
+  };
+  auto now = [] { return __builtin_amdgcn_s_memrealtime(); };
+  auto put = [](unsigned long long* p, int i, unsigned long long v) {
+    if (p) __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   if (item >= 2) {  // the expansion of n_{it+1}, it = it0, it0 + 1, ...
     for (int it = it0;; it++) {
       IterArgs X = e_par(A, B, np, (it + 1) & 1);
@@ -3397,11 +3493,19 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
       X.node_flag = Q.nx;
       X.node_flag_min = 2 * it + 2;
       X.node_flag_err = Q.err;
+      if (A.ngr_pub) {
+        X.ngr = Q.ngr + (size_t)(it & 1) * B * HA_NGR;
+        X.ngr_tag = (unsigned)it + 1;
+      }
       X.do_rs = 0;
-      if (!ha_iter_body<HWt, NBGt, true>(P, X, nullptr, slot, item - 1)) return;  // the search ended
+      unsigned long long* stp = pst(it);
+      put(stp, 0, now());
+      if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 1)) return;  // the search ended
       ha_stores_done();
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_fetch_add(Q.ex + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      put(stp, 1, now());
+      put(stp, 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 1) << 32));
     }
   }
   if (item == 0) {  // RS_connected(n_it), it = it0, it0 + 1, ...
@@ -3415,31 +3519,43 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         X.node_flag = Q.nx;
         X.node_flag_min = 2 * (it - 1) + 2;
         X.node_flag_err = Q.err;
+        if (A.ngr_pub) {
+          X.ngr = Q.ngr + (size_t)((it - 1) & 1) * B * HA_NGR;
+          X.ngr_tag = (unsigned)it;
+        }
       }
       rs_par(X, it);
       X.do_exp = 0;
-      if (!ha_iter_body<HWt, NBGt, true>(P, X, nullptr, slot, 0)) return;
+      unsigned long long* stp = pst(it);
+      put(stp, 0, now());
+      if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, 0)) return;
       ha_stores_done();
       __syncthreads();
       if (threadIdx.x == 0) st_ag(Q.rsr + s, 2 * it + 2);
+      put(stp, 1, now());
+      put(stp, 5, 2ull | ((unsigned long long)s << 4));
     }
   }
   // item 1: the bookkeeping of iteration it, it = it0, it0 + 1, ...
   for (int it = it0;; it++) {
     // E[it & 1]: every group of iteration it - 1 has expanded n_it (waited for inside, the open list's loads
     // in flight)
+    unsigned long long* stp = pst(it);
+    put(stp, 0, now());
     const auto wait_exp = [&] {
       if (it > it0) {
         if (threadIdx.x == 0) wait_ge(Q.ex + s, ng * (it - it0), Q.err);
         __syncthreads();
       }
+      put(stp, 2, now());  // (the book's wait for the expansion ends)
     };
 #ifndef HA_PREWAIT
 #define HA_PREWAIT 1
 #endif
     if (!HA_PREWAIT) wait_exp();  // (A/B build -DHA_PREWAIT=0: the wait before the bookkeeping's first load)
-    const BookRec br = HA_PREWAIT ? ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, nullptr, wait_exp)
-                                  : ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s);
+    const BookRec br = HA_PREWAIT ? ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, stp, wait_exp)
+                                  : ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, stp);
+    put(stp, 3, now());
     IterArgs F = A;
     rs_par(F, it);
     if (threadIdx.x == 0) {
@@ -3452,6 +3568,8 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         ha_finish(Q, F, B, it, s, br, false);
         sh_f = ld_ag(F.rs_ok + s) ? 1 : !br.v[RC_GO] ? 2 : 0;
       }
+      put(stp, 4, now());
+      put(stp, 5, 1ull | ((unsigned long long)s << 4) | (17ull << 32));
     }
     __syncthreads();
     if (sh_f == 1) {  // RSpath_final into the canonical buffer the host reads
@@ -3460,7 +3578,10 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         A.rs_path[(size_t)s * MAXPATH * 3 + i] = ld_ag(F.rs_path + (size_t)s * MAXPATH * 3 + i);
     }
     if (sh_f) {
-      if (threadIdx.x == 0) st_ag(Q.nx + s, HA_DONE);
+      if (A.ngr_pub && threadIdx.x < 2)  // the search ended: both parities' go words (whichever is waited on)
+        __hip_atomic_store(Q.ngr + ((size_t)threadIdx.x * B + s) * HA_NGR + 13,
+                           (unsigned long long)HA_NGR_DONE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!A.ngr_pub && threadIdx.x == 0) st_ag(Q.nx + s, HA_DONE);
       return;
     }
     __syncthreads();
@@ -3858,7 +3979,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + 256 * 56);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + nB * 2 * HA_NGR * 8 + 256 * 57);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -3900,6 +4021,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.node_tuv = (double*)take(nB * 48);
   Q.pre = (long long*)take(nB * PRE_W * 8);
   Q.nx = (int*)take(nB * 4);
+  Q.ngr = (unsigned long long*)take(nB * 2 * HA_NGR * 8);
   Q.ex = (int*)take(nB * 4);
   Q.rsr = (int*)take(nB * 4);
   Q.err = (int*)take(4);
@@ -4010,6 +4132,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.tk, 0, sizeof(int) * 2 * nB, ctx->stream));  // the finishers reset them
   MP_HIP(ctx, hipMemsetAsync(Q.rec, 0, sizeof(long long) * RC_N * nB, ctx->stream));  // record-ready flags
   MP_HIP(ctx, hipMemsetAsync(Q.nx, 0, sizeof(int) * nB, ctx->stream));  // ha_pipe_kernel's pop flags
+  MP_HIP(ctx, hipMemsetAsync(Q.ngr, 0, sizeof(unsigned long long) * nB * 2 * HA_NGR, ctx->stream));  // granule tags
   MP_HIP(ctx, hipMemsetAsync(Q.ex, 0, sizeof(int) * nB, ctx->stream));  // ha_persist_kernel's flags
   MP_HIP(ctx, hipMemsetAsync(Q.rsr, 0, sizeof(int) * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.err, 0, sizeof(int), ctx->stream));
@@ -4092,6 +4215,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool rs_last_env = !getenv("MPGPU_HA_RS_LAST") || atoi(getenv("MPGPU_HA_RS_LAST")) != 0;  // r05o: -0.2 ms
   A.rs_last = rs_last_env;
   A.no_tuv = !tuv_env;
+  static const bool ngr_env = !getenv("MPGPU_HA_NGR") || atoi(getenv("MPGPU_HA_NGR")) != 0;
+  A.ngr_pub = ngr_env;
   // (A/B, MPGPU_HA_FULL_TUV=1) the full-width groups' winners' (t, u, v) too, so a node popped there also skips
   // RS_connected's word evaluation (RS search phase 6-9 -> 1.2 us) -- neutral per plan (r05u: RS_connected is
   // not the full-width chain) and 10 more spilled VGPRs, so off
