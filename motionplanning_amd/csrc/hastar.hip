@@ -4170,26 +4170,48 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // of it fits the device at once; (A/B) MPGPU_HA_PERSIST=0 keeps one ha_pipe_kernel launch per iteration
   static const bool persist_env = !getenv("MPGPU_HA_PERSIST") || atoi(getenv("MPGPU_HA_PERSIST")) != 0;
   int persist_cap = 0;
-  // the persistent kernel's block: 6 waves (two blocks per CU, so 28 scenes fit one launch; the groups' sweep on
-  // 3 waves beside the 3 word waves) or, (A/B) MPGPU_HA_PERSIST_HW=12, the pipelined shape's 12 (one per CU, 14
-  // scenes), or MPGPU_HA_PERSIST_HW=4 (three per CU, 42 scenes: the sweep on one wave).  r05zg: 256-plan 24.7 ->
-  // 24.0 ms with 6 (lone 729-pop scenario 18.7 -> 18.9 us per iteration); r05zh: 4 plans the 256 batch in the
-  // same time, its 32-scene shards faster (strided shard 0 18.4 -> 16.4 ms), the lone scenario slower (20.4 us)
-  static const int phw_env = getenv("MPGPU_HA_PERSIST_HW") ? atoi(getenv("MPGPU_HA_PERSIST_HW")) : 6;
-  static const int phw = phw_env == 12 ? HW_TAIL : phw_env == 4 ? 4 : 6;
-  const void* persist_fn = phw == 6   ? reinterpret_cast<const void*>(ha_persist_kernel<6, NBG_TAIL>)
-                           : phw == 4 ? reinterpret_cast<const void*>(ha_persist_kernel<4, NBG_TAIL>)
-                                      : reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>);
+  // the persistent kernel's block: 12 waves (one per CU: 14 scenes per launch), 6 (two per CU: 28 scenes; the
+  // groups' sweep on 3 waves beside the 3 word waves) or 4 (three per CU: 42 scenes; the sweep on one wave).
+  // Per call, the largest block that holds the whole batch in one launch from the start, and 6 when none does
+  // (the tail then starts at 28 live scenes).  Measured: a lone scenario 18.7 / 18.9 / 20.4 us per iteration
+  // with 12 / 6 / 4 (r05zg, r05zh); the 256-plan 24.0 ms with 6 or 4, 24.7 with 12; a 32-scene shard 16.4 ms with
+  // 4 against 18.4-20.1 with 6, whose tail starts only at 28 live scenes, two blocks sharing each CU.
+  // (A/B) MPGPU_HA_PERSIST_HW=12 / 6 / 4 forces one.
+  static const int phw_env = getenv("MPGPU_HA_PERSIST_HW") ? atoi(getenv("MPGPU_HA_PERSIST_HW")) : 0;
+  const int per_ps = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
+  const void* pfn[3] = {reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
+                        reinterpret_cast<const void*>(ha_persist_kernel<6, NBG_TAIL>),
+                        reinterpret_cast<const void*>(ha_persist_kernel<4, NBG_TAIL>)};
+  const int phws[3] = {HW_TAIL, 6, 4};
+  static int pcap[3] = {-1, -1, -1};  // co-resident blocks of each (0: no cooperative launch)
+  int phw = 6;
+  const void* persist_fn = pfn[1];
   double* rs_path2 = nullptr;
   int* rs_i2 = nullptr;
   if (tail_pipe && persist_env) {
-    int nbpc = 0, cus = 0, coop = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbpc, persist_fn, 64 * phw, 0) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
-        hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device) == hipSuccess && coop)
-      persist_cap = nbpc * cus;
-    (void)hipGetLastError();
-    if (getenv("MPGPU_HA_VERBOSE")) fprintf(stderr, "ha_persist_kernel: %d blocks co-resident\n", persist_cap);
+    if (pcap[0] < 0) {
+      int cus = 0, coop = 0;
+      const bool ok = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) == hipSuccess &&
+                      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, ctx->device) == hipSuccess && coop;
+      for (int v = 0; v < 3; v++) {
+        int nbpc = 0;
+        pcap[v] = ok && hipOccupancyMaxActiveBlocksPerMultiprocessor(&nbpc, pfn[v], 64 * phws[v], 0) == hipSuccess
+                      ? nbpc * cus : 0;
+      }
+      (void)hipGetLastError();
+    }
+    int v = 1;
+    if (phw_env == 12 || phw_env == 6 || phw_env == 4) {
+      v = phw_env == 12 ? 0 : phw_env == 6 ? 1 : 2;
+    } else {
+      for (int c = 0; c < 3; c++)
+        if (B * per_ps <= pcap[c]) { v = c; break; }
+    }
+    phw = phws[v];
+    persist_fn = pfn[v];
+    persist_cap = pcap[v];
+    if (getenv("MPGPU_HA_VERBOSE"))
+      fprintf(stderr, "ha_persist_kernel<%d>: %d blocks co-resident\n", phw, persist_cap);
     rs_path2 = (double*)mp_ws(ctx, WS_IO15, sizeof(double) * 2 * nB * MAXPATH * 3);
     rs_i2 = (int*)mp_ws(ctx, WS_IO16, sizeof(int) * 4 * nB);
     if (!rs_path2 || !rs_i2) return MP_ERR_NOMEM;
