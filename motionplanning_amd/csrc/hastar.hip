@@ -4369,7 +4369,12 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                          ctx->stream, D, Q, A, B, it);
     }
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
-    if (!hm && (it % CH == 0 || it == mp)) {
+    // near the persistent tail's threshold the live count is read every 4 iterations, at most one chunk late, so
+    // the tail starts close to the iteration its count allows; (A/B) MPGPU_HA_NEAR_CH=0: every CH throughout
+    static const int near_ch = getenv("MPGPU_HA_NEAR_CH") ? atoi(getenv("MPGPU_HA_NEAR_CH")) : 4;
+    const bool near = near_ch > 0 && persist_cap > 0 && known * per_ps <= 2 * persist_cap;
+    const int ch = near ? near_ch : CH;
+    if (!hm && (it % ch == 0 || it == mp)) {
       const int slot = chunk % NCK;
       if (hipMemcpyAsync(hl + slot, Q.live + it, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
           hipEventRecord(ev[slot], ctx->stream) != hipSuccess) {
@@ -4380,7 +4385,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       // poll finished chunks without blocking; block only when two chunks ahead
       while (checked < chunk) {
         const int cs = checked % NCK;
-        const bool must = chunk - checked > 2;
+        const bool must = chunk - checked > (near ? 1 : 2);
         const hipError_t q = must ? hipEventSynchronize(ev[cs]) : hipEventQuery(ev[cs]);
         if (q == hipErrorNotReady) break;
         if (q != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "event wait failed"); }
