@@ -4369,9 +4369,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                          ctx->stream, D, Q, A, B, it);
     }
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
-    // near the persistent tail's threshold the live count is read every 4 iterations, at most one chunk late, so
-    // the tail starts close to the iteration its count allows; (A/B) MPGPU_HA_NEAR_CH=0: every CH throughout
-    static const int near_ch = getenv("MPGPU_HA_NEAR_CH") ? atoi(getenv("MPGPU_HA_NEAR_CH")) : 4;
+    // (A/B, MPGPU_HA_NEAR_CH=n) near the persistent tail's threshold the live count read every n iterations, at
+    // most one chunk late, so the tail starts close to the iteration its count allows: measured 1 ms slower per
+    // 256-plan at n = 4 (r05zn: the copies' stream gaps and the shorter lead cost more than the earlier start)
+    static const int near_ch = getenv("MPGPU_HA_NEAR_CH") ? atoi(getenv("MPGPU_HA_NEAR_CH")) : 0;
     const bool near = near_ch > 0 && persist_cap > 0 && known * per_ps <= 2 * persist_cap;
     const int ch = near ? near_ch : CH;
     if (!hm && (it % ch == 0 || it == mp)) {
