@@ -419,7 +419,8 @@ def bench_ilqr(ctx, world, rank, cpu=None, reps=20, B=4096, N=100):
     # the whole ILQR.jl loop (mp_ilqr_solve: backward + 16-wide quad line search per iteration, at most
     # 60 iterations; instances that never find a decrease stop at max_ls and are reported, not hidden)
     ps = ilqr.params(N=N, max_iter=60)
-    ilqr.ilqr_solve(ps, X, U, ctx=ctx)
+    for _ in range(2):  # warm-up (workspaces, clocks: the solve time settles after ~2 solves)
+        ilqr.ilqr_solve(ps, X, U, ctx=ctx)
     runs = []
     for _ in range(3):  # the median of three timed solves (one solve moves +-1.5 ms with the clock ramp)
         if world > 1:
@@ -462,7 +463,7 @@ def bench_hastar(ctx, world, rank, cpu=None):
 
     dev = torch.device("cuda", torch.cuda.current_device())
     hs = ha.scenario_batch(256, seed=4)
-    for _ in range(2):  # warm-up: same batch size (workspaces, clocks)
+    for _ in range(4):  # warm-up: same batch size (workspaces, clocks: the plan time settles after ~4 plans)
         D.hybrid_astar_sharded(ha.scenario_batch(256, seed=5), ctx=ctx)
     runs = []
     for _ in range(3):  # the median of three timed plans of the same batch
