@@ -3263,7 +3263,12 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
 #endif
 constexpr int HA_STAMP_EVERY = 25, HA_STAMP_N = 17;  // [6..11]: bookkeeping phases; [12..16]: block body phases
 template <int HWt, int NBGt, bool RSH = false>
-__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == HW_TAIL ? HA_WPE_TAIL : HA_WPE_FULL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
+// (the 6-wave middle shape at 3 waves per SIMD -- 139 VGPRs, no spills, still two blocks per CU -- measured 1.4 ms
+// slower per 256-plan than at 4 with 128 VGPRs and spills, r05zp; kept at 4)
+#ifndef HA_WPE_MID
+#define HA_WPE_MID 4
+#endif
+__global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == HW_TAIL ? HA_WPE_TAIL : HWt == 6 ? HA_WPE_MID : HA_WPE_FULL))) void ha_step_kernel(HaDev P, HaSearch Q, IterArgs A, int B, int it) {
   __shared__ int role;
   unsigned long long* stp = nullptr;
   if (HA_STAMP_CODE && A.stamps && it % HA_STAMP_EVERY == 0 && it / HA_STAMP_EVERY < 40 && (int)blockIdx.x < A.stamp_blocks &&
