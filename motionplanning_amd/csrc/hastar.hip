@@ -3490,6 +3490,16 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   auto put = [](unsigned long long* p, int i, unsigned long long v) {
     if (p) __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
+  // (A/B build -DHA_PERSIST_PRIO=1) where blocks of several scenes share a CU, issue priority by role -- the
+  // bookkeeping 2 and the expansion 1 (the scene's chain), RS_connected 0 (beside it): neutral (r05zr), off
+#ifndef HA_PERSIST_PRIO
+#define HA_PERSIST_PRIO 0
+#endif
+  if (HA_PERSIST_PRIO) {
+    if (item == 0) __builtin_amdgcn_s_setprio(0);
+    else if (item == 1) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(1);
+  }
   if (item >= 2) {  // the expansion of n_{it+1}, it = it0, it0 + 1, ...
     for (int it = it0;; it++) {
       IterArgs X = e_par(A, B, np, (it + 1) & 1);
