@@ -1115,6 +1115,13 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
   HSTAMP(12);
   __syncthreads();
   const int j = lane >> 2;
+  // (A/B build -DHA_SWEEP_PROBE=1, non-RSH groups) the last swept pose of every neighbour first: a neighbour that
+  // collides there (the far end of its primitive) skips its other poses -- whole waves of them, as a wave covers
+  // about one neighbour's poses.  Same result (an OR over poses); measured 0.3-0.4 ms slower per 256-plan
+  // (r05zt: the extra phase and barrier cost more than the skipped rounds), so off.
+#ifndef HA_SWEEP_PROBE
+#define HA_SWEEP_PROBE 0
+#endif
   auto sweep = [&](int npose, int nthr = 64 * HWt) {
     double nsn = 0.0, ncs = 1.0;
     if (!rs) {
@@ -1126,12 +1133,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       }
     }
     const int parts = SPLIT ? 2 * nw : 1;
-    const int total = (rs ? npose : nk * npose) * parts;
-    for (int t = tid; t < total; t += nthr) {
-      const int tp = SPLIT ? t / parts : t, part = SPLIT ? t - tp * parts : 0;
-      const int jn = rs ? 0 : tp / npose, jp = rs ? tp : tp - jn * npose;
-      if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
-      if (!g_free[jn]) continue;  // already colliding: block_collision_check stops at its first hit
+    auto item = [&](int jn, int jp, int part) {
       double q[3];
       if (rs) {
         q[0] = path_s[3 * (jp * 5)];
@@ -1152,6 +1154,21 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
         fr = SPLIT ? pose_free_part(P, q, wp, wpre, wc, wcl, part >> 1, part & 1) : pose_free(P, q, wp, wpre, wc, wcl, nw);
       }
       if (!fr) g_free[jn] = 0;  // every writer stores 0
+    };
+    constexpr bool PROBE = HA_SWEEP_PROBE && !RSH && !SPLIT;
+    if (PROBE && !rs && npose > 1) {  // block-uniform
+      for (int t = tid; t < nk; t += nthr)
+        if (g_ix[t] != 0 && g_free[t]) item(t, npose - 1, 0);
+      __syncthreads();
+    }
+    const int total = (rs ? npose : nk * npose) * parts;
+    for (int t = tid; t < total; t += nthr) {
+      const int tp = SPLIT ? t / parts : t, part = SPLIT ? t - tp * parts : 0;
+      const int jn = rs ? 0 : tp / npose, jp = rs ? tp : tp - jn * npose;
+      if (!rs && g_ix[jn] == 0) continue;  // Encode 0: skipped before the collision check (:406-408)
+      if (!g_free[jn]) continue;  // already colliding: block_collision_check stops at its first hit
+      if (PROBE && !rs && npose > 1 && jp == npose - 1) continue;  // (probed above)
+      item(jn, jp, part);
     }
   };
   double cb = 0.0;
