@@ -259,12 +259,18 @@ __device__ __forceinline__ void change_basis(const double* init, const double* t
 }
 
 // ------------------------------------------------------------- collision
+// The reference's two BLAS-dispatched products here round as Julia's OpenBLAS does (oracle/or_blas.h):
+// GetRectanglePts' R*pts is dgemm (2x2 * 2x5, K = 2: fma(a1, b1, a0*b0)) and SAT's
+// transpose(pts .- bg_pt)*normal_vec is dgemv 'T' on two rows (fma(m0, n0, m1*n1)).
+__device__ __forceinline__ double sat_dp(double mx, double my, double nx, double ny) {
+  return __builtin_fma(mx, nx, my * ny);
+}
 __device__ __forceinline__ void rect_pts(double ox, double oy, double c, double s, double l, double w, double* pts) {
   const double px[5] = {-l, -l, l, l, -l}, py[5] = {w, -w, -w, w, w};
 #pragma unroll
   for (int j = 0; j < 5; j++) {
-    pts[2 * j] = c * px[j] + (-s) * py[j] + ox;
-    pts[2 * j + 1] = s * px[j] + c * py[j] + oy;
+    pts[2 * j] = __builtin_fma(-s, py[j], c * px[j]) + ox;
+    pts[2 * j + 1] = __builtin_fma(c, py[j], s * px[j]) + oy;
   }
 }
 
@@ -278,8 +284,8 @@ __device__ __forceinline__ int sat(const double* base, const double* other) {
     double mnb = 0, mxb = 0, mno = 0, mxo = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const double db = (base[2 * j] - bx) * nx + (base[2 * j + 1] - by) * ny;
-      const double dq = (other[2 * j] - bx) * nx + (other[2 * j + 1] - by) * ny;
+      const double db = sat_dp(base[2 * j] - bx, base[2 * j + 1] - by, nx, ny);
+      const double dq = sat_dp(other[2 * j] - bx, other[2 * j + 1] - by, nx, ny);
       if (j == 0 || db < mnb) mnb = db;
       if (j == 0 || db > mxb) mxb = db;
       if (j == 0 || dq < mno) mno = dq;
@@ -299,7 +305,7 @@ __device__ __forceinline__ void sat_base_pre(const double* base, double* pre /* 
     const double nx = -vy, ny = vx;
     double mnb = 0, mxb = 0;
     for (int j = 0; j < 4; j++) {
-      const double db = (base[2 * j] - bx) * nx + (base[2 * j + 1] - by) * ny;
+      const double db = sat_dp(base[2 * j] - bx, base[2 * j + 1] - by, nx, ny);
       if (j == 0 || db < mnb) mnb = db;
       if (j == 0 || db > mxb) mxb = db;
     }
@@ -314,7 +320,7 @@ __device__ __forceinline__ int sat_pre(const double* pre, const double* other) {
     double mno = 0, mxo = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const double dq = (other[2 * j] - bx) * nx + (other[2 * j + 1] - by) * ny;
+      const double dq = sat_dp(other[2 * j] - bx, other[2 * j + 1] - by, nx, ny);
       if (j == 0 || dq < mno) mno = dq;
       if (j == 0 || dq > mxo) mxo = dq;
     }
@@ -336,7 +342,7 @@ __device__ __forceinline__ int sat_pre(const double* pre, const double* other) {
 constexpr int WT = 40;
 // The culls' margin argument (1e-6 m, and 1e-6·|n| along an edge normal n) against the rounding of the
 // computed projections: a projection fl((p - b)·n) of a computed corner p (|p|, |b| <= X, corner rounding
-// <= 3ε(X + L)) is within ~15ε(X + L)·|n| of the exact one.  ha_cull_ok enables the culls only when every
+// <= 3ε(X + L)) is within ~15ε(X + L)·|n| of the exact one (the FMA forms above round once less per term).  ha_cull_ok enables the culls only when every
 // input coordinate and length of the call (wall centres + extents, stbound, start, goal, minR, vehicle and
 // primitive sizes) is <= HA_CULL_MAX = 1e6 m; every swept pose then lies within ~10 HA_CULL_MAX of the
 // origin (a neighbour within expand_time of an in-bounds node, a Reeds-Shepp path within its length of
@@ -3641,8 +3647,8 @@ __device__ __forceinline__ void cubic_params(const double* cur, const double* nx
   mpj_pinv2(M, Pm);
   const double P0 = Pm[0], P1 = Pm[1], P2 = Pm[2], P3 = Pm[3];
   const double b0 = yg, b1 = mpj_tan(pg);
-  out[0] = P0 * b0 + P1 * b1;
-  out[1] = P2 * b0 + P3 * b1;
+  out[0] = __builtin_fma(P1, b1, P0 * b0);  // pinv(A)*B: BLAS dgemv 'N' 2x2 (oracle/or_blas.h)
+  out[1] = __builtin_fma(P3, b1, P2 * b0);
   out[2] = xg;
 }
 
@@ -3655,8 +3661,8 @@ __device__ __forceinline__ void cubic_point(const double* cur, const double* prm
   const double psi = mpj_atan((3 * prm[0]) * (x * x) + (2 * prm[1]) * x);
   double s0, c0;
   mpj_sincos(cur[2], &s0, &c0);
-  o[0] = (c0 * x + (-s0) * y) + cur[0];
-  o[1] = (s0 * x + c0 * y) + cur[1];
+  o[0] = __builtin_fma(-s0, y, c0 * x) + cur[0];  // Rmat*path: BLAS dgemm, K = 2 (oracle/or_blas.h)
+  o[1] = __builtin_fma(c0, y, s0 * x) + cur[1];
   o[2] = psi + cur[2];
 }
 
@@ -4078,17 +4084,16 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
 #ifndef HA_RS_WINNER
 #define HA_RS_WINNER 1
 #endif
-  // (A/B) MPGPU_HA_RS_FULL=1 (or -DHA_RS_WINNER=0): RS_connected always runs the 48-candidate search
-  static const bool rs_full = !HA_RS_WINNER || (getenv("MPGPU_HA_RS_FULL") && atoi(getenv("MPGPU_HA_RS_FULL")) == 1);
+  // (A/B build -DHA_RS_WINNER=0: RS_connected always runs the 48-candidate search)
+  constexpr bool rs_full = !HA_RS_WINNER;
   // the pose table (A.ptab): the neighbour sweeps' heading terms for every lattice heading -- regulated
   // headings are round(modπ(ψ)/res)·res, so m spans round(±π/res) (one spare step each side); the few
-  // microseconds of one launch per plan.  (A/B) MPGPU_HA_NOTAB=1: every sweep evaluates its sin/cos.
-  static const bool notab = getenv("MPGPU_HA_NOTAB") && atoi(getenv("MPGPU_HA_NOTAB")) == 1;
+  // microseconds of one launch per plan.
   {
     const double r = p->res[2];
     const int nsw = p->n_col > 5 ? (p->n_col - 1) / 5 + 1 : 1;
     const double lo = std::floor(-MPJ_PI / r) - 1, hi = std::ceil(MPJ_PI / r) + 1;
-    const bool ok = !notab && r > 0 && hi - lo < 4096;
+    const bool ok = r > 0 && hi - lo < 4096;
     const int mlo = ok ? (int)lo : 0, nm = ok ? (int)(hi - lo) + 1 : 0;
     const size_t n = (size_t)nm * np * nsw;
     double* tab = ok ? (double*)mp_ws(ctx, WS_IO10, sizeof(double) * 4 * n) : nullptr;
@@ -4119,16 +4124,11 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                        A.walls, wt);
     A.wtab = wt;
   }
-  // MPGPU_HA_SPLIT=1: the round-3 shape (ha_iter_kernel + ha_book_kernel per iteration), for A/B runs
-  static const bool split = getenv("MPGPU_HA_SPLIT") && atoi(getenv("MPGPU_HA_SPLIT")) == 1;
-  A.coherent = split ? 0 : 1;
-  // MPGPU_HA_NOSKIP=1: every neighbour group evaluates rs_heuristic (A/B of the Dict pre-check)
-  static const bool noskip = getenv("MPGPU_HA_NOSKIP") && atoi(getenv("MPGPU_HA_NOSKIP")) == 1;
-  A.dnid = noskip ? nullptr : Q.nid;
+  A.coherent = 1;
+  A.dnid = Q.nid;  // the Dict pre-check: groups skip rs_heuristic when no neighbour of theirs can use it
   A.dg = Q.g;
-  // (A/B, HA_DREC_CODE builds) MPGPU_HA_DREC=1: the groups' Dict records
-  static const bool drec_env = HA_DREC_CODE && getenv("MPGPU_HA_DREC") && atoi(getenv("MPGPU_HA_DREC")) == 1;
-  A.drec = drec_env ? (long long*)mp_ws(ctx, WS_HA4, sizeof(long long) * nB * np * HA_DREC) : nullptr;
+  // (A/B build -DHA_DREC_CODE=1) the groups' Dict records
+  A.drec = HA_DREC_CODE ? (long long*)mp_ws(ctx, WS_HA4, sizeof(long long) * nB * np * HA_DREC) : nullptr;
   A.dpos = Q.pos;
   A.df = Q.f;
   A.dseq = Q.seq;
@@ -4178,8 +4178,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // every scene's max_pops iterations).  (Round 1 fused the bookkeeping behind an agent-scope release
   // in every block -- an L2 write-back each -- and measured 67-90 ms vs 40 ms; ha_step_kernel hands
   // its records over with agent-coherent stores instead, so no block writes back its L2.)
-  // (A/B) MPGPU_HA_POLL_CH: iterations per live-count poll (default 16)
-  static const int CH = getenv("MPGPU_HA_POLL_CH") ? std::max(1, atoi(getenv("MPGPU_HA_POLL_CH"))) : 16;
+  constexpr int CH = 16;  // iterations per live-count poll
   constexpr int NCK = 4;
   int* hl = (int*)mp_pinned(ctx, sizeof(int) * NCK);
   if (!hl) return mp_fail(ctx, MP_ERR_NOMEM, "pinned allocation failed");
@@ -4189,18 +4188,17 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   const int per = 1 + (np + NBG - 1) / NBG, per_tail = 1 + (np + NBG_TAIL - 1) / NBG_TAIL;
   // the tail's rs_heuristic word units (ha_iter_body RSH): group g·4 + c holds neighbours 16g.. and word chunk
   // c, so there must be a group for every (16-neighbour set, chunk) -- n_prim mod 16 in {0, 13, 14, 15} with
-  // 4 neighbours per group (62: yes).  (A/B) MPGPU_HA_TAIL_RSH=0: the groups' own word search.
-  static const bool rsh_env = !getenv("MPGPU_HA_TAIL_RSH") || atoi(getenv("MPGPU_HA_TAIL_RSH")) != 0;
-  const bool tail_rsh = HA_TAIL_RSH && rsh_env && !split && NBG_TAIL == 4 && per_tail - 1 >= 4 * ((np + 15) / 16);
+  // 4 neighbours per group (62: yes); otherwise the groups' own word search.
+  const bool tail_rsh = HA_TAIL_RSH && NBG_TAIL == 4 && per_tail - 1 >= 4 * ((np + 15) / 16);
   A.hp_c = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * nB * np * 4 * 2);
   A.hp_i = (int*)mp_ws(ctx, WS_IO12, sizeof(int) * nB * np * 4 * 2);
   A.hp_t = (double*)mp_ws(ctx, WS_IO14, sizeof(double) * nB * np * 12 * 2);
-  // (A/B) MPGPU_HA_PIPE=0: the tail keeps ha_step_kernel (expansion, then the whole bookkeeping per launch)
-  static const bool pipe_env = !getenv("MPGPU_HA_PIPE") || atoi(getenv("MPGPU_HA_PIPE")) != 0;
-  const bool tail_pipe = tail_rsh && pipe_env;
+  const bool tail_pipe = tail_rsh;
   // the persistent tail (ha_persist_kernel): one cooperative launch for the rest of the search once every block
-  // of it fits the device at once; (A/B) MPGPU_HA_PERSIST=0 keeps one ha_pipe_kernel launch per iteration
-  static const bool persist_env = !getenv("MPGPU_HA_PERSIST") || atoi(getenv("MPGPU_HA_PERSIST")) != 0;
+  // of it fits the device at once.  Without cooperative launches (or when one is refused) the tail runs one
+  // ha_pipe_kernel launch per iteration; MPGPU_HA_PERSIST=0 selects that fallback (a test hook: the same
+  // results, tests/test_gpu_hastar.py runs it)
+  const bool persist_env = !getenv("MPGPU_HA_PERSIST") || atoi(getenv("MPGPU_HA_PERSIST")) != 0;
   int persist_cap = 0;
   // the persistent kernel's block: 12 waves (one per CU: 14 scenes per launch), 6 (two per CU: 28 scenes; the
   // groups' sweep on 3 waves beside the 3 word waves) or 4 (three per CU: 42 scenes; the sweep on one wave).
@@ -4208,14 +4206,12 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // (the tail then starts at 28 live scenes).  Measured: a lone scenario 18.7 / 18.9 / 20.4 us per iteration
   // with 12 / 6 / 4 (r05zg, r05zh); the 256-plan 24.0 ms with 6 or 4, 24.7 with 12; a 32-scene shard 16.4 ms with
   // 4 against 18.4-20.1 with 6, whose tail starts only at 28 live scenes, two blocks sharing each CU.
-  // (A/B) MPGPU_HA_PERSIST_HW=12 / 6 / 4 forces one.
-  static const int phw_env = getenv("MPGPU_HA_PERSIST_HW") ? atoi(getenv("MPGPU_HA_PERSIST_HW")) : 0;
   const int per_ps = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
   const void* pfn[3] = {reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
                         reinterpret_cast<const void*>(ha_persist_kernel<6, NBG_TAIL>),
                         reinterpret_cast<const void*>(ha_persist_kernel<4, NBG_TAIL>)};
   const int phws[3] = {HW_TAIL, 6, 4};
-  static int pcap[3] = {-1, -1, -1};  // co-resident blocks of each (0: no cooperative launch)
+  int* pcap = ctx->ha_pcap;  // co-resident blocks of each on this context's device (0: no cooperative launch)
   int phw = 6;
   const void* persist_fn = pfn[1];
   double* rs_path2 = nullptr;
@@ -4233,49 +4229,31 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       (void)hipGetLastError();
     }
     int v = 1;
-    if (phw_env == 12 || phw_env == 6 || phw_env == 4) {
-      v = phw_env == 12 ? 0 : phw_env == 6 ? 1 : 2;
-    } else {
-      for (int c = 0; c < 3; c++)
-        if (B * per_ps <= pcap[c]) { v = c; break; }
-    }
+    for (int c = 0; c < 3; c++)
+      if (B * per_ps <= pcap[c]) { v = c; break; }
     phw = phws[v];
     persist_fn = pfn[v];
     persist_cap = pcap[v];
-    if (getenv("MPGPU_HA_VERBOSE"))
-      fprintf(stderr, "ha_persist_kernel<%d>: %d blocks co-resident\n", phw, persist_cap);
     rs_path2 = (double*)mp_ws(ctx, WS_IO15, sizeof(double) * 2 * nB * MAXPATH * 3);
     rs_i2 = (int*)mp_ws(ctx, WS_IO16, sizeof(int) * 4 * nB);
     if (!rs_path2 || !rs_i2) return MP_ERR_NOMEM;
   }
   bool persisted = false;
+  bool piped_any = false;  // an ha_pipe_kernel launch ran: its bounded waits report through Q.err too
   // the pipelined launch's expansion blocks wait for their bookkeeping on a CU each: it pays only while the
-  // whole launch is resident at once (one 12-wave block per CU); (A/B) MPGPU_HA_PIPE_BLOCKS
-  const int pipe_blocks = getenv("MPGPU_HA_PIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_PIPE_BLOCKS")) : 256;
-  // the full-width shape pipelined the same way (ha_pipe_kernel<HW, NBG, false>: 6 four-wave blocks per scene)
-  // once its launch is resident at once (4 blocks per CU at HA_WPE_FULL = 4).  (A/B) MPGPU_HA_FPIPE_BLOCKS=1024;
-  // off by default: measured 0.4-0.9 ms slower per 256-plan (r05u/r05v), its bookkeeping publishes the pop
-  // ~10 us after its start, so pop + expansion is no shorter than expansion + the whole bookkeeping (~8 us)
-  const int fpipe_blocks = getenv("MPGPU_HA_FPIPE_BLOCKS") ? atoi(getenv("MPGPU_HA_FPIPE_BLOCKS")) : 0;
-  const int per_fpipe = 2 + (np + NBG - 1) / NBG;
-  int piped = 0;  // the format of the records the last launch left in E[it & 1]: 0 none, 1 full-width, 2 tail
-  // (A/B) MPGPU_HA_PRESCAN=1: the prescan block's PRE_K least entries merged into popfirst!.  Measured slower
-  // (r05j, lone 729-pop scenario: 26.6 vs 25.7 us per iteration): its PRE_K DPP rounds on 12 waves took ~6 us
-  // and the merge's readlane chains ~2.6 us, so the bookkeeping started later than it saved.  Off by default
-  // (the block then only marks its record stale and takes its ticket).
-  static const bool pre_env = getenv("MPGPU_HA_PRESCAN") && atoi(getenv("MPGPU_HA_PRESCAN")) == 1;
-  static const bool tuv_env = !getenv("MPGPU_HA_TUV") || atoi(getenv("MPGPU_HA_TUV")) != 0;
-  A.no_pre = !pre_env;
-  static const bool rs_last_env = !getenv("MPGPU_HA_RS_LAST") || atoi(getenv("MPGPU_HA_RS_LAST")) != 0;  // r05o: -0.2 ms
-  A.rs_last = rs_last_env;
-  A.no_tuv = !tuv_env;
-  static const bool ngr_env = !getenv("MPGPU_HA_NGR") || atoi(getenv("MPGPU_HA_NGR")) != 0;
-  A.ngr_pub = ngr_env;
-  // (A/B, MPGPU_HA_FULL_TUV=1) the full-width groups' winners' (t, u, v) too, so a node popped there also skips
-  // RS_connected's word evaluation (RS search phase 6-9 -> 1.2 us) -- neutral per plan (r05u: RS_connected is
-  // not the full-width chain) and 10 more spilled VGPRs, so off
-  static const bool ftuv_env = getenv("MPGPU_HA_FULL_TUV") && atoi(getenv("MPGPU_HA_FULL_TUV")) == 1;
-  A.full_tuv = HA_FULL_TUV_CODE && tuv_env && ftuv_env && !split;
+  // whole launch is resident at once (one 12-wave block per CU).  (Measured and removed: the full-width shape
+  // pipelined the same way, 0.4-0.9 ms slower per 256-plan, r05u/r05v: its bookkeeping publishes the pop ~10 us
+  // after its start, so pop + expansion is no shorter than expansion + the whole bookkeeping.)
+  constexpr int pipe_blocks = 256;
+  int piped = 0;  // the format of the records the last launch left in E[it & 1]: 0 none, 2 tail
+  // the prescan block only marks its record stale and takes its ticket (merging its PRE_K least entries into
+  // popfirst! measured slower, r05j: 26.6 vs 25.7 us per lone iteration)
+  A.no_pre = true;
+  A.rs_last = true;  // RS_connected blocks dispatched after the groups (r05o: -0.2 ms)
+  A.no_tuv = false;  // the tail stores the winners' (t, u, v): RS_connected rebuilds the commands from them
+  A.ngr_pub = true;  // the popped node handed over as tagged granules (r05zl)
+  // (A/B build -DHA_FULL_TUV_CODE=1) the full-width groups' winners' (t, u, v) too (neutral per plan, r05u)
+  A.full_tuv = HA_FULL_TUV_CODE;
   if (!A.hp_c || !A.hp_i || !A.hp_t) return MP_ERR_NOMEM;
   // iteration it >= 2 works on the compact list of scenes still live (written by the previous
   // bookkeeping launch, count on the device); the host sizes the grids by the last live count it has
@@ -4287,48 +4265,19 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
 #ifndef HA_MID_BLOCKS
 #define HA_MID_BLOCKS 512
 #endif
-  // (A/B) MPGPU_HA_TAIL_BLOCKS overrides the tail threshold; MPGPU_HA_MID_BLOCKS the middle shape's
-  // (HA_MID_HW-wave blocks, 16 neighbours each: 5 blocks per scene, once known * 5 fits in that many blocks;
-  // 0: off).  r05x: the 6-wave middle shape for 16..102 live scenes and the tail from 15 (its pipelined /
-  // persistent forms from 14) -- 256-plan 25.6 -> 24.9 ms, the largest strided / contiguous shard 21.0 ->
-  // 19.2 / 17.9 -> 17.6 ms (the 12-wave tail step from 30 live scenes, round 4's threshold, and no middle)
-  const int tail_blocks = getenv("MPGPU_HA_TAIL_BLOCKS") ? atoi(getenv("MPGPU_HA_TAIL_BLOCKS")) : HA_TAIL_BLOCKS;
-  const int mid_blocks = getenv("MPGPU_HA_MID_BLOCKS") ? atoi(getenv("MPGPU_HA_MID_BLOCKS")) : HA_MID_BLOCKS;
+  // the middle shape: HA_MID_HW-wave blocks, 16 neighbours each (5 blocks per scene), once known * 5 fits in
+  // HA_MID_BLOCKS blocks.  r05x: the 6-wave middle shape for 16..102 live scenes and the tail from 15 (its
+  // pipelined / persistent forms from 14) -- 256-plan 25.6 -> 24.9 ms, the largest strided / contiguous shard
+  // 21.0 -> 19.2 / 17.9 -> 17.6 ms (the 12-wave tail step from 30 live scenes, round 4's threshold, and no middle)
+  constexpr int tail_blocks = HA_TAIL_BLOCKS;
+  constexpr int mid_blocks = HA_MID_BLOCKS;
   int known = B;
   int chunk = 0, checked = 0;
   bool finished = false;
-  // (A/B, MPGPU_HA_MIRROR=1) the live-count mirror (ha_mirror): the host stays at most MIRROR_AHEAD launches
-  // ahead of the device and sizes each launch from the count of the latest one started, instead of a stream
-  // copy of the count every CH iterations read up to two chunks late.  Measured 1.1-1.4 ms slower per 256-plan
-  // (r05u/r05v): each launch's system-scope store to host memory delays its end, and the prompter shape
-  // switches gain nothing
-  static const bool mirror_env = getenv("MPGPU_HA_MIRROR") && atoi(getenv("MPGPU_HA_MIRROR")) == 1;
-  static const int mirror_ahead = getenv("MPGPU_HA_MIRROR_AHEAD") ? std::max(2, atoi(getenv("MPGPU_HA_MIRROR_AHEAD"))) : 6;
-  volatile unsigned long long* hm = nullptr;
+  // (Measured and removed: a live-count mirror in host memory written by every launch, 1.1-1.4 ms slower per
+  // 256-plan, r05u/r05v -- each launch's system-scope store delays its end.)
   A.mirror = nullptr;
-  if (mirror_env && !split) {
-    unsigned long long* dm = nullptr;
-    hm = mp_mapped(ctx, &dm);
-    if (hm) {
-      *hm = 0;
-      A.mirror = dm;
-    }
-  }
   for (int it = 1; it <= mp && !finished; it++) {
-    if (hm && it > 1) {  // the latest count the device has published; wait while too far ahead of it
-      unsigned long long v = *hm;
-      long long spins = 0;
-      while ((int)(v >> 32) < it - mirror_ahead) {
-        // a stream that has gone idle without reaching the iteration: a launch failed -- stop waiting
-        if ((++spins & 1023) == 0 && hipStreamQuery(ctx->stream) != hipErrorNotReady) break;
-        v = *hm;
-      }
-      const int mit = (int)(v >> 32), ml = (int)(v & 0xffffffffu);
-      if (mit >= 1) {
-        if (ml == 0) break;  // every search has ended
-        known = std::min(known, ml);
-      }
-    }
     A.scene_of = it == 1 ? nullptr : Q.lst + ((it - 1) & 1) * B;
     A.n_live = it == 1 ? nullptr : Q.live + (it - 1);
     A.n_active = known;
@@ -4336,19 +4285,15 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     A.node_rw = rs_full ? nullptr : Q.node_rw + (size_t)((it - 1) & 1) * B;
     A.node_tuv = Q.node_tuv + (size_t)((it - 1) & 1) * 3 * B;
     const bool tail = known * per_tail <= tail_blocks;
-    if (split) {
-      if (tail)
-        hipLaunchKernelGGL((ha_iter_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_tail)), dim3(64 * HW_TAIL),
-                           0, ctx->stream, D, A);
-      else
-        hipLaunchKernelGGL((ha_iter_kernel<HW, NBG>), dim3((unsigned)(known * per)), dim3(HT), 0, ctx->stream, D, A);
-      hipLaunchKernelGGL(ha_book_kernel, dim3((unsigned)known), dim3(BKT), 0, ctx->stream, D, Q, A, B, it);
-    } else if (tail_pipe && known * (2 + (np + NBG_TAIL - 1) / NBG_TAIL) <= persist_cap) {
+    if (tail_pipe && known * (2 + (np + NBG_TAIL - 1) / NBG_TAIL) <= persist_cap) {
       // the rest of the search in one cooperative launch, after the current nodes' expansion (bootstrap)
       const int per_pipe = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
-      if (piped != 2)
+      if (piped != 2) {
         hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL),
                            0, ctx->stream, D, Q, A, B, it, 1);
+        piped = 2;
+        piped_any = true;
+      }
       unsigned char* rs_ok2 = reinterpret_cast<unsigned char*>(rs_i2);
       int* rs_len2 = rs_i2 + 2 * nB;
       int it0 = it;
@@ -4361,8 +4306,13 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                                                 ctx->stream)
                    : hipLaunchKernel(persist_fn, dim3((unsigned)(known * per_pipe)), dim3(64 * phw), args, 0, ctx->stream);
       if (le != hipSuccess) {
-        cleanup();
-        return mp_fail(ctx, MP_ERR_HIP, "ha_persist_kernel launch failed");
+        // refused (e.g. the device's co-residency changed under this context): the per-iteration pipelined
+        // tail from this iteration on -- the bootstrap above already expanded the current nodes
+        (void)hipGetLastError();
+        persist_cap = 0;
+        pcap[0] = pcap[1] = pcap[2] = 0;
+        it--;
+        continue;
       }
       persisted = true;
       break;
@@ -4375,14 +4325,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       }
       hipLaunchKernelGGL((ha_pipe_kernel<HW_TAIL, NBG_TAIL>), dim3((unsigned)(known * per_pipe)), dim3(64 * HW_TAIL), 0,
                          ctx->stream, D, Q, A, B, it, 0);
-    } else if (!tail && tail_pipe && known * per_fpipe <= fpipe_blocks) {
-      if (piped != 1) {
-        hipLaunchKernelGGL((ha_pipe_kernel<HW, NBG, false>), dim3((unsigned)(known * per_fpipe)), dim3(HT), 0,
-                           ctx->stream, D, Q, A, B, it, 1);
-        piped = 1;
-      }
-      hipLaunchKernelGGL((ha_pipe_kernel<HW, NBG, false>), dim3((unsigned)(known * per_fpipe)), dim3(HT), 0,
-                         ctx->stream, D, Q, A, B, it, 0);
+      piped_any = true;
     } else if (tail) {
       piped = 0;
       if (tail_rsh)  // + the prescan block per scene
@@ -4401,13 +4344,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
                          ctx->stream, D, Q, A, B, it);
     }
     if (hipGetLastError() != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "ha kernel launch failed"); }
-    // (A/B, MPGPU_HA_NEAR_CH=n) near the persistent tail's threshold the live count read every n iterations, at
-    // most one chunk late, so the tail starts close to the iteration its count allows: measured 1 ms slower per
-    // 256-plan at n = 4 (r05zn: the copies' stream gaps and the shorter lead cost more than the earlier start)
-    static const int near_ch = getenv("MPGPU_HA_NEAR_CH") ? atoi(getenv("MPGPU_HA_NEAR_CH")) : 0;
-    const bool near = near_ch > 0 && persist_cap > 0 && known * per_ps <= 2 * persist_cap;
-    const int ch = near ? near_ch : CH;
-    if (!hm && (it % ch == 0 || it == mp)) {
+    // (Measured and removed: polling the live count every 4 iterations near the persistent tail's threshold,
+    // 1 ms slower per 256-plan, r05zn.)
+    if (it % CH == 0 || it == mp) {
       const int slot = chunk % NCK;
       if (hipMemcpyAsync(hl + slot, Q.live + it, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
           hipEventRecord(ev[slot], ctx->stream) != hipSuccess) {
@@ -4418,7 +4357,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       // poll finished chunks without blocking; block only when two chunks ahead
       while (checked < chunk) {
         const int cs = checked % NCK;
-        const bool must = chunk - checked > (near ? 1 : 2);
+        const bool must = chunk - checked > 2;
         const hipError_t q = must ? hipEventSynchronize(ev[cs]) : hipEventQuery(ev[cs]);
         if (q == hipErrorNotReady) break;
         if (q != hipSuccess) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "event wait failed"); }
@@ -4443,14 +4382,14 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       fclose(f);
     }
   }
-  if (persisted) {  // a bounded wait that ran out means the search is not trusted
+  if (persisted || piped_any) {  // a bounded wait (persistent or pipelined launch) that ran out: not trusted
     int err = 0;
     if (hipMemcpyAsync(&err, Q.err, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
         hipStreamSynchronize(ctx->stream) != hipSuccess) {
       cleanup();
       return mp_fail(ctx, MP_ERR_HIP, "persistent search failed");
     }
-    if (err) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "persistent search: a cross-block wait timed out"); }
+    if (err) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "Hybrid A* search: a cross-block wait timed out"); }
   }
   // outputs: per-scene counters, then the used prefix of pop_seq / states / RS paths
   std::vector<int> si(SI_N * nB);

@@ -584,441 +584,27 @@ __device__ __forceinline__ void pinv2(const double* M, double* Pm, int&) {
   else mpj_pinv2(M, Pm);
 }
 
-// Exchange a double with the other lane of the pair (DPP quad_perm [1,0,3,2]).
-__device__ __forceinline__ double dswap(double v) {
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
+// The products of ILQR.jl:56-66 and :76 are BLAS calls in Julia (lx, lu and hence Vx, Qx, Qu, k are
+// n x 1 matrices, GetMatrix.jl:6-7, so every Riccati product is dgemm; Klist * (xtilde .- xn) is dgemv
+// 'N'), and they round as OpenBLAS's FMA kernels do (oracle/or_blas.h, pinned against OpenBLAS 0.3.29):
+//   dgemm, K = 2 or 4: the fma chain from k = 0, acc = a0*b0, acc = fma(a_k, b_k, acc)
+//   dgemv 'N' 2x4:     fma(a0, x0, a1*x1) + fma(a2, x2, a3*x3)
+__device__ __forceinline__ double bk2(double a0, double b0, double a1, double b1) {
+  return __builtin_fma(a1, b1, a0 * b0);
+}
+__device__ __forceinline__ double bk4(double a0, double b0, double a1, double b1, double a2, double b2, double a3,
+                                      double b3) {
+  return __builtin_fma(a3, b3, __builtin_fma(a2, b2, __builtin_fma(a1, b1, a0 * b0)));
+}
+// row r of the knot's gain K ([4][2] column-major: K[r][c] = Kr[2c + r]) times dx
+__device__ __forceinline__ double kdx(const double* Kr, int r, const double* dx) {
+  return __builtin_fma(Kr[r], dx[0], Kr[2 + r] * dx[1]) + __builtin_fma(Kr[4 + r], dx[2], Kr[6 + r] * dx[3]);
 }
 
-// pinv2 on a lane pair: both lanes evaluate the whole (short, libm-free) LAPACK path.
-template <bool FT>
-__device__ __forceinline__ void pinv2_pair(const double* M, double* Pm, int, int& bad) { pinv2<FT>(M, Pm, bad); }
-
-// ILQR.jl:46-67 for instance b: one thread per instance (the sweep is a serial chain in j).
-// The derivative record of knot j-1 is loaded while knot j is processed (coalesced: the
-// records are component-major, instance fastest), so the chain never waits on memory.
 // LDS barrier between the compute wave and the loader wave of a staged block: LDS traffic
 // retired, no vmcnt wait (the compute wave's gain stores and the loader's in-flight record
 // loads stay outstanding across it), and a compiler barrier for memory.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-template <bool FT, bool STAGED = false, bool PP = false>
-__device__ __forceinline__ void backward_sweep(const IlqrDev& P, int B, int b, bool live, const double* X,
-                                               const double* D, double* kout, double* Kout, int& bad,
-                                               const double* lds = nullptr, int lane = 0, int side = 0) {
-  const int N = P.N;
-  const double e = P.eps;
-  const int V = P.variant;
-  const size_t ks = (size_t)ND * B;  // knot stride of the records
-  const double* Db = D + b;
-  double cur[ND];
-  if (!STAGED)
-#pragma unroll
-    for (int q = 0; q < ND; q++) cur[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
-  double Vx[4], Vxx[16];
-  {  // CalculateMatrix(StatesList[:, end], [0 0], TerminalCost): only lx, lxx are used
-    const double* xs = X + ((size_t)b * N + N - 1) * 4;
-    const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
-    double sp[4], sm[4], t1[4], t2[4], t3[4], t4[4];
-    const double c12 = 1 / (12 * (e * e)), c4 = 1 / (4 * (e * e));
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
-      sp[i] = s[i] + e;
-      sm[i] = s[i] - e;
-      Vx[i] = (terminal(V, sp) - terminal(V, sm)) / (2 * e);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) { t1[r] = s[r]; t2[r] = s[r]; t3[r] = s[r]; t4[r] = s[r]; }
-        if (i == j) {
-          t1[i] = s[i] + 2 * e; t2[i] = s[i] + e; t3[i] = s[i] - e; t4[i] = s[i] - 2 * e;
-          Vxx[4 * i + j] = c12 * (-terminal(V, t1) + 16 * terminal(V, t2) - 30 * terminal(V, s) +
-                                  16 * terminal(V, t3) - terminal(V, t4));
-        } else {
-          t1[i] = s[i] + e; t1[j] = s[j] + e;
-          t2[i] = s[i] - e; t2[j] = s[j] - e;
-          t3[i] = s[i] + e; t3[j] = s[j] - e;
-          t4[i] = s[i] - e; t4[j] = s[j] + e;
-          Vxx[4 * i + j] = c4 * (terminal(V, t1) + terminal(V, t2) - terminal(V, t3) - terminal(V, t4));
-        }
-      }
-  }
-  for (int j = N - 2, t = 0; j >= 0; j--, t++) {
-    double nxt[ND];
-    if (STAGED) {  // knot j's records, staged by the loader wave before barrier t
-      lds_barrier();
-      const double* bf = lds + (size_t)(t & 1) * ND * 64 + lane;
-#pragma unroll
-      for (int q = 0; q < ND; q++) cur[q] = bf[q * 64];
-    } else {
-      const size_t jn = j > 0 ? (size_t)(j - 1) : 0;
-#pragma unroll
-      for (int q = 0; q < ND; q++) nxt[q] = Db[jn * ks + (size_t)q * B];
-    }
-    const double* A = cur;        // [4][4]
-    const double* Bm = cur + 16;  // [4][2]
-    const double* lx = cur + 24;
-    const double* lu = cur + 28;
-    const double* lxx = cur + 30;
-    const double* luu = cur + 46;
-    const double* lux = cur + 50;
-    double Qx[4], Qu[2], Qxx[16], Quu[4], Qux[8], T44[16], T24[8], Pm[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      double acc = A[0 * 4 + i] * Vx[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vx[k];
-      Qx[i] = lx[i] + acc;
-    }
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      double acc = Bm[0 * 2 + i] * Vx[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vx[k];
-      Qu[i] = lu[i] + acc;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = A[0 * 4 + i] * Vxx[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vxx[k * 4 + c];
-        T44[4 * i + c] = acc;
-      }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = T44[4 * i + 0] * A[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + T44[4 * i + k] * A[k * 4 + c];
-        Qxx[4 * i + c] = lxx[4 * i + c] + acc;
-      }
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = Bm[0 * 2 + i] * Vxx[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vxx[k * 4 + c];
-        T24[4 * i + c] = acc;
-      }
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int c = 0; c < 2; c++) {
-        double acc = T24[4 * i + 0] * Bm[0 * 2 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * Bm[k * 2 + c];
-        Quu[2 * i + c] = luu[2 * i + c] + acc;
-      }
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = T24[4 * i + 0] * A[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * A[k * 4 + c];
-        Qux[4 * i + c] = lux[4 * i + c] + acc;
-      }
-    if (PP) pinv2_pair<FT>(Quu, Pm, side, bad);  // the lane pair splits the pinv's libm calls
-    else pinv2<FT>(Quu, Pm, bad);
-    double kk[2], KK[8];
-#pragma unroll
-    for (int i = 0; i < 2; i++) kk[i] = (-Pm[2 * i + 0]) * Qu[0] + (-Pm[2 * i + 1]) * Qu[1];
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) KK[4 * i + c] = (-Pm[2 * i + 0]) * Qux[0 * 4 + c] + (-Pm[2 * i + 1]) * Qux[1 * 4 + c];
-    if (live && side == 0) {
-      double* ko = kout + ((size_t)b * (N - 1) + j) * 2;
-      double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8;
-      ko[0] = kk[0];
-      ko[1] = kk[1];
-#pragma unroll
-      for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) Ko[2 * c + r] = KK[4 * r + c];
-    }
-    double qk[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++) qk[i] = Quu[2 * i + 0] * kk[0] + Quu[2 * i + 1] * kk[1];
-#pragma unroll
-    for (int i = 0; i < 4; i++) Vx[i] = Qx[i] - (KK[0 * 4 + i] * qk[0] + KK[1 * 4 + i] * qk[1]);
-    double KQ[8];
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int c = 0; c < 2; c++) KQ[2 * i + c] = KK[0 * 4 + i] * Quu[0 * 2 + c] + KK[1 * 4 + i] * Quu[1 * 2 + c];
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int c = 0; c < 4; c++)
-        Vxx[4 * i + c] = Qxx[4 * i + c] - (KQ[2 * i + 0] * KK[0 * 4 + c] + KQ[2 * i + 1] * KK[1 * 4 + c]);
-    if (!STAGED)
-#pragma unroll
-      for (int q = 0; q < ND; q++) cur[q] = nxt[q];
-  }
-}
-
-// The loader wave of a staged block: knot j's records (component-major, the 64 instances of
-// the block contiguous per component: coalesced 512-B loads) into LDS buffer t&1 before barrier
-// t, with knot j-1's loads already in flight across that barrier and the compute wave's step.
-__device__ __forceinline__ void record_loader(const IlqrDev& P, int B, int b, const double* D, double* lds,
-                                              int lane) {
-  const int N = P.N;
-  const size_t ks = (size_t)ND * B;
-  const double* Db = D + b;
-  double v[ND];
-#pragma unroll
-  for (int q = 0; q < ND; q++) v[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
-  for (int j = N - 2, t = 0; j >= 0; j--, t++) {
-    double* bf = lds + (size_t)(t & 1) * ND * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < ND; q++) bf[q * 64] = v[q];
-    if (j > 0) {
-#pragma unroll
-      for (int q = 0; q < ND; q++) v[q] = Db[(size_t)(j - 1) * ks + (size_t)q * B];
-    }
-    lds_barrier();
-  }
-}
-
-// ILQR.jl:46-67 on a LANE PAIR per instance (side = lane & 1): the pair splits every matrix
-// product by rows (4x4: rows 2s, 2s+1; 2x4: row s), the pinv, Qu and the stores, and swaps the
-// halves the next product needs (DPP): Quu, KK, Vx and Vxx each step.  Each entry is computed
-// by exactly the operations of backward_sweep (same order), so the gains are bit-identical;
-// a lane issues ~60 % of the single-lane sweep's instructions and 2x the waves run.
-template <bool FT>
-__device__ __forceinline__ void backward_sweep_pair(const IlqrDev& P, int B, int b, int side, bool live,
-                                                    const double* X, const double* D, double* kout, double* Kout,
-                                                    int& bad) {
-  const int N = P.N;
-  const double e = P.eps;
-  const int V = P.variant;
-  const size_t ks = (size_t)ND * B;
-  const double* Db = D + b;
-  double cur[ND];
-#pragma unroll
-  for (int q = 0; q < ND; q++) cur[q] = Db[(size_t)(N - 2) * ks + (size_t)q * B];
-  double Vx[4], Vxx[16];
-  {  // terminal FD (both lanes, once per sweep)
-    const double* xs = X + ((size_t)b * N + N - 1) * 4;
-    const double s[4] = {xs[0], xs[1], xs[2], xs[3]};
-    double sp[4], sm[4], t1[4], t2[4], t3[4], t4[4];
-    const double c12 = 1 / (12 * (e * e)), c4 = 1 / (4 * (e * e));
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) { sp[r] = s[r]; sm[r] = s[r]; }
-      sp[i] = s[i] + e;
-      sm[i] = s[i] - e;
-      Vx[i] = (terminal(V, sp) - terminal(V, sm)) / (2 * e);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-#pragma unroll
-        for (int r = 0; r < 4; r++) { t1[r] = s[r]; t2[r] = s[r]; t3[r] = s[r]; t4[r] = s[r]; }
-        if (i == j) {
-          t1[i] = s[i] + 2 * e; t2[i] = s[i] + e; t3[i] = s[i] - e; t4[i] = s[i] - 2 * e;
-          Vxx[4 * i + j] = c12 * (-terminal(V, t1) + 16 * terminal(V, t2) - 30 * terminal(V, s) +
-                                  16 * terminal(V, t3) - terminal(V, t4));
-        } else {
-          t1[i] = s[i] + e; t1[j] = s[j] + e;
-          t2[i] = s[i] - e; t2[j] = s[j] - e;
-          t3[i] = s[i] + e; t3[j] = s[j] - e;
-          t4[i] = s[i] - e; t4[j] = s[j] + e;
-          Vxx[4 * i + j] = c4 * (terminal(V, t1) + terminal(V, t2) - terminal(V, t3) - terminal(V, t4));
-        }
-      }
-  }
-  for (int j = N - 2; j >= 0; j--) {
-    double nxt[ND];
-    const size_t jn = j > 0 ? (size_t)(j - 1) : 0;
-#pragma unroll
-    for (int q = 0; q < ND; q++) nxt[q] = Db[jn * ks + (size_t)q * B];
-    const double* A = cur;
-    const double* Bm = cur + 16;
-    const double* lx = cur + 24;
-    const double* lu = cur + 28;
-    const double* lxx = cur + 30;
-    const double* luu = cur + 46;
-    const double* lux = cur + 50;
-    // own rows: i0 = 2*side, i0+1 of the 4-row products; row `side` of the 2-row ones
-    double Qx[2], Qxx[8], T44[8], T24[4], Qux_own[4], Quu_own[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int i = 2 * side + h;
-      double acc = A[0 * 4 + i] * Vx[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vx[k];
-      Qx[h] = lx[i] + acc;
-    }
-    double Qu[2];
-    {
-      const int i = side;
-      double acc = Bm[0 * 2 + i] * Vx[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vx[k];
-      const double q0 = lu[i] + acc, q1 = dswap(q0);
-      Qu[0] = side ? q1 : q0;
-      Qu[1] = side ? q0 : q1;
-    }
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int i = 2 * side + h;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = A[0 * 4 + i] * Vxx[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vxx[k * 4 + c];
-        T44[4 * h + c] = acc;
-      }
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = T44[4 * h + 0] * A[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + T44[4 * h + k] * A[k * 4 + c];
-        Qxx[4 * h + c] = lxx[4 * i + c] + acc;
-      }
-    }
-    {
-      const int i = side;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = Bm[0 * 2 + i] * Vxx[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + Bm[k * 2 + i] * Vxx[k * 4 + c];
-        T24[c] = acc;
-      }
-#pragma unroll
-      for (int c = 0; c < 2; c++) {
-        double acc = T24[0] * Bm[0 * 2 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + T24[k] * Bm[k * 2 + c];
-        Quu_own[c] = luu[2 * i + c] + acc;
-      }
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        double acc = T24[0] * A[0 * 4 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + T24[k] * A[k * 4 + c];
-        Qux_own[c] = lux[4 * i + c] + acc;
-      }
-    }
-    double Quu[4];
-    {
-      const double o0 = dswap(Quu_own[0]), o1 = dswap(Quu_own[1]);
-      Quu[0] = side ? o0 : Quu_own[0];
-      Quu[1] = side ? o1 : Quu_own[1];
-      Quu[2] = side ? Quu_own[0] : o0;
-      Quu[3] = side ? Quu_own[1] : o1;
-    }
-    double Pm[4];
-    pinv2_pair<FT>(Quu, Pm, side, bad);
-    double kk[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++) kk[i] = (-Pm[2 * i + 0]) * Qu[0] + (-Pm[2 * i + 1]) * Qu[1];
-    // KK row `side` needs both Qux rows: swap the own row, then the other half of KK
-    double KK[8];
-    {
-      double Qo[4];
-#pragma unroll
-      for (int c = 0; c < 4; c++) Qo[c] = dswap(Qux_own[c]);
-      const int i = side;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const double q0 = side ? Qo[c] : Qux_own[c], q1 = side ? Qux_own[c] : Qo[c];
-        const double kv = (-Pm[2 * i + 0]) * q0 + (-Pm[2 * i + 1]) * q1;
-        const double ko = dswap(kv);
-        KK[0 * 4 + c] = side ? ko : kv;
-        KK[1 * 4 + c] = side ? kv : ko;
-      }
-    }
-    if (live) {
-      double* ko = kout + ((size_t)b * (N - 1) + j) * 2;
-      double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8;
-      ko[side] = kk[side];
-#pragma unroll
-      for (int c = 0; c < 4; c++) Ko[2 * c + side] = KK[4 * side + c];
-    }
-    double qk[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++) qk[i] = Quu[2 * i + 0] * kk[0] + Quu[2 * i + 1] * kk[1];
-    double vx[2], vxx[8];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int i = 2 * side + h;
-      vx[h] = Qx[h] - (KK[0 * 4 + i] * qk[0] + KK[1 * 4 + i] * qk[1]);
-      double KQ[2];
-#pragma unroll
-      for (int c = 0; c < 2; c++) KQ[c] = KK[0 * 4 + i] * Quu[0 * 2 + c] + KK[1 * 4 + i] * Quu[1 * 2 + c];
-#pragma unroll
-      for (int c = 0; c < 4; c++) vxx[4 * h + c] = Qxx[4 * h + c] - (KQ[0] * KK[0 * 4 + c] + KQ[1] * KK[1 * 4 + c]);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const double o = dswap(vx[h]);
-      Vx[h] = side ? o : vx[h];
-      Vx[2 + h] = side ? vx[h] : o;
-    }
-#pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const double o = dswap(vxx[q]);
-      Vxx[q] = side ? o : vxx[q];
-      Vxx[8 + q] = side ? vxx[q] : o;
-    }
-#pragma unroll
-    for (int q = 0; q < ND; q++) cur[q] = nxt[q];
-  }
-}
-
-// Riccati sweep with LDS-staged records (default): block = compute wave + loader wave for 64
-// instances.  The single-wave sweep spent ~2 us of its ~3.6 us per knot waiting on the knot's
-// 58 record loads (the compiler sinks prefetches to cut register pressure); here the compute
-// wave reads them from LDS and the loader wave keeps the next knot's loads in flight.
-template <int LANES>
-__global__ __launch_bounds__(64 * (LANES + 1)) void ilqr_backward_staged_kernel(IlqrDev P, int B, const double* X,
-                                                                               const double* D, const int* list,
-                                                                               const int* n_dev, int nmax, double* kout,
-                                                                               double* Kout) {
-  extern __shared__ double recs[];  // [2][ND][64]
-  __shared__ int sh_redo;
-  const int tid = threadIdx.x;
-  const bool loader = tid >= 64 * LANES;  // the last wave
-  const int il = loader ? tid - 64 * LANES : tid / LANES;  // instance within the block's 64
-  const int side = LANES == 2 ? (tid & 1) : 0;
-  const int n = n_dev ? *n_dev : nmax;
-  if ((int)blockIdx.x * 64 >= n) return;  // block-uniform: the grid covers nmax >= n
-  const int i0 = blockIdx.x * 64 + il;  // record column (compact index with a list)
-  const bool live = i0 < n;
-  const int i = live ? i0 : n - 1;       // dead lanes recompute the last one and store nothing
-  const int b = list ? list[i] : i;
-  if (tid == 0) sh_redo = 0;  // read only after the sweep's barriers
-  if (loader) {
-    record_loader(P, B, i, D, recs, il);
-    lds_barrier();  // the compute waves' redo decision
-    if (kFastBwd && kRedo && sh_redo) record_loader(P, B, i, D, recs, il);
-    return;
-  }
-  int bad = 0;
-  backward_sweep<kFastBwd, true, LANES == 2>(P, B, b, live, X, D, kout, Kout, bad, recs, il, side);
-  if (kFastBwd && kRedo && __any(bad) && (tid & 63) == 0) sh_redo = 1;  // any compute wave
-  lds_barrier();  // matches the loader's redo-decision barrier
-  if (sh_redo) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
-    int d = 0;
-    backward_sweep<false, true, LANES == 2>(P, B, b, live, X, D, kout, Kout, d, recs, il, side);
-  }
-}
 
 // Broadcast lane k of each lane quad to the quad (DPP quad_perm [k,k,k,k], one VALU op per half).
 template <int K>
@@ -1115,82 +701,46 @@ __device__ __forceinline__ void backward_sweep_quad(const IlqrDev& P, int b, boo
     for (int c = 0; c < 4; c++) luu[c] = bf[(46 + c) * IPB];
     const double lux0q = bf[(50 + q) * IPB], lux1q = bf[(54 + q) * IPB];
     // Qx[q] = lx[q] + fx' * Vx  (own entry)
-    double Qxq;
-    {
-      double acc = Acol[0] * Vx[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) acc = acc + Acol[k] * Vx[k];
-      Qxq = lxq + acc;
-    }
-    double Qu[2];  // every lane
-    {
-      double a0 = Bm[0 * 2 + 0] * Vx[0], a1 = Bm[0 * 2 + 1] * Vx[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) {
-        a0 = a0 + Bm[k * 2 + 0] * Vx[k];
-        a1 = a1 + Bm[k * 2 + 1] * Vx[k];
-      }
-      Qu[0] = lu0 + a0;
-      Qu[1] = lu1 + a1;
-    }
+    // every product is dgemm in Julia: bk4 / bk2 (the fma chain from k = 0)
+    const double Qxq = lxq + bk4(Acol[0], Vx[0], Acol[1], Vx[1], Acol[2], Vx[2], Acol[3], Vx[3]);  // lx + fx' * Vx
+    double Qu[2];  // every lane: lu + fu' * Vx
+    Qu[0] = lu0 + bk4(Bm[0], Vx[0], Bm[2], Vx[1], Bm[4], Vx[2], Bm[6], Vx[3]);
+    Qu[1] = lu1 + bk4(Bm[1], Vx[0], Bm[3], Vx[1], Bm[5], Vx[2], Bm[7], Vx[3]);
     // T24 column q = (fu' Vxx)[:, q], gathered to the full 2x4
     double T24[8];
     {
-      double c0 = Bm[0 * 2 + 0] * Vcol[0], c1 = Bm[0 * 2 + 1] * Vcol[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) {
-        c0 = c0 + Bm[k * 2 + 0] * Vcol[k];
-        c1 = c1 + Bm[k * 2 + 1] * Vcol[k];
-      }
+      const double c0 = bk4(Bm[0], Vcol[0], Bm[2], Vcol[1], Bm[4], Vcol[2], Bm[6], Vcol[3]);
+      const double c1 = bk4(Bm[1], Vcol[0], Bm[3], Vcol[1], Bm[5], Vcol[2], Bm[7], Vcol[3]);
       qgather(c0, T24);
       qgather(c1, T24 + 4);
     }
     // T44 row q = (fx' Vxx)[q, :], Qxx row q = lxx[q, :] + T44[q, :] fx  (own)
     double T44q[4], Qxxq[4];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      double acc = Acol[0] * Vxx[0 * 4 + c];
+    for (int c = 0; c < 4; c++)
+      T44q[c] = bk4(Acol[0], Vxx[c], Acol[1], Vxx[4 + c], Acol[2], Vxx[8 + c], Acol[3], Vxx[12 + c]);
 #pragma unroll
-      for (int k = 1; k < 4; k++) acc = acc + Acol[k] * Vxx[k * 4 + c];
-      T44q[c] = acc;
-    }
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      double acc = T44q[0] * A[0 * 4 + c];
-#pragma unroll
-      for (int k = 1; k < 4; k++) acc = acc + T44q[k] * A[k * 4 + c];
-      Qxxq[c] = lxxq[c] + acc;
-    }
+    for (int c = 0; c < 4; c++)
+      Qxxq[c] = lxxq[c] + bk4(T44q[0], A[c], T44q[1], A[4 + c], T44q[2], A[8 + c], T44q[3], A[12 + c]);
     // Quu (every lane), Qux column q (own)
     double Quu[4];
 #pragma unroll
     for (int i = 0; i < 2; i++)
 #pragma unroll
-      for (int c = 0; c < 2; c++) {
-        double acc = T24[4 * i + 0] * Bm[0 * 2 + c];
-#pragma unroll
-        for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * Bm[k * 2 + c];
-        Quu[2 * i + c] = luu[2 * i + c] + acc;
-      }
+      for (int c = 0; c < 2; c++)
+        Quu[2 * i + c] = luu[2 * i + c] + bk4(T24[4 * i], Bm[c], T24[4 * i + 1], Bm[2 + c], T24[4 * i + 2], Bm[4 + c],
+                                              T24[4 * i + 3], Bm[6 + c]);
     double Quxq[2];
-    {
-      double a0 = T24[0] * Acol[0], a1 = T24[4] * Acol[0];
-#pragma unroll
-      for (int k = 1; k < 4; k++) {
-        a0 = a0 + T24[k] * Acol[k];
-        a1 = a1 + T24[4 + k] * Acol[k];
-      }
-      Quxq[0] = lux0q + a0;
-      Quxq[1] = lux1q + a1;
-    }
+    Quxq[0] = lux0q + bk4(T24[0], Acol[0], T24[1], Acol[1], T24[2], Acol[2], T24[3], Acol[3]);
+    Quxq[1] = lux1q + bk4(T24[4], Acol[0], T24[5], Acol[1], T24[6], Acol[2], T24[7], Acol[3]);
     double Pm[4];
     int bad = 0;
     pinv2<true>(Quu, Pm, bad);
     double kk[2], KKq[2];
 #pragma unroll
-    for (int i = 0; i < 2; i++) kk[i] = (-Pm[2 * i + 0]) * Qu[0] + (-Pm[2 * i + 1]) * Qu[1];
+    for (int i = 0; i < 2; i++) kk[i] = bk2(-Pm[2 * i + 0], Qu[0], -Pm[2 * i + 1], Qu[1]);
 #pragma unroll
-    for (int i = 0; i < 2; i++) KKq[i] = (-Pm[2 * i + 0]) * Quxq[0] + (-Pm[2 * i + 1]) * Quxq[1];
+    for (int i = 0; i < 2; i++) KKq[i] = bk2(-Pm[2 * i + 0], Quxq[0], -Pm[2 * i + 1], Quxq[1]);
     if (live) {
       if (q < 2) kout[((size_t)b * (N - 1) + j) * 2 + q] = q == 0 ? kk[0] : kk[1];
       double* Ko = Kout + ((size_t)b * (N - 1) + j) * 8 + 2 * q;  // Klist[:, :, j] column q = (KK[0][q], KK[1][q])
@@ -1199,17 +749,17 @@ __device__ __forceinline__ void backward_sweep_quad(const IlqrDev& P, int b, boo
     }
     double qk[2];
 #pragma unroll
-    for (int i = 0; i < 2; i++) qk[i] = Quu[2 * i + 0] * kk[0] + Quu[2 * i + 1] * kk[1];
-    const double vxq = Qxq - (KKq[0] * qk[0] + KKq[1] * qk[1]);
-    double KQ[2];
+    for (int i = 0; i < 2; i++) qk[i] = bk2(Quu[2 * i + 0], kk[0], Quu[2 * i + 1], kk[1]);  // Quu * k
+    const double vxq = Qxq - bk2(KKq[0], qk[0], KKq[1], qk[1]);                                // K' * (Quu k)
+    double KQ[2];  // (K' * Quu)[q, :]
 #pragma unroll
-    for (int c = 0; c < 2; c++) KQ[c] = KKq[0] * Quu[0 * 2 + c] + KKq[1] * Quu[1 * 2 + c];
+    for (int c = 0; c < 2; c++) KQ[c] = bk2(KKq[0], Quu[0 * 2 + c], KKq[1], Quu[1 * 2 + c]);
     double KK0[4], KK1[4];
     qgather(KKq[0], KK0);
     qgather(KKq[1], KK1);
     double vxxq[4];
 #pragma unroll
-    for (int c = 0; c < 4; c++) vxxq[c] = Qxxq[c] - (KQ[0] * KK0[c] + KQ[1] * KK1[c]);
+    for (int c = 0; c < 4; c++) vxxq[c] = Qxxq[c] - bk2(KQ[0], KK0[c], KQ[1], KK1[c]);
     qgather(vxq, Vx);
 #pragma unroll
     for (int c = 0; c < 4; c++) {
@@ -1431,41 +981,6 @@ __global__ __launch_bounds__(64 * (1 + kFusedDW)) void ilqr_backward_fused_kerne
                                 live ? inst : (n - 1 - col0), q);
 }
 
-// Compute lanes per instance.  Round 2 ran two (the whole sweep on both, the closed-form pinv's
-// sqrt / atan2 / sincos / reciprocal pairs split over the pair: 247 vs 294 us for one lane); the
-// LAPACK pinv has no libm pairs to split, so one lane per instance is the default now and
-// -DMP_ILQR_PAIRPINV builds the pair (both lanes then run the identical pinv).
-#if defined(MP_ILQR_PAIRPINV)
-constexpr int kBwdStagedLanes = 2;
-#else
-constexpr int kBwdStagedLanes = 1;
-#endif
-
-#if defined(MP_ILQR_PAIR)  // A/B build: a lane pair per instance (measured slower: 391 vs 354 us)
-constexpr int kBwdLanes = 2;
-#else
-constexpr int kBwdLanes = 1;
-#endif
-__global__ __launch_bounds__(64) void ilqr_backward_kernel(IlqrDev P, int B, const double* X, const double* D,
-                                                           const int* active, double* kout, double* Kout) {
-  // kBwdLanes = 2: a lane pair per instance (32 instances per wave).  Every lane stays active
-  // (the straight-line libm selects with wave ballots, the pair swaps are DPP): lanes past B or
-  // of converged instances recompute a live instance's sweep and store nothing
-  const int b0 = blockIdx.x * (64 / kBwdLanes) + (int)threadIdx.x / kBwdLanes;
-  const int side = kBwdLanes == 2 ? (threadIdx.x & 1) : 0;
-  const bool live = b0 < B && (!active || active[b0]);
-  if (__all(!live)) return;
-  const int b = b0 < B ? b0 : B - 1;
-  int bad = 0;
-  if (kBwdLanes == 2) backward_sweep_pair<kFastBwd>(P, B, b, side, live, X, D, kout, Kout, bad);
-  else backward_sweep<kFastBwd>(P, B, b, live, X, D, kout, Kout, bad);
-  if (kFastBwd && kRedo && __any(bad)) {  // a lane left a straight-line core's range: redo the sweep with the exact libm
-    int d = 0;
-    if (kBwdLanes == 2) backward_sweep_pair<false>(P, B, b, side, live, X, D, kout, Kout, d);
-    else backward_sweep<false>(P, B, b, live, X, D, kout, Kout, d);
-  }
-}
-
 // ILQR.jl:72-80: one closed-loop roll out at step size alpha; returns TotalCost.  (Staging the
 // per-knot inputs through LDS as the Riccati sweep does measured no gain here, 371 vs 365 us: the
 // one-knot-ahead prefetch already covers the loads under the knot's ~8k-cycle RK4 chain.)  The rolled
@@ -1501,12 +1016,7 @@ __device__ double forward_trial(const IlqrDev& P, const double* X, const double*
 #pragma unroll
     for (int r = 0; r < 4; r++) dx[r] = x[r] - xr[r];
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-      double acc = Kr[2 * 0 + r] * dx[0];
-#pragma unroll
-      for (int c = 1; c < 4; c++) acc = acc + Kr[2 * c + r] * dx[c];
-      u[r] = (ur[r] + alpha * kr[r]) + acc;
-    }
+    for (int r = 0; r < 2; r++) u[r] = (ur[r] + alpha * kr[r]) + kdx(Kr, r, dx);  // Klist * (xtilde .- xn): dgemv
     if (wr) {
       Un[2 * i] = u[0];
       Un[2 * i + 1] = u[1];
@@ -1586,12 +1096,7 @@ __device__ double forward_trial_quad(const IlqrDev& P, const double* X, const do
 #pragma unroll
     for (int r = 0; r < 4; r++) dx[r] = x[r] - xr[r];
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-      double acc = Kr[2 * 0 + r] * dx[0];
-#pragma unroll
-      for (int c = 1; c < 4; c++) acc = acc + Kr[2 * c + r] * dx[c];
-      u[r] = (ur[r] + alpha * kr[r]) + acc;
-    }
+    for (int r = 0; r < 2; r++) u[r] = (ur[r] + alpha * kr[r]) + kdx(Kr, r, dx);  // Klist * (xtilde .- xn): dgemv
     if ((i & 3) == sub) {
       su[0] = u[0];
       su[1] = u[1];
@@ -1722,12 +1227,7 @@ __device__ double forward_trial_pair(const IlqrDev& P, const double* X, const do
 #pragma unroll
     for (int r = 0; r < 4; r++) dx[r] = x[r] - xr[r];
 #pragma unroll
-    for (int r = 0; r < 2; r++) {
-      double acc = Kr[2 * 0 + r] * dx[0];
-#pragma unroll
-      for (int c = 1; c < 4; c++) acc = acc + Kr[2 * c + r] * dx[c];
-      u[r] = (ur[r] + alpha * kr[r]) + acc;
-    }
+    for (int r = 0; r < 2; r++) u[r] = (ur[r] + alpha * kr[r]) + kdx(Kr, r, dx);  // Klist * (xtilde .- xn): dgemv
     if (((i & 3) >> 1) == sub) {
       su[i & 1][0] = u[0];
       su[i & 1][1] = u[1];
@@ -2201,21 +1701,13 @@ int make_ilqr(mp_ctx* ctx, const mp_ilqr_params* p, int B, IlqrDev* D) {
 // for na), or nullptr/nullptr/B for all.
 int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const double* dU, const int* list,
                  const int* n_dev, int na, double* dk, double* dK) {
-#if defined(MP_ILQR_UNSTAGED) || defined(MP_ILQR_PAIR)
-  list = nullptr;  // A/B builds: the unstaged sweeps index records by instance; all B run
-  n_dev = nullptr;
-  na = B;
-#endif
   const size_t n = (size_t)na * (D.N - 1);
-#if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR) && !defined(MP_ILQR_STAGED)
   // derivatives + sweep in one launch (ilqr_backward_fused_kernel) while more than kDeriv4Max instances
-  // are active; MPGPU_ILQR_FUSED=0: always the two-kernel path, =2: always fused.  A fused block makes
-  // the records of its 16 instances on its own CU, so with few blocks (the solve's tail) the derivative
-  // work, spread over the whole chip by ilqr_deriv4_kernel, is confined to a few CUs: measured 252 us per
-  // fused launch over a whole solve vs 32 + 180 us split, and 210 vs 108 + 180 us at full activity
-  // (profiles/r04_ilqr_fused_ab.txt)
-  static const int fused_mode = getenv("MPGPU_ILQR_FUSED") ? atoi(getenv("MPGPU_ILQR_FUSED")) : 1;
-  if (fused_mode == 2 || (fused_mode == 1 && na > kDeriv4Max)) {
+  // are active.  A fused block makes the records of its 16 instances on its own CU, so with few blocks (the
+  // solve's tail) the derivative work, spread over the whole chip by ilqr_deriv4_kernel, is confined to a
+  // few CUs: measured 252 us per fused launch over a whole solve vs 32 + 180 us split, and 210 vs 108 +
+  // 180 us at full activity (profiles/r04_ilqr_fused_ab.txt)
+  if (na > kDeriv4Max) {
     if (!ctx->ilqr_fused_attr) {
       MP_HIP(ctx, hipSetDevice(ctx->device));
       MP_HIP(ctx, hipFuncSetAttribute((const void*)ilqr_backward_fused_kernel,
@@ -2229,7 +1721,6 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
     mp_time_end(ctx);
     return MP_OK;
   }
-#endif
   double* dD = (double*)mp_ws(ctx, WS_ILQR0, sizeof(double) * (size_t)B * (D.N - 1) * ND);  // knot stride ND*B
   if (!dD) return MP_ERR_NOMEM;
   mp_time_begin(ctx);  // the timed region covers both kernels of the backward pass
@@ -2240,18 +1731,8 @@ int run_backward(mp_ctx* ctx, const IlqrDev& D, int B, const double* dX, const d
     hipLaunchKernelGGL(ilqr_deriv_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, D, B, dX, dU,
                        list, n_dev, na, dD);
   MP_HIP(ctx, hipGetLastError());
-#if !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR) && !defined(MP_ILQR_STAGED)
   hipLaunchKernelGGL(ilqr_backward_quad_kernel, dim3((na + kQuadIPB - 1) / kQuadIPB), dim3(128),
                      sizeof(double) * 2 * ND * kQuadIPB, ctx->stream, D, B, dX, dD, list, n_dev, na, dk, dK);
-#elif !defined(MP_ILQR_UNSTAGED) && !defined(MP_ILQR_PAIR)
-  hipLaunchKernelGGL(ilqr_backward_staged_kernel<kBwdStagedLanes>, dim3((na + 63) / 64),
-                     dim3(64 * (kBwdStagedLanes + 1)), sizeof(double) * 2 * ND * 64, ctx->stream, D, B, dX, dD,
-                     list, n_dev, na, dk, dK);
-#else
-  const int ipb = 64 / kBwdLanes;  // instances per 64-thread block
-  hipLaunchKernelGGL(ilqr_backward_kernel, dim3((B + ipb - 1) / ipb), dim3(64), 0, ctx->stream, D, B, dX, dD, nullptr,
-                     dk, dK);
-#endif
   MP_HIP(ctx, hipGetLastError());
   mp_time_end(ctx);
   return MP_OK;
@@ -2451,14 +1932,11 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   // hn[2q] = instances left pending by the pipelined round 0 (their rest pass runs in the next
   // launch, then they rejoin the list), hn[2q + 1] = the list count: their sum bounds the next list
   // the counts come from host memory the next backward pass's first kernel writes (ilqr_mirror) instead of a
-  // stream copy + event per iteration: 0.3-0.5 ms per 4096-instance solve (r05zd); (A/B) MPGPU_ILQR_MIRROR=0
-  static const bool imirror_env = !getenv("MPGPU_ILQR_MIRROR") || atoi(getenv("MPGPU_ILQR_MIRROR")) != 0;
-  volatile unsigned long long* hmr = nullptr;
+  // stream copy + event per iteration: 0.3-0.5 ms per 4096-instance solve (r05zd); the copy + event poll
+  // remains for a context without mapped host memory
   unsigned long long* dmr = nullptr;
-  if (imirror_env) {
-    hmr = mp_mapped(ctx, &dmr);
-    if (hmr) hmr[0] = hmr[1] = 0;
-  }
+  volatile unsigned long long* hmr = mp_mapped(ctx, &dmr);
+  if (hmr) hmr[0] = hmr[1] = 0;
   auto poll = [&](int outer, bool* stop) -> int {
     *stop = false;
     if (hmr) {  // the counts of iteration outer - 1's search, reported by this iteration's backward pass
@@ -2467,8 +1945,17 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
       unsigned long long a = hmr[0], pd = hmr[1];  // (each word carries its seq: no order between them)
       long long spins = 0;
       while ((a >> 32) < want || (pd >> 32) < want) {
-        if ((++spins & 1023) == 0 && hipStreamQuery(ctx->stream) != hipErrorNotReady)
-          return mp_fail(ctx, MP_ERR_HIP, "iLQR count mirror never arrived");
+        if ((++spins & 1023) == 0) {
+          const hipError_t q = hipStreamQuery(ctx->stream);
+          if (q != hipErrorNotReady) {
+            // the stream is idle (or failed): the kernel's stores are visible now, so one more read decides
+            a = hmr[0];
+            pd = hmr[1];
+            if ((a >> 32) >= want && (pd >> 32) >= want) break;
+            if (q != hipSuccess) return mp_fail(ctx, MP_ERR_HIP, "iLQR solve stream failed: %s", hipGetErrorString(q));
+            return mp_fail(ctx, MP_ERR_HIP, "iLQR count mirror never arrived");
+          }
+        }
         a = hmr[0];
         pd = hmr[1];
       }
@@ -2498,13 +1985,11 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   // (an instance in a rest pass sits one launch out, so the pipelined loop may take more launches
   // than max_iter + 2; each instance still stops at its own max_iter)
   bool w_zeroed = true;  // this iteration's list buffer's counts are zero (initially: the memsets above)
-  // (A/B) MPGPU_ILQR_MEMSET=1: a memset launch per iteration instead of the finish kernel's zeroing
-  static const bool memset_env = getenv("MPGPU_ILQR_MEMSET") && atoi(getenv("MPGPU_ILQR_MEMSET")) == 1;
   for (int outer = 0; outer <= 2 * (D.max_iter + 2); outer++) {
     int* rd = par[(outer + 1) & 1];  // the list the previous iteration wrote (or the init kernel)
     dnp = par[outer & 1];
     dn = dnp + 1;
-    int* zn = memset_env ? nullptr : rd;  // zeroed by this iteration's finish kernel, for the next iteration
+    int* zn = rd;  // zeroed by this iteration's finish kernel, for the next iteration
     // the derivative and sweep launches cover the active instances only (compact list)
     IlqrDev Dm = D;  // (the mirror: the previous iteration's counts, seq = outer; 0 = none yet)
     if (hmr && outer > 0) {

@@ -933,16 +933,15 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   // interleaved in a lane, costs evaluated once) 0.536 ms vs LPR 2 (4 waves/SIMD) 0.703 ms;
   // 8 scenes, LPR 1 (1 wave/SIMD) 0.384 ms vs LPR 2 (2 waves/SIMD) 0.375 ms: a lone wave
   // cannot cover the fp64 dependency latency.
-  const char* lpr_s = getenv("MPGPU_LPR");  // 1 / 2 forces the layout (tests, comparisons)
+  // (test hook) MPGPU_LPR = 1 / 2 forces the layout: the results are the same bits either way
+  // (tests/test_gpu_mppi_lane.py), only the launch shape changes
+  const char* lpr_s = getenv("MPGPU_LPR");
   const int lpr_env = lpr_s ? atoi(lpr_s) : 0;
   const int LPR = lpr_env == 1 || lpr_env == 2 ? lpr_env : ((size_t)S * K >= 131072 ? 1 : 2);
-  int BT = LPR == 1 ? ((size_t)S * ((K + 511) / 512) >= 256 ? 512 : 256)
-                    : ((size_t)S * ((K + 255) / 256) >= 256 ? 512 : 256);
-  // MPGPU_BT = 128 / 256 / 512 forces the block size (A/B runs).  Single scene (64 blocks):
-  // BT 128 (2 waves per CU on 128 CUs) 0.278 ms vs BT 256 (4 waves, one per SIMD, on 64 CUs)
-  // 0.242 ms -- a CU's four SIMDs each holding one wave beat half-filled CUs.
-  const char* bt_s = getenv("MPGPU_BT");
-  if (bt_s && (atoi(bt_s) == 128 || atoi(bt_s) == 256 || atoi(bt_s) == 512)) BT = atoi(bt_s);
+  // Single scene (64 blocks): BT 128 (2 waves per CU on 128 CUs) 0.278 ms vs BT 256 (4 waves, one per
+  // SIMD, on 64 CUs) 0.242 ms -- a CU's four SIMDs each holding one wave beat half-filled CUs.
+  const int BT = LPR == 1 ? ((size_t)S * ((K + 511) / 512) >= 256 ? 512 : 256)
+                          : ((size_t)S * ((K + 255) / 256) >= 256 ? 512 : 256);
   const int RPBh = BT / LPR;
   const int nb = (K + RPBh - 1) / RPBh;
   const int pstride = 4 + 2 * H;
@@ -950,8 +949,7 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   A.live = live;
   A.X0 = X0; A.goal = goal; A.unom = U_nom; A.obs = D.n_obs > 0 ? obstacles : nullptr;
   A.grid = D.gnx > 0 ? grid : nullptr;
-  static const bool noise_pass = getenv("MPGPU_NOISE_PASS") != nullptr;
-  A.inline_noise = D.noise_mode == MP_NOISE_PHILOX && !noise_pass;
+  A.inline_noise = D.noise_mode == MP_NOISE_PHILOX;
   A.noise = nullptr;
   if (!A.inline_noise) {  // caller's z (parity mode): transposed h-major by noise_prep_kernel
     double* zh = (double*)mp_ws(ctx, WS_NOISE, sizeof(double) * (size_t)S * K * H * 2);

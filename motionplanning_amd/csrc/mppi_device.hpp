@@ -303,13 +303,14 @@ __device__ __forceinline__ void store_state(const TrajOut& T, int j, const doubl
 }
 
 // The control cost λ·u_nomᵀ·inv(Σ)·(u − u_nom) of step j (MPPIUtils.jl:45, Julia's n-ary `*` as a
-// left fold): its row vector t = (λ·u_nom)ᵀ·inv(Σ) depends only on the scene's nominal control,
-// so the plan kernel evaluates it once per (scene, step) into LDS (same operations, same bits)
-// instead of once per rollout-step.
+// left fold, ((λ·u_nomᵀ)·inv(Σ))·d): its row vector t = (λ·u_nom)ᵀ·inv(Σ) depends only on the scene's
+// nominal control, so the plan kernel evaluates it once per (scene, step) into LDS (same operations,
+// same bits) instead of once per rollout-step.  The vector-matrix product is BLAS dgemv 'T' and the
+// last one BLAS ddot in Julia; both round as OpenBLAS's FMA kernels do (oracle/or_blas.h).
 __device__ __forceinline__ void ctrl_cost_row(const MppiDev& P, double un0, double un1, double* t) {
   const double a0 = P.lambda * un0, a1 = P.lambda * un1;
-  t[0] = a0 * P.Si[0] + a1 * P.Si[2];
-  t[1] = a0 * P.Si[1] + a1 * P.Si[3];
+  t[0] = __builtin_fma(P.Si[0], a0, P.Si[2] * a1);
+  t[1] = __builtin_fma(P.Si[1], a0, P.Si[3] * a1);
 }
 
 // --------------------------------------------------------------- rollout
@@ -373,7 +374,7 @@ __device__ __forceinline__ double rollout_pair(const MppiDev& P, const double* X
         ctrl_cost_row(P, un0, un1, t);
       }
       const double d0 = u[0] - un0, d1 = u[1] - un1;
-      cj = cj + (t[0] * d0 + t[1] * d1);
+      cj = cj + __builtin_fma(t[1], d1, t[0] * d0);  // ddot, n = 2
     }
     sum = sum + cj;
     ok_all &= okc & okb;

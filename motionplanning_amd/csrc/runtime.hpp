@@ -57,6 +57,7 @@ struct mp_ctx {
   // (a context is used by one thread at a time, so the flags need no lock)
   bool mppi_lds_attr = false, fin_lds_attr = false;
   bool ilqr_fused_attr = false;  // the fused iLQR backward kernel's dynamic-LDS attribute is set
+  int ha_pcap[3] = {-1, -1, -1};  // co-resident blocks of each ha_persist_kernel shape on this device (0: none)
   // multi-GPU in one process (mp_comm_init): the group and this context's rank in it
   mp_comm_group* comm = nullptr;
   int comm_rank = -1;

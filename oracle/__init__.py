@@ -66,6 +66,11 @@ def lib():
         L.or_svd2_batch.argtypes = [ctypes.c_int, _V, _V, _V, _V]
         L.or_pinv2_fast_batch.argtypes = [ctypes.c_int, _V, _V, _V]
         L.or_chol2.argtypes = [_V, _V]
+        L.or_mppi_ctrl_term.restype = _D
+        L.or_mppi_ctrl_term.argtypes = [_D, _V, _V, _V]
+        L.or_set_blas.argtypes = [ctypes.c_int]
+        L.or_set_blas.restype = None
+        L.or_get_blas.restype = ctypes.c_int
         for name, args in [
             ("or_ilqr_rollout", [ctypes.POINTER(ILQRParams), _V, _V, _V]),
             ("or_ilqr_backward", [ctypes.POINTER(ILQRParams), _V, _V, _V, _V]),
@@ -78,6 +83,29 @@ def lib():
                 f.argtypes = args
         _lib = L
     return _lib
+
+
+# ------------------------------------------------- BLAS rounding convention
+def set_blas(v):
+    """or_blas.h: 1 = the reference's BLAS-dispatched products rounded as OpenBLAS does (the
+    default), 0 = the left fold of separately rounded products.  Returns the previous value."""
+    L = lib()
+    old = L.or_get_blas()
+    L.or_set_blas(int(v))
+    return old
+
+
+class blas_mode:
+    """with oracle.blas_mode(0): ... -- the other convention for the block (tools/blas_replay.py)."""
+
+    def __init__(self, v):
+        self.v = v
+
+    def __enter__(self):
+        self.old = set_blas(self.v)
+
+    def __exit__(self, *a):
+        set_blas(self.old)
 
 
 # ----------------------------------------------------------------- math
@@ -290,6 +318,14 @@ def _ha():
         L.or_change_basis.argtypes = [_V, _V, _D, _V]
         L.or_ha_retrieve.restype = ctypes.c_int
         L.or_ha_retrieve.argtypes = [_V, ctypes.c_int, _V, ctypes.c_int, _V, _V, _V, _V, _V]
+        L.or_ha_rect_pts.restype = None
+        L.or_ha_rect_pts.argtypes = [_V, _V]
+        L.or_ha_sat_dps.restype = None
+        L.or_ha_sat_dps.argtypes = [_V, _V, ctypes.c_int, _V, _V]
+        L.or_ha_census_set.restype = None
+        L.or_ha_census_set.argtypes = [ctypes.c_int]
+        L.or_ha_census_get.restype = None
+        L.or_ha_census_get.argtypes = [_V]
         L.or_ha_plan.restype = ctypes.c_int
         L.or_ha_plan.argtypes = [P] + [_V] * 12
         L._ha_ready = True

@@ -17,6 +17,7 @@
 
 #include "../include/mp_jlmath.h"
 #include "../include/mpgpu.h"
+#include "or_blas.h"
 
 #define NRS 48
 #define PI2 (MPJ_PI / 2)
@@ -250,13 +251,17 @@ int or_ha_act_path(const double* init, double minR, const double* cm, double* pa
 }
 
 /* ------------------------------------------------------- collision check */
-/* GetRectanglePts, CollisionDetection/src/utils.jl:14-25: pts[5][2] */
+/* GetRectanglePts, CollisionDetection/src/utils.jl:14-25: pts[5][2].  R*pts is BLAS dgemm
+ * (2x2 * 2x5, K = 2: or_blas.h blk2), then `.+ [ox; oy]`. */
 static void rect_pts(double ox, double oy, double c, double s, double l, double w, double* pts) {
   const double px[5] = {-l, -l, l, l, -l}, py[5] = {w, -w, -w, w, w};
   for (int j = 0; j < 5; j++) {
-    pts[2 * j] = c * px[j] + (-s) * py[j] + ox;
-    pts[2 * j + 1] = s * px[j] + c * py[j] + oy;
+    pts[2 * j] = blk2(c, px[j], -s, py[j]) + ox;
+    pts[2 * j + 1] = blk2(s, px[j], c, py[j]) + oy;
   }
+}
+void or_ha_rect_pts(const double* blk, double* pts) { /* GetRectanglePts(block) with Julia's sin/cos */
+  rect_pts(blk[0], blk[1], mpj_cos(blk[2]), mpj_sin(blk[2]), blk[3], blk[4], pts);
 }
 
 /* SeparatingAxisTheorem, utils.jl:37-62: 1 if an edge normal of `base` separates */
@@ -267,8 +272,9 @@ static int sat(const double* base, const double* other) {
     double nx = -vy, ny = vx;
     double mnb = 0, mxb = 0, mno = 0, mxo = 0;
     for (int j = 0; j < 5; j++) {
-      double db = (base[2 * j] - bx) * nx + (base[2 * j + 1] - by) * ny;
-      double dq = (other[2 * j] - bx) * nx + (other[2 * j + 1] - by) * ny;
+      /* transpose(pts .- bg_pt) * normal_vec: BLAS dgemv 'T' on the 2x5 (or_blas.h blv_t2) */
+      double db = blv_t2(base[2 * j] - bx, nx, base[2 * j + 1] - by, ny);
+      double dq = blv_t2(other[2 * j] - bx, nx, other[2 * j + 1] - by, ny);
       if (j == 0 || db < mnb) mnb = db;
       if (j == 0 || db > mxb) mxb = db;
       if (j == 0 || dq < mno) mno = dq;
@@ -279,6 +285,17 @@ static int sat(const double* base, const double* other) {
   return 0;
 }
 
+/* the projections of edge e's SAT test (utils.jl:48-49), for tests/test_oracle_blas.py */
+void or_ha_sat_dps(const double* base, const double* other, int e, double* db, double* dq) {
+  double bx = base[2 * e], by = base[2 * e + 1];
+  double vx = base[2 * e + 2] - bx, vy = base[2 * e + 3] - by;
+  double nx = -vy, ny = vx;
+  for (int j = 0; j < 5; j++) {
+    db[j] = blv_t2(base[2 * j] - bx, nx, base[2 * j + 1] - by, ny);
+    dq[j] = blv_t2(other[2 * j] - bx, nx, other[2 * j + 1] - by, ny);
+  }
+}
+
 /* ConvexCollision, utils.jl:64-74: 1 = no collision (note the && of both SATs) */
 int or_ha_convex_free(const double* p1, const double* p2) { return sat(p1, p2) && sat(p2, p1); }
 
@@ -287,8 +304,55 @@ static void wall_pts(const double* wl, double* pts) {
   rect_pts(wl[0], wl[1], mpj_cos(wl[2]), mpj_sin(wl[2]), wl[3], wl[4], pts);
 }
 
+/* tools/blas_replay.py's census: with or_ha_census set, every block check also evaluates every
+ * (pose, wall) ConvexCollision under both or_blas conventions and counts the pairs and checks whose
+ * booleans differ (the result returned is the current convention's). */
+int or_ha_census = 0;
+long long or_ha_census_n[4]; /* pairs, pairs split, checks, checks split */
+void or_ha_census_set(int on) { or_ha_census = on; memset(or_ha_census_n, 0, sizeof or_ha_census_n); }
+void or_ha_census_get(long long* out) { memcpy(out, or_ha_census_n, sizeof or_ha_census_n); }
+
+static int block_free_mode(const mp_ha_params* p, const double* path, int n, const double* walls, int mode,
+                           uint8_t* pair_free) {
+  const int save = or_blas;
+  or_blas = mode;
+  const int sp = 5;
+  int npose = n > sp ? (n - 1) / sp + 1 : 1;
+  int nw = p->n_walls < 64 ? p->n_walls : 64;
+  double L2 = p->vehicle_len / 2, W2 = p->vehicle_wid / 2;
+  int all = 1;
+  for (int i = 0; i < nw; i++) {
+    double wp[10];
+    wall_pts(walls + 5 * i, wp);
+    for (int j = 0; j < npose; j++) {
+      const double* q = path + 3 * (j * sp);
+      double x = q[0] + L2 * mpj_cos(q[2]), y = q[1] + L2 * mpj_sin(q[2]);
+      double yaw = mpj_modpi(q[2]);
+      double vp[10];
+      rect_pts(x, y, mpj_cos(yaw), mpj_sin(yaw), L2, W2, vp);
+      const int f = or_ha_convex_free(wp, vp);
+      pair_free[i * npose + j] = (uint8_t)f;
+      all &= f;
+    }
+  }
+  or_blas = save;
+  return all;
+}
+
 /* block_collision_check, hybrid_astar_utils.jl:180-204 on path[n][3]; 1 = collision free */
 int or_ha_block_free(const mp_ha_params* p, const double* path, int n, const double* walls) {
+  if (or_ha_census) {
+    const int npose = n > 5 ? (n - 1) / 5 + 1 : 1, np = (p->n_walls < 64 ? p->n_walls : 64) * npose;
+    uint8_t* f0 = (uint8_t*)malloc((size_t)np * 2);
+    const int r0 = block_free_mode(p, path, n, walls, 0, f0);
+    const int r1 = block_free_mode(p, path, n, walls, 1, f0 + np);
+    for (int i = 0; i < np; i++) or_ha_census_n[1] += f0[i] != f0[np + i];
+    or_ha_census_n[0] += np;
+    or_ha_census_n[2] += 1;
+    or_ha_census_n[3] += r0 != r1;
+    free(f0);
+    return or_blas ? r1 : r0;
+  }
   const int sp = 5;
   int npose = n > sp ? (n - 1) / sp + 1 : 1;
   double wp[64][10];
@@ -546,15 +610,16 @@ static void or_cubic_fit(const double* cur, const double* nxt, double* out /* [1
   double Pm[4];
   or_pinv2(A, Pm);
   const double b0 = yg, b1 = mpj_tan(pg);
-  const double p1 = Pm[0] * b0 + Pm[1] * b1, p2 = Pm[2] * b0 + Pm[3] * b1;
+  /* pinv(A)*B: BLAS dgemv 'N' 2x2 (or_blas.h blv_n22) */
+  const double p1 = blv_n22(Pm[0], b0, Pm[1], b1), p2 = blv_n22(Pm[2], b0, Pm[3], b1);
   const double s0 = mpj_sin(cur[2]), c0 = mpj_cos(cur[2]);
   for (int k = 0; k < 100; k++) {
     const double t = (double)k / 99; /* LinRange(0, xg, 100): (1-t)*0 + t*xg */
     const double x = (1 - t) * 0.0 + t * xg;
     const double y = p1 * (x * x * x) + p2 * (x * x);
     const double psi = mpj_atan((3 * p1) * (x * x) + (2 * p2) * x);
-    out[3 * k] = (c0 * x + (-s0) * y) + cur[0]; /* Rmat*path[1:2,:] .+ [x0; y0] */
-    out[3 * k + 1] = (s0 * x + c0 * y) + cur[1];
+    out[3 * k] = blk2(c0, x, -s0, y) + cur[0]; /* Rmat*path[1:2,:] (dgemm, K = 2) .+ [x0; y0] */
+    out[3 * k + 1] = blk2(s0, x, c0, y) + cur[1];
     out[3 * k + 2] = psi + cur[2];
   }
 }

@@ -18,6 +18,7 @@
 
 #include "../include/mp_jlmath.h"
 #include "../include/mpgpu.h"
+#include "or_blas.h"
 
 /* Dynamics.jl:1-16 ; state [x, y, ux, ψ], control [ax, δ] */
 static void dyn(const double* s, const double* u, double* d) {
@@ -214,64 +215,40 @@ int or_ilqr_backward(const mp_ilqr_params* p, const double* X, const double* U, 
     linearize(xc, uc, p->dT, e, A, B);
     calc_matrix(cs, xc, uc, e, lx, lu, lxx, luu, lux);
     double Qx[4], Qu[2], Qxx[16], Quu[4], Qux[8], T44[16], T24[8], P[4];
-    for (int i = 0; i < 4; i++) {  /* Qx = lx + fx' * Vx */
-      double acc = A[0 * 4 + i] * Vx[0];
-      for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vx[k];
-      Qx[i] = lx[i] + acc;
-    }
-    for (int i = 0; i < 2; i++) {  /* Qu = lu + fu' * Vx */
-      double acc = B[0 * 2 + i] * Vx[0];
-      for (int k = 1; k < 4; k++) acc = acc + B[k * 2 + i] * Vx[k];
-      Qu[i] = lu[i] + acc;
-    }
-    for (int i = 0; i < 4; i++)  /* T44 = fx' * Vxx */
-      for (int c = 0; c < 4; c++) {
-        double acc = A[0 * 4 + i] * Vxx[0 * 4 + c];
-        for (int k = 1; k < 4; k++) acc = acc + A[k * 4 + i] * Vxx[k * 4 + c];
-        T44[4 * i + c] = acc;
-      }
-    for (int i = 0; i < 4; i++)  /* Qxx = lxx + (fx' Vxx) fx */
-      for (int c = 0; c < 4; c++) {
-        double acc = T44[4 * i + 0] * A[0 * 4 + c];
-        for (int k = 1; k < 4; k++) acc = acc + T44[4 * i + k] * A[k * 4 + c];
-        Qxx[4 * i + c] = lxx[4 * i + c] + acc;
-      }
-    for (int i = 0; i < 2; i++)  /* T24 = fu' * Vxx */
-      for (int c = 0; c < 4; c++) {
-        double acc = B[0 * 2 + i] * Vxx[0 * 4 + c];
-        for (int k = 1; k < 4; k++) acc = acc + B[k * 2 + i] * Vxx[k * 4 + c];
-        T24[4 * i + c] = acc;
-      }
-    for (int i = 0; i < 2; i++)  /* Quu = luu + (fu' Vxx) fu */
-      for (int c = 0; c < 2; c++) {
-        double acc = T24[4 * i + 0] * B[0 * 2 + c];
-        for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * B[k * 2 + c];
-        Quu[2 * i + c] = luu[2 * i + c] + acc;
-      }
-    for (int i = 0; i < 2; i++)  /* Qux = lux + (fu' Vxx) fx */
-      for (int c = 0; c < 4; c++) {
-        double acc = T24[4 * i + 0] * A[0 * 4 + c];
-        for (int k = 1; k < 4; k++) acc = acc + T24[4 * i + k] * A[k * 4 + c];
-        Qux[4 * i + c] = lux[4 * i + c] + acc;
-      }
+    /* Every product is BLAS dgemm in Julia (lx, lu, Vx are n x 1 matrices, GetMatrix.jl:6-7), with the
+     * association of Julia's 3-argument `*` (LinearAlgebra._tri_matmul: equal costs -> (A*B)*C, and
+     * K'*(Quu*k) for Vx); or_blas.h blk4 / blk2 round them as OpenBLAS does. */
+    for (int i = 0; i < 4; i++) Qx[i] = lx[i] + blk4(A + i, 4, Vx, 1);      /* Qx = lx + fx' * Vx */
+    for (int i = 0; i < 2; i++) Qu[i] = lu[i] + blk4(B + i, 2, Vx, 1);      /* Qu = lu + fu' * Vx */
+    for (int i = 0; i < 4; i++)                                             /* T44 = fx' * Vxx */
+      for (int c = 0; c < 4; c++) T44[4 * i + c] = blk4(A + i, 4, Vxx + c, 4);
+    for (int i = 0; i < 4; i++)                                             /* Qxx = lxx + (fx' Vxx) fx */
+      for (int c = 0; c < 4; c++) Qxx[4 * i + c] = lxx[4 * i + c] + blk4(T44 + 4 * i, 1, A + c, 4);
+    for (int i = 0; i < 2; i++)                                             /* T24 = fu' * Vxx */
+      for (int c = 0; c < 4; c++) T24[4 * i + c] = blk4(B + i, 2, Vxx + c, 4);
+    for (int i = 0; i < 2; i++)                                             /* Quu = luu + (fu' Vxx) fu */
+      for (int c = 0; c < 2; c++) Quu[2 * i + c] = luu[2 * i + c] + blk4(T24 + 4 * i, 1, B + c, 2);
+    for (int i = 0; i < 2; i++)                                             /* Qux = lux + (fu' Vxx) fx */
+      for (int c = 0; c < 4; c++) Qux[4 * i + c] = lux[4 * i + c] + blk4(T24 + 4 * i, 1, A + c, 4);
     or_pinv2(Quu, P);
     double kk[2], KK[8];
-    for (int i = 0; i < 2; i++) kk[i] = (-P[2 * i + 0]) * Qu[0] + (-P[2 * i + 1]) * Qu[1];
+    /* k = -pinv(Quu) * Qu, K = -pinv(Quu) * Qux: dgemm with K = 2 (2x1 and 2x4 right operands) */
+    for (int i = 0; i < 2; i++) kk[i] = blk2(-P[2 * i + 0], Qu[0], -P[2 * i + 1], Qu[1]);
     for (int i = 0; i < 2; i++)
-      for (int c = 0; c < 4; c++) KK[4 * i + c] = (-P[2 * i + 0]) * Qux[0 * 4 + c] + (-P[2 * i + 1]) * Qux[1 * 4 + c];
+      for (int c = 0; c < 4; c++) KK[4 * i + c] = blk2(-P[2 * i + 0], Qux[0 * 4 + c], -P[2 * i + 1], Qux[1 * 4 + c]);
     for (int i = 0; i < 2; i++) kout[2 * j + i] = kk[i];
     for (int r = 0; r < 2; r++)
       for (int c = 0; c < 4; c++) Kout[8 * j + 2 * c + r] = KK[4 * r + c];
     /* Vx = Qx - K' * (Quu * k)   (Julia's 3-arg * picks A*(B*C) here) */
     double qk[2];
-    for (int i = 0; i < 2; i++) qk[i] = Quu[2 * i + 0] * kk[0] + Quu[2 * i + 1] * kk[1];
-    for (int i = 0; i < 4; i++) Vx[i] = Qx[i] - (KK[0 * 4 + i] * qk[0] + KK[1 * 4 + i] * qk[1]);
+    for (int i = 0; i < 2; i++) qk[i] = blk2(Quu[2 * i + 0], kk[0], Quu[2 * i + 1], kk[1]);
+    for (int i = 0; i < 4; i++) Vx[i] = Qx[i] - blk2(KK[0 * 4 + i], qk[0], KK[1 * 4 + i], qk[1]);
     /* Vxx = Qxx - (K' * Quu) * K */
     double KQ[8];
     for (int i = 0; i < 4; i++)
-      for (int c = 0; c < 2; c++) KQ[2 * i + c] = KK[0 * 4 + i] * Quu[0 * 2 + c] + KK[1 * 4 + i] * Quu[1 * 2 + c];
+      for (int c = 0; c < 2; c++) KQ[2 * i + c] = blk2(KK[0 * 4 + i], Quu[0 * 2 + c], KK[1 * 4 + i], Quu[1 * 2 + c]);
     for (int i = 0; i < 4; i++)
-      for (int c = 0; c < 4; c++) Vxx[4 * i + c] = Qxx[4 * i + c] - (KQ[2 * i + 0] * KK[0 * 4 + c] + KQ[2 * i + 1] * KK[1 * 4 + c]);
+      for (int c = 0; c < 4; c++) Vxx[4 * i + c] = Qxx[4 * i + c] - blk2(KQ[2 * i + 0], KK[0 * 4 + c], KQ[2 * i + 1], KK[1 * 4 + c]);
   }
   return 0;
 }
@@ -284,11 +261,8 @@ double or_ilqr_forward(const mp_ilqr_params* p, const double* X, const double* U
   for (int i = 0; i < N - 1; i++) {
     double dx[4], u[2];
     for (int r = 0; r < 4; r++) dx[r] = Xn[4 * i + r] - X[4 * i + r];
-    for (int r = 0; r < 2; r++) {
-      double acc = Kg[8 * i + 2 * 0 + r] * dx[0];
-      for (int c = 1; c < 4; c++) acc = acc + Kg[8 * i + 2 * c + r] * dx[c];
-      u[r] = (U[2 * i + r] + alpha * k[2 * i + r]) + acc;
-    }
+    for (int r = 0; r < 2; r++) /* Klist[:, :, i] * (xtilde .- xn): BLAS dgemv 'N' 2x4 (or_blas.h) */
+      u[r] = (U[2 * i + r] + alpha * k[2 * i + r]) + blv_n24(Kg + 8 * i + r, 2, dx);
     Un[2 * i] = u[0];
     Un[2 * i + 1] = u[1];
     or_ilqr_rk4(Xn + 4 * i, u, p->dT, Xn + 4 * (i + 1));

@@ -19,6 +19,11 @@
 
 #include "../include/mp_jlmath.h"
 #include "../include/mpgpu.h"
+#include "or_blas.h"
+
+int or_blas = 1; /* or_blas.h: the products round as Julia's OpenBLAS dispatch rounds them */
+void or_set_blas(int v) { or_blas = v; }
+int or_get_blas(void) { return or_blas; }
 
 /* OptimalControl/MPPI/src/vehicledynamics.jl:1-54.  Returns the running cost
  * (:52); ds gets dstates (:50). */
@@ -132,6 +137,18 @@ void or_chol2(const double* A, double* L) {
  * p->ctrl_cost == 0).  ctrl: H rows of 2 with row stride `cs` (0 = constant).
  * states_his[(H+1)][7] optional.  Returns cost_total; *feas = constraint.
  */
+/* MPPIUtils.jl:45, λ * u_nom' * inv(Σ) * (u - u_nom): Base's n-ary `*` folds left, ((λ*u')*Σ⁻¹)*d;
+ * the vector-matrix product is BLAS dgemv 'T' (Σ⁻¹' * λu) and the last one BLAS ddot (or_blas.h) */
+static double ctrl_term(double lambda, const double* Si, const double* un, const double* u) {
+  double a0 = lambda * un[0], a1 = lambda * un[1];
+  double t0 = blv_t2(Si[0], a0, Si[2], a1), t1 = blv_t2(Si[1], a0, Si[3], a1);
+  double d0 = u[0] - un[0], d1 = u[1] - un[1];
+  return bl_dot2(t0, d0, t1, d1);
+}
+double or_mppi_ctrl_term(double lambda, const double* Si, const double* un, const double* u) {
+  return ctrl_term(lambda, Si, un, u);
+}
+
 double or_rollout(const mp_mppi_params* p, const double* X0, const double* goal,
                   const double* ctrl, int64_t cs, const double* unom, const double* obs,
                   const uint8_t* grid, double* states_his, int* feas) {
@@ -156,11 +173,7 @@ double or_rollout(const mp_mppi_params* p, const double* X0, const double* goal,
     double cj = pc + cb + cc;
     if (p->ctrl_cost) {
       const double* un = unom + 2 * j;
-      /* λ * u_nom' * inv(Σ) * (u - u_nom), left-fold of Julia's n-ary `*` */
-      double a0 = p->lambda * un[0], a1 = p->lambda * un[1];
-      double t0 = a0 * Si[0] + a1 * Si[2], t1 = a0 * Si[1] + a1 * Si[3];
-      double d0 = u[0] - un[0], d1 = u[1] - un[1];
-      cj = cj + (t0 * d0 + t1 * d1);
+      cj = cj + ctrl_term(p->lambda, Si, un, u);
     }
     sum = sum + cj;
     if (!(okc && okb)) ok_all = 0;

@@ -81,6 +81,27 @@ def test_scenario_batch_lockstep_bitexact(ctx, n, seed):
     assert mism == 0
 
 
+def test_pipelined_tail_without_persistent_launch_bitexact(ctx):
+    """The per-iteration pipelined tail (ha_pipe_kernel, the path a device without cooperative launches
+    takes, or a refused cooperative launch falls back to; MPGPU_HA_PERSIST=0 selects it): bit-exact, and its
+    bounded cross-block waits report through the same error flag the persistent tail's do (mp_ha_plan
+    checks it after any pipelined launch and fails loudly)."""
+    import os
+    hs = ha.scenario_batch(12, seed=4) + [ha.driver_searcher(ha.PERPENDICULAR), ha.driver_searcher(ha.PARALLEL)]
+    _, p, sc, pc = _setup(ctx)
+    os.environ["MPGPU_HA_PERSIST"] = "0"
+    try:
+        ha.plan_batch(hs, ctx=ctx)
+    finally:
+        del os.environ["MPGPU_HA_PERSIST"]
+    for h in hs:
+        ref = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
+        assert h.r.found == ref["found"] and h.r.loop_count == ref["pops"] and h.r.n_nodes == ref["n_nodes"]
+        assert np.array_equal(h.r.pop_sequence, ref["pop_seq"])
+        assert np.array_equal(h.r.hybrid_astar_states.T, ref["states"])
+        assert np.array_equal(h.r.RSpath_final.T, ref["rs_path"])
+
+
 @pytest.mark.parametrize("max_pops", [1, 7, 40])
 def test_max_pops_and_out_of_bounds_start_bitexact(ctx, max_pops):
     """Device-resident search edge cases vs the oracle: the max_pops stop (pop_seq truncated,

@@ -106,35 +106,49 @@ def _model(**kw):
     return ilqr_ulp_sources.Model(**kw)
 
 
+@pytest.mark.skipif(__import__("oracle.openblas").openblas.lib() is None, reason="numpy without its OpenBLAS")
 def test_backward_matches_independent_restatement():
     """k, K of the first sweep (ILQR.jl:46-67) vs tools/ilqr_ulp_sources.py, an independent Python
     restatement (Julia's `states .+ Δ` perturbations, matrix-shaped lx/Vx, its own loops): bit for bit
-    with the oracle's rounding sources, and within 1e-10 with glibc trig/exp and numpy's OpenBLAS
-    products in place of the Julia-libm restatements and the sequential sums."""
+    with the oracle's rounding sources -- every product through numpy's OpenBLAS called as Julia calls it
+    (oracle/openblas.py) against the oracle's default or_blas.h, and the sequential sums against
+    or_blas = 0 -- and within 1e-10 with glibc trig/exp and numpy's own matmul choices."""
     p, X, U, _ = _setup()
     k, K = oracle.ilqr_backward(p, X, U)
     kk, KK = _model().backward(X, U, p.dT)
     assert np.array_equal(k, kk[:, :, 0]) and np.array_equal(K, np.swapaxes(KK, 1, 2))
+    with oracle.blas_mode(0):
+        k0, K0 = oracle.ilqr_backward(p, X, U)
+    kk, KK = _model(prod="seq").backward(X, U, p.dT)
+    assert np.array_equal(k0, kk[:, :, 0]) and np.array_equal(K0, np.swapaxes(KK, 1, 2))
+    assert not np.array_equal(k0, k)  # the conventions differ in the last bits
     kk, KK = _model(trig="libm", exp="libm", prod="blas").backward(X, U, p.dT)
     np.testing.assert_allclose(k, kk[:, :, 0], rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(K, np.swapaxes(KK, 1, 2), rtol=1e-10, atol=1e-12)
 
 
+@pytest.mark.skipif(__import__("oracle.openblas").openblas.lib() is None, reason="numpy without its OpenBLAS")
 def test_solve_converges():
     """ILQR.jl loop at N = 20: the oracle == the independent restatement bit for bit (12 passes,
-    J = 10093.673801764775).  The pass count is a property of Julia's pinv composition: with it, every
-    choice of trig / exp (Julia-libm or glibc) and products (sequential or OpenBLAS) converges in 12
-    passes to J in [10093.65, 10093.68]; only numpy's pinv (BLAS-composed, rcond 1e-15) together with
-    OpenBLAS products gives the 13 passes / J = 10086.6 of the SURVEY's probe (tools/ilqr_ulp_sources.py,
-    DESIGN.md §2)."""
-    p, X, U, J0 = _setup()
-    X, U, J, iters, flags = oracle.ilqr_solve(p, X, U)
-    assert flags == 0 and iters == 13 and J == 10093.673801764775
+    J = 10093.685266152588 with the products rounded as Julia's OpenBLAS dispatch rounds them,
+    10093.673801764775 with sequential sums).  The pass count is a property of Julia's pinv composition:
+    with it, every choice of trig / exp (Julia-libm or glibc) and products (sequential, numpy's matmul or
+    Julia's dispatch) converges in 12 passes to J in [10093.65, 10093.69]; only numpy's pinv (BLAS-composed,
+    rcond 1e-15) together with numpy's matmul products gives the 13 passes / J = 10086.6 of the SURVEY's
+    probe (tools/ilqr_ulp_sources.py)."""
+    p, X0, U0, J0 = _setup()
+    X, U, J, iters, flags = oracle.ilqr_solve(p, X0, U0)
+    assert flags == 0 and iters == 13 and J == 10093.685266152588
     it, Jm, _ = _model().solve()
     assert it == iters and Jm == J
-    for kw in (dict(trig="libm", exp="libm", prod="blas"), dict(exp="fdlibm", prod="blas")):
+    with oracle.blas_mode(0):
+        _, _, J, iters, flags = oracle.ilqr_solve(p, X0, U0)
+    assert flags == 0 and iters == 13 and J == 10093.673801764775
+    it, Jm, _ = _model(prod="seq").solve()
+    assert it == iters and Jm == J
+    for kw in (dict(trig="libm", exp="libm", prod="blas"), dict(exp="fdlibm", prod="blas"), dict(trig="libm")):
         it, Jm, _ = _model(**kw).solve()
-        assert it == 13 and 10093.65 < Jm < 10093.68, kw
+        assert it == 13 and 10093.65 < Jm < 10093.69, kw
     it, Jm, _ = _model(pinv="numpy", prod="blas").solve()
     assert it == 14 and 10086.6 < Jm < 10086.7
 

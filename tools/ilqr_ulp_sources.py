@@ -14,6 +14,9 @@ can be swapped independently:
          numpy  np.linalg.pinv (BLAS composition, rcond 1e-15)
   prod   seq    every matrix product as a left-to-right sum of rounded products (the oracle)
          blas   numpy's OpenBLAS for the same shapes (FMA kernels; the gemm->gemv forward for n = 1)
+         julia  numpy's OpenBLAS called as Julia calls it (oracle/openblas.py: dgemm_64_ with Julia's
+                trans flags for every matrix product -- lx/lu/Vx are n x 1 matrices -- and dgemv_64_
+                'N' for Klist * (xtilde .- xn)); = the C oracle with or_blas = 1 bit for bit
   pert   plus   Julia's `states .+ Δ` (untouched entries get + 0.0: -0.0 -> +0.0)
          copy   the perturbed entry only (round-1/2 oracle; -0.0 survives)
 
@@ -33,7 +36,7 @@ LA, LB = 1.56, 1.64
 
 
 class Model:
-    def __init__(self, trig="jl", exp="julia", pinv="lapack", prod="seq", pert="plus"):
+    def __init__(self, trig="jl", exp="julia", pinv="lapack", prod="julia", pert="plus"):
         self.cfg = dict(trig=trig, exp=exp, pinv=pinv, prod=prod, pert=pert)
         L = oracle.lib()
         if trig == "jl":
@@ -52,9 +55,15 @@ class Model:
         self.pert = pert
 
     # ---------------------------------------------------------------- products
-    def mm(self, A, B):
+    def mm(self, A, B, ta=False):
+        """op(A) * B; ta: A' * B (Julia's A' * B)."""
+        if self.prod == "julia":
+            from oracle import openblas
+            return openblas.gemm(A, B, ta=ta)
         A = np.asarray(A, np.float64)
         B = np.asarray(B, np.float64)
+        if ta:
+            A = A.T
         if self.prod == "blas":
             return np.asfortranarray(A) @ np.asfortranarray(B)
         m, k = A.shape
@@ -163,17 +172,17 @@ class Model:
         for j in range(N - 2, -1, -1):
             fx, fu = self.lin(X[j], U[j], dT)
             lx, lu, lxx, luu, lux = self.calc(X[j], U[j], self.stage)
-            Qx = lx + mm(fx.T, Vx)
-            Qu = lu + mm(fu.T, Vx)
-            Qxx = lxx + mm(mm(fx.T, Vxx), fx)
-            Quu = luu + mm(mm(fu.T, Vxx), fu)
-            Qux = lux + mm(mm(fu.T, Vxx), fx)
+            Qx = lx + mm(fx, Vx, ta=True)
+            Qu = lu + mm(fu, Vx, ta=True)
+            Qxx = lxx + mm(mm(fx, Vxx, ta=True), fx)
+            Quu = luu + mm(mm(fu, Vxx, ta=True), fu)
+            Qux = lux + mm(mm(fu, Vxx, ta=True), fx)
             P = -np.asarray(self.pinv(Quu))
             kk = mm(P, Qu)
             KK = mm(P, Qux)
             k[j], K[j] = kk, KK
-            Vx = Qx - mm(KK.T, mm(Quu, kk))
-            Vxx = Qxx - mm(mm(KK.T, Quu), KK)
+            Vx = Qx - mm(KK, mm(Quu, kk), ta=True)
+            Vxx = Qxx - mm(mm(KK, Quu, ta=True), KK)
         return k, K
 
     def forward(self, X, U, k, K, alpha, dT):
@@ -182,7 +191,12 @@ class Model:
         Un = np.zeros_like(U)
         for i in range(N - 1):
             dx = (Xn[i] - X[i]).reshape(4, 1)
-            u = (U[i] + alpha * k[i][:, 0]) + self.mm(K[i], dx)[:, 0]
+            if self.prod == "julia":  # Klist[:, :, i] * (xtilde .- xn): a matrix times a Vector -> dgemv
+                from oracle import openblas
+                Kdx = openblas.gemv(K[i], dx[:, 0])
+            else:
+                Kdx = self.mm(K[i], dx)[:, 0]
+            u = (U[i] + alpha * k[i][:, 0]) + Kdx
             Un[i] = u
             Xn[i + 1] = self.rk4(Xn[i], u, dT)
         return Xn, Un, self.total(Xn, Un)
@@ -213,16 +227,18 @@ class Model:
 
 
 CONFIGS = [
-    ("round-2 oracle (jl trig, fdlibm exp, closed pinv, seq, copy)", dict(exp="fdlibm", pinv="closed", pert="copy")),
-    ("round-3 oracle (jl trig, julia exp, lapack pinv, seq, plus)", dict()),
+    ("round-2 oracle (jl trig, fdlibm exp, closed pinv, seq, copy)", dict(exp="fdlibm", pinv="closed", pert="copy",
+                                                                        prod="seq")),
+    ("round-3..5 oracle (jl trig, julia exp, lapack pinv, seq, plus)", dict(prod="seq")),
+    ("round-6 oracle (products as Julia's OpenBLAS dispatch rounds them)", dict()),
     ("  swap pinv -> closed", dict(pinv="closed")),
     ("  swap pinv -> numpy", dict(pinv="numpy")),
     ("  swap exp -> fdlibm", dict(exp="fdlibm")),
     ("  swap exp -> glibc", dict(exp="libm")),
     ("  swap trig -> glibc", dict(trig="libm")),
-    ("  swap prod -> OpenBLAS", dict(prod="blas")),
+    ("  swap prod -> numpy's @ (OpenBLAS, numpy's own gemm/gemv choice)", dict(prod="blas")),
+    ("  swap prod -> sequential", dict(prod="seq")),
     ("  swap pert -> copy", dict(pert="copy")),
-    ("round-3 oracle with OpenBLAS products", dict(prod="blas")),
     ("numpy restatement (glibc trig+exp, numpy pinv, OpenBLAS, plus)", dict(trig="libm", exp="libm", pinv="numpy",
                                                                           prod="blas")),
 ]
@@ -244,7 +260,7 @@ def factorial():
     print("| trig | exp | pinv | prod | passes | J | trials |")
     print("|---|---|---|---|---|---|---|")
     for trig, exp, pinv, prod in itertools.product(("jl", "libm"), ("julia", "libm"), ("lapack", "numpy"),
-                                                   ("seq", "blas")):
+                                                   ("seq", "blas", "julia")):
         it, J, trials = Model(trig=trig, exp=exp, pinv=pinv, prod=prod).solve()
         print("| %s | %s | %s | %s | %d | %.10f | %s |" % (trig, exp, pinv, prod, it - 1, J, ",".join(map(str, trials))))
 

@@ -1,6 +1,6 @@
 """Per-launch HBM traffic of the dominant kernels from rocprofv3 --pmc passes.
 
-usage: python tools/pmc_traffic.py DIR S K H  (DIR holds pmc1/ pmc2/ pmc3/ from tools/gpu_pass.sh;
+usage: python tools/pmc_traffic.py DIR S K H  (DIR holds pmc1/ pmc2/ pmc3/ from tools/gpu_pass4.sh;
        S, K, H = the bench configuration those passes ran)
 
 FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM [CDNA4]): on gfx950
