@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--rotate", type=int, default=3, help="output buffer sets rotated (>256 MB MALL at S=8)")
     ap.add_argument("--no-single", action="store_true", help="skip the single-scene (configs[1]) line")
+    ap.add_argument("--no-whole", action="store_true", help="skip the configs[4]-whole (64 scenes, one GPU) line")
     ap.add_argument("--roofline", default=os.path.join(ROOT, "profiles", "roofline_latest.json"),
                     help="per-kernel VALU counts + durations (tools/pmc_roofline.py) for the iLQR / HA* rooflines")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -276,6 +277,10 @@ def main():
     if tr is not None:
         out["roofline"]["traffic"] = tr["traffic_bytes"]
         out["roofline"]["traffic_source"] = tr["source"]
+        out["roofline"]["counters_note"] = ("PMC counters (FETCH_SIZE / WRITE_SIZE / SQ_*) per launch from the builder's "
+                                            "rocprofv3 pass recorded in " + os.path.relpath(a.traffic, ROOT) +
+                                            " (rocprofv3 cannot run inside this bench); kernel_ms is this run's "
+                                            "live HIP-event time")
         if tr.get("valu_insts"):
             # the bound that binds: fp64 VALU issue.  A wave64 fp64 instruction occupies a SIMD-32
             # for 4 cycles (78.6 TF fp64 vector = 1024 SIMDs x 2.4 GHz x 16 FMA lanes x 2), so the
@@ -299,6 +304,17 @@ def main():
                                                         * tr["waves"] / VALU_SIMDS)
                 out["roofline"]["valu"]["simd_busy_source"] = (tr["source"] + " SQ_ACTIVE_INST_VALU / "
                                                                "SQ_WAVE_CYCLES x SQ_WAVES / 1024 SIMDs")
+    if not a.no_whole and world == 1 and S < 64:
+        # configs[4] whole on this one GPU: the 64 scenes in one call (the strong-scaling base of configs[4];
+        # one rollout per lane, 2 waves per SIMD), 1.9 GB of TrajectoryCollection per step
+        sw = max(2, a.steps // 4)
+        e64, k64, ok64 = run(a, 64, ctx, dev, world, rank, sw, max(1, a.warmup // 2), 2)[:3]
+        out["configs4_whole"] = {
+            "workload": "configs[4] whole: all 64 scenes (obstacle_field.mat fields 1-64) in one call on one GPU",
+            "value": 64 * K * H * sw / e64, "unit": "rollout-steps/s", "steps": sw, "ms_per_step": e64 / sw * 1e3,
+            "kernel_ms": k64, "hbm_frac": algorithmic_bytes(64, K, H) / (k64 * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "valid": ok64,
+        }
     if not a.no_single and S != 1:
         e1, k1, ok1 = run(a, 1, ctx, dev, world, rank, a.steps, a.warmup, 12, cfg5=False)[:3]
         out["single_scene"] = {
@@ -319,6 +335,24 @@ def main():
             target[key] = fn()
         if a.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
+    # the headline numbers of every leg once more at the END of the line (the driver keeps its tail)
+    sm = {"mppi_rollout_steps_per_s": out["value"], "mppi_ms_per_step": out["ms_per_step"],
+          "mppi_plan_kernel_ms": kern_ms}
+    if "configs4_whole" in out:
+        sm["configs4_whole_rollout_steps_per_s"] = out["configs4_whole"]["value"]
+    if "single_scene" in out:
+        sm["configs1_single_scene_rollout_steps_per_s"] = out["single_scene"]["value"]
+    if "ilqr" in out:
+        sm["ilqr_solve_ms"] = out["ilqr"]["solve"]["ms"]
+        sm["ilqr_pass_ms"] = out["ilqr"]["ms_per_pass"]
+    if "hybrid_astar" in out:
+        sm["hybrid_astar_plan_ms"] = out["hybrid_astar"]["ms_total"]
+        if "shards_world8" in out["hybrid_astar"]:
+            sw8 = out["hybrid_astar"]["shards_world8"]
+            sm["hybrid_astar_world8_projection"] = {k: sw8[k]["projected_speedup"] for k in ("contiguous", "strided") if k in sw8}
+    if "closed_loop" in out:
+        sm["closed_loop_ms_per_replan"] = out["closed_loop"].get("ms_per_replan")
+    out["summary"] = sm
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -1553,18 +1553,27 @@ int make_ha(mp_ctx* ctx, const mp_ha_params* p, HaDev* D) {
 // half length, half width), a and b [B][3] (nodes / starts, goals)
 void ha_cull_ok(const mp_ctx* ctx, const mp_ha_params* p, HaDev* D, int B, const double* walls, const double* a,
                 const double* b) {
-  double m = std::max({p->minR, p->vehicle_len, p->vehicle_wid, p->expand_time, ctx->ha_prim_ext});
-  for (int i = 0; i < 6; i++) m = std::max(m, std::fabs(p->stbound[i]));
+  // the largest magnitude, and whether any input is NaN or infinite (std::max drops a NaN operand, so it is
+  // tracked separately: a non-finite coordinate or length turns the culls off, every SAT call then runs)
+  double m = 0.0;
+  bool finite = true;
+  auto see = [&](double v) {
+    finite &= std::isfinite(v);
+    m = std::max(m, std::fabs(v));
+  };
+  for (double v : {p->minR, p->vehicle_len, p->vehicle_wid, p->expand_time, ctx->ha_prim_ext}) see(v);
+  for (int i = 0; i < 6; i++) see(p->stbound[i]);
   for (size_t i = 0; walls && i < (size_t)B * p->n_walls; i++) {
     const double* w = walls + 5 * i;
-    m = std::max(m, std::fabs(w[0]) + std::fabs(w[3]) + std::fabs(w[4]));
-    m = std::max(m, std::fabs(w[1]) + std::fabs(w[3]) + std::fabs(w[4]));
+    see(w[2]);
+    see(std::fabs(w[0]) + std::fabs(w[3]) + std::fabs(w[4]));
+    see(std::fabs(w[1]) + std::fabs(w[3]) + std::fabs(w[4]));
   }
   for (size_t i = 0; i < 3 * (size_t)B; i++) {
-    if (a && i % 3 != 2) m = std::max(m, std::fabs(a[i]));
-    if (b && i % 3 != 2) m = std::max(m, std::fabs(b[i]));
+    if (a) i % 3 != 2 ? see(a[i]) : (void)(finite &= std::isfinite(a[i]));
+    if (b) i % 3 != 2 ? see(b[i]) : (void)(finite &= std::isfinite(b[i]));
   }
-  D->cull = m <= HA_CULL_MAX;  // NaN: off
+  D->cull = finite && m <= HA_CULL_MAX;
 }
 
 int need_prims(mp_ctx* ctx, const mp_ha_params* p) {

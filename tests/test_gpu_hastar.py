@@ -244,6 +244,36 @@ def test_translated_scene_bitexact(ctx, shift, cull):
     assert ref["pops"] > 1
 
 
+def test_sat_cull_guard_non_finite(ctx):
+    """A NaN or infinite coordinate, length or heading anywhere in a call's inputs turns the SAT culls off
+    (mp_ha_sat_cull_active 0): std::max would drop a NaN, so the guard tracks finiteness itself."""
+    import ctypes
+
+    from motionplanning_amd.abi import ptr
+
+    h = ha.driver_searcher(ha.PERPENDICULAR)
+    p = ha.params_of(h)
+    ha.install_primitives(h, ctx)
+    W0 = np.array(h.s.obstacle_list, float)[None]
+    a0 = np.array(h.s.starting_states, float)[None]
+    b0 = np.array(h.s.ending_states, float)[None]
+
+    def active(W, a, b):
+        on = ctypes.c_int32(-1)
+        ctx.check(ctx.lib.mp_ha_sat_cull_active(ctx.handle, ctypes.byref(p), 1, ptr(W), ptr(a), ptr(b),
+                                                ctypes.byref(on)))
+        return on.value
+
+    assert active(W0, a0, b0) == 1
+    for bad in (np.nan, np.inf, -np.inf):
+        for where in ("wall_x", "wall_len", "wall_psi", "start_x", "start_psi", "goal_y"):
+            W, a, b = W0.copy(), a0.copy(), b0.copy()
+            {"wall_x": lambda: W.__setitem__((0, 1, 0), bad), "wall_len": lambda: W.__setitem__((0, 0, 3), bad),
+             "wall_psi": lambda: W.__setitem__((0, 2, 2), bad), "start_x": lambda: a.__setitem__((0, 0), bad),
+             "start_psi": lambda: a.__setitem__((0, 2), bad), "goal_y": lambda: b.__setitem__((0, 1), bad)}[where]()
+            assert active(W, a, b) == 0, (bad, where)
+
+
 def test_primitive_table_memo(ctx):
     """mp_ha_neighbor_origin keeps the installed table while the settings repeat (plan_batch calls it every
     time): a repeat returns the same table, different settings install their own (each vs the oracle), and a
