@@ -5,11 +5,13 @@ S scenes per GPU (default 8 = the per-GPU shard of configs[4], "64 scenes sharde
 8xMI355X"); every scene is configs[1]: K=8192 rollouts, H=50 horizon steps, 7-state
 dynamic bicycle, 100x100 occupancy grid, device Philox noise, the full
 TrajectoryCollection (every rollout's trajectory and control list) written to HBM,
-weights + MPPICtrl + final rollout.  One plan launch per step on the context stream (Philox
-noise drawn inside the rollout loop) + the final rollout of MPPICtrl on the side stream
-(final_stream=1; --final-inline keeps it in the plan kernel),
-so step i's serial final rollout overlaps step i+1's rollouts; every step's outputs are
-complete when the timed region's closing synchronize returns.  Inputs
+weights + MPPICtrl + final rollout.  One plan launch per step (Philox noise drawn inside the
+rollout loop) + the final rollout of MPPICtrl on its context's side stream (final_stream=1;
+--final-inline keeps it in the plan kernel); consecutive steps are independent batches and
+alternate over --streams contexts (default 2, one stream each: step i+1's rollouts fill the SIMDs
+step i's last waves leave idle), so step i's serial final rollout and its straggler waves overlap
+step i+1's rollouts; every step's outputs are complete when the timed region's closing
+synchronize returns.  Inputs
 are resident in HBM before the timed region.  N>1: one process per GPU, each
 solves its own S scenes (weak scaling) and the ranks all-gather the optimal
 controls over RCCL (the north star's exchange step).  The single-scene
@@ -48,6 +50,8 @@ def parse():
     ap.add_argument("--rotate", type=int, default=3, help="output buffer sets rotated (>256 MB MALL at S=8)")
     ap.add_argument("--no-single", action="store_true", help="skip the single-scene (configs[1]) line")
     ap.add_argument("--no-whole", action="store_true", help="skip the configs[4]-whole (64 scenes, one GPU) line")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="contexts (streams) the headline's consecutive independent plan calls alternate over")
     ap.add_argument("--roofline", default=os.path.join(ROOT, "profiles", "roofline_latest.json"),
                     help="per-kernel VALU counts + durations (tools/pmc_roofline.py) for the iLQR / HA* rooflines")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
@@ -100,10 +104,13 @@ def gather_f64(vals, dev):
     return [p.tolist() for p in parts]
 
 
-def run(a, S, ctx, dev, world, rank, steps, warmup, rotate, cfg5=True):
+def run(a, S, ctx, dev, world, rank, steps, warmup, rotate, cfg5=True, nstreams=1):
     """Time `steps` plan calls of S scenes; returns (elapsed_s_max, kernel_ms_mean, valid, K, H, fc, fields).
     cfg5: the scenes are rank r's block [rS, (r+1)S) of configs[4]'s 64 (own X0 and own obstacle_field.mat
-    grid each, configs.cfg5_shard); else S copies of configs[1]'s scene."""
+    grid each, configs.cfg5_shard); else S copies of configs[1]'s scene.
+    nstreams > 1: consecutive (independent) calls alternate over that many contexts -- one stream each --
+    so call i+1's rollouts fill the SIMDs call i's last waves leave idle (the straggler window of a lone
+    launch); each call's outputs are complete when the closing synchronize returns."""
     from motionplanning_amd import configs
     from motionplanning_amd.abi import MP_NOISE_PHILOX, ptr
 
@@ -124,8 +131,15 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate, cfg5=True):
     dX0, dgoal = t(X0), t(goal)
     dun = t(np.zeros((S, H, 2)))
     dgrid = t(grid, torch.uint8)
+    from motionplanning_amd.context import Context
+    ctxs = [ctx] + [Context(ctx.device) for _ in range(nstreams - 1)]
+    for c_ in ctxs[1:]:
+        c_.lib.mp_ctx_kernel_timing(c_.handle, 1)
+    tstreams = [torch.cuda.ExternalStream(c_.stream, device=dev) for c_ in ctxs]
     sets = []
-    for _ in range(max(1, rotate)):
+    # output sets: a multiple of the stream count, so two calls in flight on different streams never share one
+    nsets = -(-max(1, rotate) // nstreams) * nstreams
+    for _ in range(nsets):
         sets.append(dict(
             U=torch.empty((S, H, 2), dtype=torch.float64, device=dev),
             traj=torch.empty((S, H + 1, 7), dtype=torch.float64, device=dev),
@@ -138,45 +152,61 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate, cfg5=True):
             ccost=torch.empty((S, K), dtype=torch.float64, device=dev),
             cfeas=torch.empty((S, K), dtype=torch.uint8, device=dev),
         ))
-    gathered = torch.empty((world * S, H, 2), dtype=torch.float64, device=dev)
+    gathered = [torch.empty((world * S, H, 2), dtype=torch.float64, device=dev) for _ in range(nstreams)]
 
     def step(i):
         b = sets[i % len(sets)]
+        c_ = ctxs[i % nstreams]
         p.offset = i
-        ctx.check(ctx.lib.mp_mppi_plan_dev(
-            ctx.handle, ctypes.byref(p), S, ptr(dX0), ptr(dgoal), ptr(dun), None, ptr(dgrid), None, ptr(b["U"]),
+        c_.check(c_.lib.mp_mppi_plan_dev(
+            c_.handle, ctypes.byref(p), S, ptr(dX0), ptr(dgoal), ptr(dun), None, ptr(dgrid), None, ptr(b["U"]),
             ptr(b["traj"]), ptr(b["cost"]), ptr(b["feas"]), ptr(b["rc"]), ptr(b["fc"]), ptr(b["ctraj"]),
             ptr(b["cctrl"]), ptr(b["ccost"]), ptr(b["cfeas"])))
         if world > 1 and dist.get_backend() == "nccl":
-            dist.all_gather_into_tensor(gathered, b["U"])  # RCCL, on the library's stream
+            with torch.cuda.stream(tstreams[i % nstreams]):  # RCCL, on the stream of the call's context
+                dist.all_gather_into_tensor(gathered[i % nstreams], b["U"])
         elif world > 1:  # --share-device rehearsal over gloo: host copies
             parts = [torch.empty((S, H, 2), dtype=torch.float64) for _ in range(world)]
             dist.all_gather(parts, b["U"].cpu())
-            gathered.copy_(torch.cat(parts))
+            gathered[i % nstreams].copy_(torch.cat(parts))
+
+    def sync():
+        for c_ in ctxs:
+            c_.check(c_.lib.mp_ctx_synchronize(c_.handle))
+        torch.cuda.synchronize()
+
+    def kernel_ms():  # summed HIP-event spans and launch counts over the contexts (resets them)
+        tot, n = 0.0, 0
+        for c_ in ctxs:
+            ms, cnt = ctypes.c_double(), ctypes.c_int32()
+            c_.check(c_.lib.mp_ctx_kernel_ms(c_.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+            tot, n = tot + ms.value, n + cnt.value
+        return tot, n
 
     for i in range(warmup):
         step(i)
-    torch.cuda.synchronize()
-    ms, cnt = ctypes.c_double(), ctypes.c_int32()
-    ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))  # drop warmup events
+    sync()
+    kernel_ms()  # drop the warmup events
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(steps):
         step(warmup + i)
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
-    kern_ms = ms.value / max(1, cnt.value)
+    ms_sum, cnt = kernel_ms()
+    kern_ms = ms_sum / max(1, cnt)
     ok = all(bool((b["rc"] == K + 1).all().item()) and bool(torch.isfinite(b["cost"]).all().item())
              for b in sets[: min(len(sets), warmup + steps)])
     if world > 1:
         rows = gather_f64([elapsed, kern_ms, 0.0 if ok else 1.0], dev)
         elapsed, kern_ms = max(r[0] for r in rows), max(r[1] for r in rows)
         ok = all(r[2] == 0.0 for r in rows)
+    for c_ in ctxs[1:]:
+        c_.close()
     return elapsed, kern_ms, ok, K, H, p.feasibility_count, fields
 
 
@@ -222,10 +252,15 @@ def main():
         extras["ilqr"] = bench_ilqr(ctx, world, rank, cpu=cpu_jobs)
         extras["hybrid_astar"] = bench_hastar(ctx, world, rank, cpu=cpu_jobs)
         extras["closed_loop"] = bench_closed_loop(ctx, world, rank, cpu=cpu_jobs)
-    elapsed, kern_ms, ok, K, H, fc, fields = run(a, S, ctx, dev, world, rank, a.steps, a.warmup, a.rotate)
+    elapsed, kern_ms, ok, K, H, fc, fields = run(a, S, ctx, dev, world, rank, a.steps, a.warmup, a.rotate,
+                                                 nstreams=max(1, a.streams))
     value = world * S * K * H * a.steps / elapsed
     nbytes = algorithmic_bytes(S, K, H)
-    achieved = nbytes / (kern_ms * 1e-3) / 1e9
+    # the device time per launch: with one stream the launch's own HIP-event span; with several the launches
+    # overlap (each span covers the time it shares the device), so the timed region per step -- an upper bound
+    # on the device time per launch, idle gaps included
+    t_launch = kern_ms if a.streams <= 1 else elapsed / a.steps * 1e3
+    achieved = nbytes / (t_launch * 1e-3) / 1e9
     out = {
         "metric": BASE["metric"],
         "value": value,
@@ -253,6 +288,7 @@ def main():
             "K": K, "H": H, "scenes_per_gpu": S, "feasibility_count": fc,
             "final_rollout": "in plan kernel" if a.final_inline else
                              "side stream (final_stream=1): overlaps the next step's rollouts",
+            "streams": max(1, a.streams),
             "parallelism": f"scene-sharded x{world}" + ((" + gloo all_gather(MPPICtrl), all ranks on cuda:0 "
                                                           "(--share-device rehearsal)") if a.share_device and world > 1
                                                          else " + RCCL all_gather(MPPICtrl)" if world > 1 else ""),
@@ -261,6 +297,12 @@ def main():
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
             "kernel": "mppi_plan_kernel", "kernel_ms": kern_ms, "algorithmic_bytes": nbytes,
+            "launches_in_flight": max(1, a.streams), "device_ms_per_launch": t_launch,
+            "time_basis": ("kernel_ms: the mean HIP-event span of one launch (rocprofv3's average duration); "
+                           "achieved divides by device_ms_per_launch = " +
+                           ("kernel_ms" if a.streams <= 1 else
+                            f"timed region / steps ({a.streams} launches in flight on {a.streams} streams overlap, "
+                            "so one launch's span is ~that many device times per launch)")),
         },
         "valid": ok,
         # what ran before the timed region (round-4+ headlines are timed on a warm GPU, earlier
@@ -286,7 +328,7 @@ def main():
             # for 4 cycles (78.6 TF fp64 vector = 1024 SIMDs x 2.4 GHz x 16 FMA lanes x 2), so the
             # chip issues at most 1024 * 2.4e9 / 4 = 6.14e11 wave-level fp64 instructions per s.
             peak = VALU_SIMDS * VALU_CLOCK_HZ / FP64_ISSUE_CYCLES
-            rate = tr["valu_insts"] / (kern_ms * 1e-3)
+            rate = tr["valu_insts"] / (t_launch * 1e-3)
             out["roofline"]["valu"] = {
                 "insts_per_launch": tr["valu_insts"], "achieved": rate, "peak": peak, "unit": "wave-insts/s",
                 "frac": rate / peak, "source": tr["source"] + " SQ_INSTS_VALU",

@@ -1,6 +1,8 @@
 """Device context: one libmpgpu mp_ctx per (process, GPU)."""
+import atexit
 import ctypes
 import threading
+import weakref
 
 from .abi import MP_OK, MPGPUError, load_library
 
@@ -18,6 +20,7 @@ class Context:
             raise MPGPUError(st, self.lib.mp_last_error(None).decode())
         self.handle = h
         self.device = device
+        _live.add(self)
 
     def check(self, st):
         if st != MP_OK:
@@ -85,6 +88,20 @@ class CommGroup:
     def __del__(self):
         try:
             self.close()
+        except Exception:
+            pass
+
+
+_live = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    """Destroy every context still open at interpreter exit (synchronised, workspaces and streams released)
+    while the HIP runtime is still up, instead of leaving them to garbage collection after it."""
+    for c in list(_live):
+        try:
+            c.close()
         except Exception:
             pass
 
