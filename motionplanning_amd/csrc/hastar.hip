@@ -732,12 +732,13 @@ __device__ __forceinline__ int wait_ge(const int* p, int v, int* err) {
 // data IS the flag): 14 one-word {tag = iteration + 1, value} records -- the state's and the stored commands'
 // six double halves each, the winner word, the go bit -- each written by ONE agent-scope 8-byte store of its
 // own lane, so the bookkeeping neither drains its stores nor raises a separate flag, and a consumer wave polls
-// the 14 words until every tag matches (one round trip instead of flag + node).  HA_NGR_DONE in the go word:
-// the scene's search ended.
+// the 14 words until every tag matches (one round trip instead of flag + node).  HA_NGR_DONE in the go word's
+// tag: the scene's search ended.  The go word's value: bit 0 go (a node follows), bit 1 skip (the consumer has
+// nothing to do this round: the node's expansion was made speculatively, or no runner-up exists; HA_SPEC).
 constexpr int HA_NGR = 16;
 constexpr unsigned HA_NGR_DONE = 0xffffffffu;
 __device__ __forceinline__ void ha_publish_node(unsigned long long* g, unsigned tag, int lane, const long long* w,
-                                                bool go) {
+                                                unsigned go) {
   if (lane >= 14) return;
   unsigned v;
   if (lane < 6) v = (unsigned)((unsigned long long)w[3 + (lane >> 1)] >> (32 * (lane & 1)));  // state
@@ -746,7 +747,8 @@ __device__ __forceinline__ void ha_publish_node(unsigned long long* g, unsigned 
   else v = go;
   __hip_atomic_store(g + lane, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// wave 0 of a consumer block; returns go (0: the search ended or the wait ran out), the node in st / tuv / rw
+// wave 0 of a consumer block; returns the go word (0: the search ended or the wait ran out; bit 1: skip), the
+// node in st / tuv / rw
 __device__ __forceinline__ int ha_consume_node(const unsigned long long* g, unsigned tag, int lane, double* st,
                                                double* tuv, int* rw, int* err) {
   unsigned long long x = 0;
@@ -1082,6 +1084,7 @@ __device__ __forceinline__ bool ha_iter_body(const HaDev& P, const IterArgs& A, 
       }
       __syncthreads();
       if (!nd_go) return false;  // block-uniform: the search ended, nothing to expand
+      if (nd_go & 2) return true;  // block-uniform: nothing to do this round (HA_SPEC: expanded speculatively)
     } else {
       if (tid == 0) nd_go = wait_ge(A.node_flag + s, A.node_flag_min, A.node_flag_err) & 1;
       __syncthreads();
@@ -1702,6 +1705,11 @@ struct HaSearch {
   int* ex;               // [B] (ha_persist_kernel) expansions finished (neighbour groups, cumulative)
   int* rsr;              // [B] (ha_persist_kernel) 2·it + 2 once RS_connected(n_it) has run
   int* err;              // [1] (ha_persist_kernel) a bounded wait ran out (the search is then not trusted)
+  // (ha_persist_kernel, HA_SPEC) the runner-up: popfirst!'s second-least entry when n_{it+1} is popped, the
+  // candidate for n_{it+2}, expanded (and RS_connected) speculatively
+  unsigned long long* ngr2;  // [2][B][HA_NGR] the runner-up as tagged granules, by parity
+  int* exs;              // [B] speculative expansions finished (neighbour groups, cumulative)
+  int* rsrs;             // [B] 2·it + 2 once RS_connected(r_it) has run
 };
 // prescan record: [0] iteration tag, [1] kc = min(K, n_open), then K entries of 13 words: f (bits), seq, position,
 // node id, g (bits), Encode index, state (3, bits), rw, (t, u, v) (3, bits)
@@ -2867,10 +2875,17 @@ __device__ __forceinline__ IterArgs e_par(const IterArgs& A, int B, int np, int 
 }
 
 // pre_wait (ha_persist_kernel): the wait for this iteration's expansion records, run after the open list's loads
-// are issued (the list stands as the previous iteration's bookkeeping left it) so they land meanwhile
-template <int NT, bool RSH = true, class Wait = NoMid>
+// are issued (the list stands as the previous iteration's bookkeeping left it) so they land meanwhile.
+// SPEC (ha_persist_kernel, HA_SPEC): also the runner-up -- the second-least of popfirst!'s candidates, which is
+// the next pop unless one of the popped node's children beats it (87 % of the pops of configs[3]) -- published
+// as Q.ngr2 granules after the writes; sr (LDS, kept by the caller across iterations) holds the previous one
+// (10 payload words + valid), and the pop's go word carries skip = hit (the popped node IS the previous
+// runner-up, identical id, state and stored commands: its expansion and RS_connected were made speculatively);
+// *hit_out returns it.
+template <int NT, bool RSH = true, class Wait = NoMid, bool SPEC = false>
 __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& Q, const IterArgs& E, int B, int it,
-                                                int b, unsigned long long* stp = nullptr, const Wait& pre_wait = Wait()) {
+                                                int b, unsigned long long* stp = nullptr, const Wait& pre_wait = Wait(),
+                                                long long* sr = nullptr, int* hit_out = nullptr) {
 #define PSTAMP(i) if (stp) __hip_atomic_store(stp + (i), __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
   constexpr int SC = 4;  // open entries per thread held in registers (more are re-read)
   __shared__ int s_nopen, s_nnew, s_nchg, s_go;
@@ -2881,7 +2896,7 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
   __shared__ long long r_s[NT / 64];
   __shared__ int r_p[NT / 64];
   __shared__ long long r_pay[NT / 64][11];  // each wave winner's payload: id, g, ix, st[3], rw, tuv[3]
-  __shared__ long long s_win[12];           // the pop's winner: payload as r_pay, position
+  __shared__ long long s_win[12];           // the pop's winner: payload as r_pay, position, (SPEC) hit
   static_assert(NT >= 256 && NT / 64 <= 16, "four waves for the duplicate check, the wave winners fit a row");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * Q.C;
@@ -3058,19 +3073,29 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
     for (int i = 0; i < nchg; i++) c |= s_chg[i] == p;
     return c;
   };
-  double bf = __builtin_inf();
-  long long bs = 0x7fffffffffffffffLL;
-  int bp = -1;
+  double bf = __builtin_inf(), bf2 = __builtin_inf();
+  long long bs = 0x7fffffffffffffffLL, bs2 = 0x7fffffffffffffffLL;
+  int bp = -1, bp2 = -1;  // (SPEC) the thread's second-least too
+  auto consider = [&](double f, long long sq, int p) {
+    if (bp < 0 || key_before(f, sq, bf, bs)) {
+      if (SPEC) { bf2 = bf; bs2 = bs; bp2 = bp; }
+      bf = f; bs = sq; bp = p;
+    } else if (SPEC && (bp2 < 0 || key_before(f, sq, bf2, bs2))) {
+      bf2 = f; bs2 = sq; bp2 = p;
+    }
+  };
 #pragma unroll
   for (int u = 0; u < SC; u++) {
     const int p = tid + u * NT;
-    if (p < n_open0 && !changed(p) && (bp < 0 || key_before(fv[u], sv[u], bf, bs))) { bf = fv[u]; bs = sv[u]; bp = p; }
+    if (p < n_open0 && !changed(p)) consider(fv[u], sv[u], p);
   }
   for (int p = tid + SC * NT; p < n_open0; p += NT) {  // long lists: the rest re-read
     const double f = Q.of[base + p];
     const long long sq = Q.oseq[base + p];
-    if (!changed(p) && (bp < 0 || key_before(f, sq, bf, bs))) { bf = f; bs = sq; bp = p; }
+    if (!changed(p)) consider(f, sq, p);
   }
+  const double own_f = bf;  // (SPEC) the thread's least, before the reductions overwrite bf / bs / bp
+  const long long own_s = bs;
   // the thread's own best entry's payload, its latency behind the reductions
   long long pay[11];
 #pragma unroll
@@ -3153,13 +3178,22 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the winner's LDS writes before the wave reads them
+    // (SPEC) the pop is the previous runner-up: same node id, state and stored commands (the inputs of its
+    // expansion and of RS_connected), so both were made speculatively
+    bool hit = false;
+    if (SPEC && go && sr[10]) {
+      hit = s_win[0] == sr[0];
+#pragma unroll
+      for (int e = 3; e < 10; e++) hit = hit && s_win[e] == sr[e];
+    }
     if (RSH && E.ngr_pub) {
       // publish the next node as tagged granules (ha_publish_node): no drain, no separate flag; the node
       // buffers too, for the next launch's RS_connected (a launch boundary orders those)
       long long wv[10];
 #pragma unroll
       for (int e = 0; e < 10; e++) wv[e] = go ? s_win[e] : 0;
-      ha_publish_node(Q.ngr + ((size_t)(it & 1) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv, go);
+      ha_publish_node(Q.ngr + ((size_t)(it & 1) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv,
+                      go ? 1u | (hit ? 2u : 0u) : 0u);
       if (go && lane < 3) {
         Q.node[(size_t)(it & 1) * 3 * B + 3 * b + lane] = __longlong_as_double(s_win[3 + lane]);
         Q.node_tuv[(size_t)(it & 1) * 3 * B + 3 * b + lane] = __longlong_as_double(s_win[7 + lane]);
@@ -3182,6 +3216,7 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
     if (lane == 0) {
       s_go = go;
       s_win[10] = wpos;
+      if (SPEC) s_win[11] = hit;
     }
     PSTAMP(8);
     // ---- FindNewNode's writes (as ha_book_spec)
@@ -3270,6 +3305,92 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
     }
   }
   __syncthreads();
+  if (SPEC) {
+    // ---- the runner-up: the least of the same candidates without the winner -- each thread's least old entry
+    // (its second when its least won), the waves' minima, then wave 0 with the lanes' changed / appended entries
+    __shared__ double u_f[NT / 64];
+    __shared__ long long u_s[NT / 64];
+    __shared__ int u_p[NT / 64];
+    const int wpos = (int)s_win[10];
+    if (s_go) {  // block-uniform
+      double cf = own_f;
+      long long cs = own_s;
+      int cp = own;
+      if (own >= 0 && own == wpos) { cf = bf2; cs = bs2; cp = bp2; }
+      key_min_dpp<0xB1>(cf, cs, cp);
+      key_min_dpp<0x4E>(cf, cs, cp);
+      key_min_dpp<0x141>(cf, cs, cp);
+      key_min_dpp<0x140>(cf, cs, cp);
+      double wf = __longlong_as_double(readlane_l(__double_as_longlong(cf), 0));
+      long long ws = readlane_l(cs, 0);
+      int wp_ = __builtin_amdgcn_readlane(cp, 0);
+#pragma unroll
+      for (int q = 1; q < 4; q++) {
+        const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(cf), 16 * q));
+        const long long os = readlane_l(cs, 16 * q);
+        const int op = __builtin_amdgcn_readlane(cp, 16 * q);
+        if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
+      }
+      if (lane == 0) { u_f[wave] = wf; u_s[wave] = ws; u_p[wave] = wp_; }
+    }
+    __syncthreads();
+    if (s_go && tid < 64) {
+      double cf = __builtin_inf();
+      long long cs = 0x7fffffffffffffffLL;
+      int cp = -1, src = -1;
+      if (lane < NT / 64 && u_p[lane] >= 0) { cf = u_f[lane]; cs = u_s[lane]; cp = u_p[lane]; src = lane; }
+      if (myp >= 0 && myp != wpos && (cp < 0 || key_before(tf, nseq, cf, cs))) { cf = tf; cs = nseq; cp = myp; src = 64 + lane; }
+      const int mine = cp, msrc = src;
+      key_min_dpp<0xB1>(cf, cs, cp);
+      key_min_dpp<0x4E>(cf, cs, cp);
+      key_min_dpp<0x141>(cf, cs, cp);
+      key_min_dpp<0x140>(cf, cs, cp);
+      double wf = __longlong_as_double(readlane_l(__double_as_longlong(cf), 0));
+      long long ws = readlane_l(cs, 0);
+      int rpos = __builtin_amdgcn_readlane(cp, 0);
+#pragma unroll
+      for (int q = 1; q < 4; q++) {
+        const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(cf), 16 * q));
+        const long long os = readlane_l(cs, 16 * q);
+        const int op = __builtin_amdgcn_readlane(cp, 16 * q);
+        if (op >= 0 && (rpos < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; rpos = op; }
+      }
+      if (rpos >= 0 && mine == rpos) {  // the owner lane: its own values, or the old entry (this block wrote it)
+        if (msrc >= 64) {
+          sr[0] = id;
+          sr[1] = __double_as_longlong(tg);
+          sr[2] = nix;
+          sr[3] = __double_as_longlong(nst0);
+          sr[4] = __double_as_longlong(nst1);
+          sr[5] = __double_as_longlong(nst2);
+          sr[6] = nrw;
+          sr[7] = __double_as_longlong(nt0);
+          sr[8] = __double_as_longlong(nt1);
+          sr[9] = __double_as_longlong(nt2);
+        } else {
+          const size_t q = base + rpos;
+          sr[0] = Q.oid[q];
+          sr[1] = __double_as_longlong(Q.og[q]);
+          sr[2] = Q.oix[q];
+#pragma unroll
+          for (int e = 0; e < 3; e++) sr[3 + e] = __double_as_longlong(Q.ost[q * 3 + e]);
+          sr[6] = Q.orw[q];
+#pragma unroll
+          for (int e = 0; e < 3; e++) sr[7 + e] = __double_as_longlong(Q.otuv[q * 3 + e]);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the owner's LDS writes before the wave reads
+      const bool valid = rpos >= 0;
+      long long wv[10];
+#pragma unroll
+      for (int e = 0; e < 10; e++) wv[e] = valid ? sr[e] : 0;
+      // skip (no runner-up): the speculative blocks count the round and wait for the next one
+      ha_publish_node(Q.ngr2 + ((size_t)(it & 1) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv, valid ? 1u : 3u);
+      if (lane == 0) sr[10] = valid;
+    }
+    if (hit_out) *hit_out = s_go ? (int)s_win[11] : 0;
+    __syncthreads();  // sr and s_win reused by the next iteration
+  }
   BookRec br;
   br.v[RC_GO] = s_go;
   br.v[RC_LOOP] = loop;
@@ -3494,22 +3615,35 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
 // parity buffer); the bookkeeping of iteration it waits for E[it & 1] and RS_connected(n_it) and finishes the
 // iteration as ha_step_kernel's finisher.  A finished scene publishes HA_DONE: every block of it leaves its loop.
 // Same operations on the same values as ha_pipe_kernel: the same search, bit for bit.  Every wait is bounded.
-template <int HWt, int NBGt>
+// HA_SPEC (default 1): the speculative runner-up (ha_book_pipe<..., SPEC>).  The bookkeeping of iteration it also
+// publishes r_{it+1}, the second-least of popfirst!'s candidates (Q.ngr2): the next pop is r_{it+1} or one of
+// n_{it+1}'s children (the least of the two), and in configs[3] it is r_{it+1} for 87 % of the pops.  The
+// expansion groups, after n_{it+1}, expand r_{it+1} into E slot 2 + ((it+1) & 3) (Q.exs), the RS block, after
+// RS_connected(n_it), runs RS_connected(r_it) into RS slot 2 + (it & 3) (Q.rsrs).  When the pop IS the runner-up
+// (same node id, state and stored commands: the inputs of both), its granules carry skip, the groups and the RS
+// block skip it and the bookkeeping reads the speculative records instead: the lone chain per iteration is then
+// the bookkeeping (~10 us) instead of expansion + bookkeeping (~18.5 us).  The same records, the same decisions:
+// the search is bit for bit the same (the expansion and RS_connected are functions of the node alone).
+#ifndef HA_SPEC
+#define HA_SPEC 1
+#endif
+template <int HWt, int NBGt, bool SPEC = HA_SPEC>
 __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == HW_TAIL ? HA_WPE_TAIL : 3))) void ha_persist_kernel(
     HaDev P, HaSearch Q, IterArgs A, int B, int it0, double* rs_path2, unsigned char* rs_ok2, int* rs_len2) {
   __shared__ int sh_f;
+  __shared__ long long sh_run[12];  // (SPEC, the bookkeeping block) the last runner-up: payload + valid
   const int np = P.n_prim, ng = (np + NBGt - 1) / NBGt, per = 2 + ng;
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
   const int n_live = A.n_live ? *A.n_live : A.n_active;
   if (slot >= n_live) return;
   const int s = A.scene_of ? A.scene_of[slot] : slot;
   if (!A.n_live && A.active && !A.active[s]) return;
-  // RS_connected's outputs in the iteration's parity (the next iteration's may be written before the
-  // bookkeeping reads this one's)
-  auto rs_par = [&](IterArgs& X, int it) {
-    X.rs_ok = rs_ok2 + (size_t)(it & 1) * B;
-    X.rs_len = rs_len2 + (size_t)(it & 1) * B;
-    X.rs_path = rs_path2 + (size_t)(it & 1) * B * MAXPATH * 3;
+  // RS_connected's outputs by slot: 0 / 1 the pop's (iteration parity), 2..5 the runner-up's (SPEC, it & 3) -- the
+  // next iteration's may be written before the bookkeeping reads this one's
+  auto rs_slot = [&](IterArgs& X, int k) {
+    X.rs_ok = rs_ok2 + (size_t)k * B;
+    X.rs_len = rs_len2 + (size_t)k * B;
+    X.rs_path = rs_path2 + (size_t)k * B * MAXPATH * 3;
   };
   // (HA_STAMP_CODE builds, MPGPU_HA_STAMPS=1) this block's stamp record for iteration it, as ha_step_kernel's
   auto pst = [&](int it) -> unsigned long long* {
@@ -3522,93 +3656,100 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   auto put = [](unsigned long long* p, int i, unsigned long long v) {
     if (p) __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  // (A/B build -DHA_PERSIST_PRIO=1) where blocks of several scenes share a CU, issue priority by role -- the
-  // bookkeeping 2 and the expansion 1 (the scene's chain), RS_connected 0 (beside it): neutral (r05zr), off
-#ifndef HA_PERSIST_PRIO
-#define HA_PERSIST_PRIO 0
-#endif
-  if (HA_PERSIST_PRIO) {
-    if (item == 0) __builtin_amdgcn_s_setprio(0);
-    else if (item == 1) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(1);
-  }
-  if (item >= 2) {  // the expansion of n_{it+1}, it = it0, it0 + 1, ...
+  if (item >= 2) {  // the expansion of n_{it+1} (skipped when it is the runner-up), then (SPEC) of r_{it+1}
     for (int it = it0;; it++) {
-      IterArgs X = e_par(A, B, np, (it + 1) & 1);
-      X.node = Q.node + (size_t)(it & 1) * 3 * B;
-      X.node_ag = 1;
-      X.node_flag = Q.nx;
-      X.node_flag_min = 2 * it + 2;
-      X.node_flag_err = Q.err;
-      if (A.ngr_pub) {
-        X.ngr = Q.ngr + (size_t)(it & 1) * B * HA_NGR;
-        X.ngr_tag = (unsigned)it + 1;
-      }
-      X.do_rs = 0;
-      unsigned long long* stp = pst(it);
-      put(stp, 0, now());
-      if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 1)) return;  // the search ended
-      ha_stores_done();
-      __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_fetch_add(Q.ex + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      put(stp, 1, now());
-      put(stp, 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 1) << 32));
-    }
-  }
-  if (item == 0) {  // RS_connected(n_it), it = it0, it0 + 1, ...
-    for (int it = it0;; it++) {
-      IterArgs X = A;
-      X.node = Q.node + (size_t)((it - 1) & 1) * 3 * B;
-      X.node_rw = Q.node_rw + (size_t)((it - 1) & 1) * B;
-      X.node_tuv = Q.node_tuv + (size_t)((it - 1) & 1) * 3 * B;
-      if (it > it0) {  // n_it: published by iteration it - 1's bookkeeping in this launch
+      for (int job = 0; job < (SPEC ? 2 : 1); job++) {  // (one body for both: a loop, not two inlined copies)
+        const bool r = SPEC && job == 1;
+        IterArgs X = e_par(A, B, np, r ? 2 + ((it + 1) & 3) : (it + 1) & 1);
+        X.node = Q.node + (size_t)(it & 1) * 3 * B;
         X.node_ag = 1;
         X.node_flag = Q.nx;
-        X.node_flag_min = 2 * (it - 1) + 2;
+        X.node_flag_min = 2 * it + 2;
         X.node_flag_err = Q.err;
-        if (A.ngr_pub) {
-          X.ngr = Q.ngr + (size_t)((it - 1) & 1) * B * HA_NGR;
-          X.ngr_tag = (unsigned)it;
+        if (A.ngr_pub || r) {
+          X.ngr = (r ? Q.ngr2 : Q.ngr) + (size_t)(it & 1) * B * HA_NGR;
+          X.ngr_tag = (unsigned)it + 1;
         }
+        X.do_rs = 0;
+        unsigned long long* stp = r ? nullptr : pst(it);
+        put(stp, 0, now());
+        if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 1)) return;  // the search ended
+        ha_stores_done();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add((r ? Q.exs : Q.ex) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        put(stp, 1, now());
+        put(stp, 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 1) << 32));
       }
-      rs_par(X, it);
-      X.do_exp = 0;
-      unsigned long long* stp = pst(it);
-      put(stp, 0, now());
-      if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, 0)) return;
-      ha_stores_done();
-      __syncthreads();
-      if (threadIdx.x == 0) st_ag(Q.rsr + s, 2 * it + 2);
-      put(stp, 1, now());
-      put(stp, 5, 2ull | ((unsigned long long)s << 4));
+    }
+  }
+  if (item == 0) {  // RS_connected(n_it) (skipped when it is the runner-up), then (SPEC) RS_connected(r_it)
+    for (int it = it0;; it++) {
+      for (int job = 0; job < (SPEC && it > it0 ? 2 : 1); job++) {  // r_it: published by iteration it - 1 too
+        const bool r = SPEC && job == 1;
+        IterArgs X = A;
+        X.node = Q.node + (size_t)((it - 1) & 1) * 3 * B;
+        X.node_rw = Q.node_rw + (size_t)((it - 1) & 1) * B;  // (with granules: non-null = use the stored winner)
+        X.node_tuv = Q.node_tuv + (size_t)((it - 1) & 1) * 3 * B;
+        if (it > it0) {  // n_it / r_it: published by iteration it - 1's bookkeeping in this launch
+          X.node_ag = 1;
+          X.node_flag = Q.nx;
+          X.node_flag_min = 2 * (it - 1) + 2;
+          X.node_flag_err = Q.err;
+          if (A.ngr_pub || r) {
+            X.ngr = (r ? Q.ngr2 : Q.ngr) + (size_t)((it - 1) & 1) * B * HA_NGR;
+            X.ngr_tag = (unsigned)it;
+          }
+        }
+        rs_slot(X, r ? 2 + (it & 3) : it & 1);
+        X.do_exp = 0;
+        unsigned long long* stp = r ? nullptr : pst(it);
+        put(stp, 0, now());
+        if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, 0)) return;
+        ha_stores_done();
+        __syncthreads();
+        if (threadIdx.x == 0) st_ag((r ? Q.rsrs : Q.rsr) + s, 2 * it + 2);
+        put(stp, 1, now());
+        put(stp, 5, 2ull | ((unsigned long long)s << 4));
+      }
     }
   }
   // item 1: the bookkeeping of iteration it, it = it0, it0 + 1, ...
+  if (SPEC && threadIdx.x < 12) sh_run[threadIdx.x] = 0;  // no runner-up yet: iteration it0's pop is no hit
+  __syncthreads();
+  int hit = 0;  // (SPEC) n_it is r_{it-1}: its records and RS_connected are the speculative ones
   for (int it = it0;; it++) {
     // E[it & 1]: every group of iteration it - 1 has expanded n_it (waited for inside, the open list's loads
-    // in flight)
+    // in flight); on a hit the speculative E slot of r_{it-1} (its groups' round it - 2)
     unsigned long long* stp = pst(it);
     put(stp, 0, now());
+    const int h = hit;
     const auto wait_exp = [&] {
       if (it > it0) {
-        if (threadIdx.x == 0) wait_ge(Q.ex + s, ng * (it - it0), Q.err);
+        if (threadIdx.x == 0) {
+          if (h) wait_ge(Q.exs + s, ng * (it - 1 - it0), Q.err);
+          else wait_ge(Q.ex + s, ng * (it - it0), Q.err);
+        }
         __syncthreads();
       }
       put(stp, 2, now());  // (the book's wait for the expansion ends)
     };
+    const IterArgs Ei = e_par(A, B, np, h ? 2 + ((it - 1) & 3) : it & 1);
+    int hit_next = 0;
 #ifndef HA_PREWAIT
 #define HA_PREWAIT 1
 #endif
     if (!HA_PREWAIT) wait_exp();  // (A/B build -DHA_PREWAIT=0: the wait before the bookkeeping's first load)
-    const BookRec br = HA_PREWAIT ? ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, stp, wait_exp)
-                                  : ha_book_pipe<64 * HWt>(P, Q, e_par(A, B, np, it & 1), B, it, s, stp);
+    const BookRec br = HA_PREWAIT ? ha_book_pipe<64 * HWt, true, decltype(wait_exp), SPEC>(P, Q, Ei, B, it, s, stp,
+                                                                                        wait_exp, sh_run, &hit_next)
+                                  : ha_book_pipe<64 * HWt, true, NoMid, SPEC>(P, Q, Ei, B, it, s, stp, NoMid(),
+                                                                          sh_run, &hit_next);
     put(stp, 3, now());
     IterArgs F = A;
-    rs_par(F, it);
+    rs_slot(F, h ? 2 + ((it - 1) & 3) : it & 1);
     if (threadIdx.x == 0) {
       // RS_connected(n_it) done; Q.rsr may already hold iteration it + 1's flag (that RS block starts once this
-      // iteration's pop is published), the verdict itself stays in the parity buffer until iteration it + 2
-      const int f = wait_ge(Q.rsr + s, 2 * it + 2, Q.err);
+      // iteration's pop is published), the verdict itself stays in its slot until iteration it + 2 (+ 4: runner-up)
+      const int f = h ? wait_ge(Q.rsrs + s, 2 * (it - 1) + 2, Q.err) : wait_ge(Q.rsr + s, 2 * it + 2, Q.err);
       if (f == HA_DONE) {
         sh_f = 2;
       } else {
@@ -3628,9 +3769,13 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
       if (A.ngr_pub && threadIdx.x < 2)  // the search ended: both parities' go words (whichever is waited on)
         __hip_atomic_store(Q.ngr + ((size_t)threadIdx.x * B + s) * HA_NGR + 13,
                            (unsigned long long)HA_NGR_DONE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (SPEC && threadIdx.x >= 2 && threadIdx.x < 4)  // and the runner-up's
+        __hip_atomic_store(Q.ngr2 + ((size_t)(threadIdx.x - 2) * B + s) * HA_NGR + 13,
+                           (unsigned long long)HA_NGR_DONE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!A.ngr_pub && threadIdx.x == 0) st_ag(Q.nx + s, HA_DONE);
       return;
     }
+    hit = hit_next;
     __syncthreads();
   }
 }
@@ -4026,7 +4171,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + nB * 2 * HA_NGR * 8 + 256 * 57);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + nB * 2 * HA_NGR * 8 + 256 * 57 +
+                                           nB * 2 * HA_NGR * 8 + nB * 8 + 256 * 3);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -4074,20 +4220,25 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.err = (int*)take(4);
   Q.node_g = (double*)take(nB * 16);
   Q.node_nn = (int*)take(nB * 8);
+  Q.ngr2 = (unsigned long long*)take(nB * 2 * HA_NGR * 8);
+  Q.exs = (int*)take(nB * 4);
+  Q.rsrs = (int*)take(nB * 4);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
   const double* dstart = mp_upload(ctx, WS_IO0, start, 3 * nB, &st);
-  A.h = (double*)mp_ws(ctx, WS_IO1, sizeof(double) * nB * np * 2);
+  // the expansion records: 2 parities (E[it & 1]) + (HA_SPEC) 4 runner-up slots
+  constexpr size_t NPAR = HA_SPEC ? 6 : 2;
+  A.h = (double*)mp_ws(ctx, WS_IO1, sizeof(double) * nB * np * NPAR);
   // the expansion records (nb, idx, fr, h, hw, hp_*) hold two parities: ha_pipe_kernel's launch it reads E[it & 1]
   // while its expansion blocks write E[(it + 1) & 1]; every other launch uses parity 0
-  A.nb = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * nB * np * 3 * 2);
-  A.idx = (long long*)mp_ws(ctx, WS_IO3, sizeof(long long) * nB * np * 2);
-  A.fr = (unsigned char*)mp_ws(ctx, WS_IO4, nB * np * 2);
+  A.nb = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * nB * np * 3 * NPAR);
+  A.idx = (long long*)mp_ws(ctx, WS_IO3, sizeof(long long) * nB * np * NPAR);
+  A.fr = (unsigned char*)mp_ws(ctx, WS_IO4, nB * np * NPAR);
   A.rs_ok = (unsigned char*)mp_ws(ctx, WS_IO5, nB);
   A.rs_len = (int*)mp_ws(ctx, WS_IO6, sizeof(int) * nB);
   A.rs_path = (double*)mp_ws(ctx, WS_IO7, sizeof(double) * nB * MAXPATH * 3);
-  A.hw = (int*)mp_ws(ctx, WS_IO9, sizeof(int) * nB * np * 2);
+  A.hw = (int*)mp_ws(ctx, WS_IO9, sizeof(int) * nB * np * NPAR);
   if (st || !A.h || !A.nb || !A.idx || !A.fr || !A.rs_ok || !A.rs_len || !A.rs_path || !A.hw)
     return st ? st : MP_ERR_NOMEM;
 #ifndef HA_RS_WINNER
@@ -4176,6 +4327,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.ngr, 0, sizeof(unsigned long long) * nB * 2 * HA_NGR, ctx->stream));  // granule tags
   MP_HIP(ctx, hipMemsetAsync(Q.ex, 0, sizeof(int) * nB, ctx->stream));  // ha_persist_kernel's flags
   MP_HIP(ctx, hipMemsetAsync(Q.rsr, 0, sizeof(int) * nB, ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.ngr2, 0, sizeof(unsigned long long) * nB * 2 * HA_NGR, ctx->stream));  // (HA_SPEC)
+  MP_HIP(ctx, hipMemsetAsync(Q.exs, 0, sizeof(int) * nB, ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.rsrs, 0, sizeof(int) * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.err, 0, sizeof(int), ctx->stream));
   hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
   MP_HIP(ctx, hipGetLastError());
@@ -4199,9 +4353,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // c, so there must be a group for every (16-neighbour set, chunk) -- n_prim mod 16 in {0, 13, 14, 15} with
   // 4 neighbours per group (62: yes); otherwise the groups' own word search.
   const bool tail_rsh = HA_TAIL_RSH && NBG_TAIL == 4 && per_tail - 1 >= 4 * ((np + 15) / 16);
-  A.hp_c = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * nB * np * 4 * 2);
-  A.hp_i = (int*)mp_ws(ctx, WS_IO12, sizeof(int) * nB * np * 4 * 2);
-  A.hp_t = (double*)mp_ws(ctx, WS_IO14, sizeof(double) * nB * np * 12 * 2);
+  A.hp_c = (double*)mp_ws(ctx, WS_IO11, sizeof(double) * nB * np * 4 * NPAR);
+  A.hp_i = (int*)mp_ws(ctx, WS_IO12, sizeof(int) * nB * np * 4 * NPAR);
+  A.hp_t = (double*)mp_ws(ctx, WS_IO14, sizeof(double) * nB * np * 12 * NPAR);
   const bool tail_pipe = tail_rsh;
   // the persistent tail (ha_persist_kernel): one cooperative launch for the rest of the search once every block
   // of it fits the device at once.  Without cooperative launches (or when one is refused) the tail runs one
@@ -4243,8 +4397,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     phw = phws[v];
     persist_fn = pfn[v];
     persist_cap = pcap[v];
-    rs_path2 = (double*)mp_ws(ctx, WS_IO15, sizeof(double) * 2 * nB * MAXPATH * 3);
-    rs_i2 = (int*)mp_ws(ctx, WS_IO16, sizeof(int) * 4 * nB);
+    // RS_connected's outputs by slot (ha_persist_kernel rs_slot): NPAR slots of rs_path, rs_ok (bytes), rs_len
+    rs_path2 = (double*)mp_ws(ctx, WS_IO15, sizeof(double) * NPAR * nB * MAXPATH * 3);
+    rs_i2 = (int*)mp_ws(ctx, WS_IO16, sizeof(int) * 2 * NPAR * nB);
     if (!rs_path2 || !rs_i2) return MP_ERR_NOMEM;
   }
   bool persisted = false;
@@ -4304,7 +4459,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
         piped_any = true;
       }
       unsigned char* rs_ok2 = reinterpret_cast<unsigned char*>(rs_i2);
-      int* rs_len2 = rs_i2 + 2 * nB;
+      int* rs_len2 = rs_i2 + NPAR * nB;
       int it0 = it;
       void* args[] = {&D, &Q, &A, (void*)&B, &it0, &rs_path2, &rs_ok2, &rs_len2};
       // (MPGPU_HA_COOP=0: an ordinary launch of the same grid, co-resident by the occupancy check alone -- for
