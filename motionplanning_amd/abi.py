@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libmpgpu.so")
-LIB_PATH = os.environ.get("MPGPU_LIB", LIB_PATH)  # alternate builds (A/B experiments)
+LIB_PATH = os.environ.get("MPGPU_LIB") or LIB_PATH  # alternate builds (A/B experiments)
 
 MP_OK = 0
 MP_ERR_INVALID = 1

@@ -1710,6 +1710,7 @@ struct HaSearch {
   unsigned long long* ngr2;  // [2][B][HA_NGR] the runner-up as tagged granules, by parity
   int* exs;              // [B] speculative expansions finished (neighbour groups, cumulative)
   int* rsrs;             // [B] 2·it + 2 once RS_connected(r_it) has run
+  int* nhit;             // [2][B] (diagnostics) pops that were the runner-up, runner-ups published
 };
 // prescan record: [0] iteration tag, [1] kc = min(K, n_open), then K entries of 13 words: f (bits), seq, position,
 // node id, g (bits), Encode index, state (3, bits), rw, (t, u, v) (3, bits)
@@ -3389,6 +3390,10 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
       if (lane == 0) sr[10] = valid;
     }
     if (hit_out) *hit_out = s_go ? (int)s_win[11] : 0;
+    if (tid == 0 && s_go) {  // (diagnostics: MPGPU_HA_SPEC_STATS=1 prints the sums)
+      Q.nhit[b] += (int)s_win[11];
+      Q.nhit[B + b] += (int)sr[10];
+    }
     __syncthreads();  // sr and s_win reused by the next iteration
   }
   BookRec br;
@@ -3658,8 +3663,10 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   };
   if (item >= 2) {  // the expansion of n_{it+1} (skipped when it is the runner-up), then (SPEC) of r_{it+1}
     for (int it = it0;; it++) {
+      unsigned long long* stp0 = pst(it);  // (stamps: the r job's start / end in slots 6 / 7 of the n job's record)
       for (int job = 0; job < (SPEC ? 2 : 1); job++) {  // (one body for both: a loop, not two inlined copies)
         const bool r = SPEC && job == 1;
+        if (r) put(stp0, 6, now());
         IterArgs X = e_par(A, B, np, r ? 2 + ((it + 1) & 3) : (it + 1) & 1);
         X.node = Q.node + (size_t)(it & 1) * 3 * B;
         X.node_ag = 1;
@@ -3677,6 +3684,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         ha_stores_done();
         __syncthreads();
         if (threadIdx.x == 0) __hip_atomic_fetch_add((r ? Q.exs : Q.ex) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r) put(stp0, 7, now());
         put(stp, 1, now());
         put(stp, 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 1) << 32));
       }
@@ -3684,8 +3692,10 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   }
   if (item == 0) {  // RS_connected(n_it) (skipped when it is the runner-up), then (SPEC) RS_connected(r_it)
     for (int it = it0;; it++) {
+      unsigned long long* stp0 = pst(it);
       for (int job = 0; job < (SPEC && it > it0 ? 2 : 1); job++) {  // r_it: published by iteration it - 1 too
         const bool r = SPEC && job == 1;
+        if (r) put(stp0, 6, now());
         IterArgs X = A;
         X.node = Q.node + (size_t)((it - 1) & 1) * 3 * B;
         X.node_rw = Q.node_rw + (size_t)((it - 1) & 1) * B;  // (with granules: non-null = use the stored winner)
@@ -3708,6 +3718,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         ha_stores_done();
         __syncthreads();
         if (threadIdx.x == 0) st_ag((r ? Q.rsrs : Q.rsr) + s, 2 * it + 2);
+        if (r) put(stp0, 7, now());
         put(stp, 1, now());
         put(stp, 5, 2ull | ((unsigned long long)s << 4));
       }
@@ -4172,7 +4183,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
                                            sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + nB * 2 * HA_NGR * 8 + 256 * 57 +
-                                           nB * 2 * HA_NGR * 8 + nB * 8 + 256 * 3);
+                                           nB * 2 * HA_NGR * 8 + nB * 16 + 256 * 4);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -4223,6 +4234,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.ngr2 = (unsigned long long*)take(nB * 2 * HA_NGR * 8);
   Q.exs = (int*)take(nB * 4);
   Q.rsrs = (int*)take(nB * 4);
+  Q.nhit = (int*)take(nB * 8);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
   A.walls = p->n_walls ? mp_upload(ctx, WS_HA1, walls, 5 * (size_t)p->n_walls * B, &st) : nullptr;
@@ -4330,6 +4342,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.ngr2, 0, sizeof(unsigned long long) * nB * 2 * HA_NGR, ctx->stream));  // (HA_SPEC)
   MP_HIP(ctx, hipMemsetAsync(Q.exs, 0, sizeof(int) * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.rsrs, 0, sizeof(int) * nB, ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.nhit, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.err, 0, sizeof(int), ctx->stream));
   hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
   MP_HIP(ctx, hipGetLastError());
@@ -4554,6 +4567,15 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       return mp_fail(ctx, MP_ERR_HIP, "persistent search failed");
     }
     if (err) { cleanup(); return mp_fail(ctx, MP_ERR_HIP, "Hybrid A* search: a cross-block wait timed out"); }
+  }
+  if (getenv("MPGPU_HA_SPEC_STATS")) {  // diagnostics: how often the speculative runner-up was the next pop
+    std::vector<int> nh(2 * nB);
+    MP_HIP(ctx, hipMemcpyAsync(nh.data(), Q.nhit, sizeof(int) * 2 * nB, hipMemcpyDeviceToHost, ctx->stream));
+    MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    long long hits = 0, pubs = 0;
+    for (size_t i = 0; i < nB; i++) { hits += nh[i]; pubs += nh[nB + i]; }
+    fprintf(stderr, "[ha spec] persisted %d: runner-ups published %lld, pops that were the runner-up %lld\n",
+            (int)persisted, pubs, hits);
   }
   // outputs: per-scene counters, then the used prefix of pop_seq / states / RS paths
   std::vector<int> si(SI_N * nB);

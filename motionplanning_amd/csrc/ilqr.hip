@@ -89,7 +89,7 @@ constexpr int kSearchL = ILQR_SEARCH_L;  // lanes per line-search trial in mp_il
 #endif
 constexpr int kRound0L = ILQR_ROUND0_L;  // lanes per trial in the pipelined launch's round 0 (2 or 4) ...
 #ifndef ILQR_PAIR_MIN
-#define ILQR_PAIR_MIN 0
+#define ILQR_PAIR_MIN 2048
 #endif
 constexpr int kPairMin = ILQR_PAIR_MIN;  // ... while at least this many instances are active (else 4)
 #ifndef ILQR_ONEPASS_MAX

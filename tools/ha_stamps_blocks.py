@@ -32,6 +32,8 @@ def main(fn, n_it=6):
             f = lambda j: f"{(e[b, j] - t0) * tick:5.1f}" if e[b, j] > 0 else "   - "
             kind = "RS " if item[b] == 0 else f"g{int(item[b]):02d}"
             line = f"  {kind} r{int(role[b])} entry {f(0)} | 12 {f(12)} 13 {f(13)} 14 {f(14)} 15 {f(15)} 16 {f(16)} | body {f(1)} role {f(2)}"
+            if e[b, 3] == 0 and e[b, 6] > 0:  # (persistent tail, HA_SPEC) the runner-up job of an RS / group block
+                line += f" | spec {f(6)} .. {f(7)}"
             if e[b, 3] > 0:
                 line += f" | book: 6 {f(6)} 7 {f(7)} 10 {f(10)} 11 {f(11)} 8 {f(8)} done {f(3)}"
             if e[b, 4] > 0:

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--scenes", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--final", type=int, nargs="+", default=[1], help="final_stream values to try (0: inline)")
     a = ap.parse_args()
     from motionplanning_amd import configs
     from motionplanning_amd.abi import MP_NOISE_PHILOX, ptr
@@ -35,7 +36,6 @@ def main():
     S = a.scenes
     c = configs.cfg5_shard(0, S, noise_mode=MP_NOISE_PHILOX, seed=20260415)
     p = c["params"]
-    p.final_stream = 1
     K, H = p.K, p.H
     t = lambda x, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(x), dtype=dt, device=dev)
     X0, goal, un, grid = t(c["X0"]), t(c["goal"]), t(np.zeros((S, H, 2))), t(c["grid"], torch.uint8)
@@ -64,6 +64,8 @@ def main():
 
     for rep in range(a.reps):
         for C in a.ctx:
+          for fs in a.final:
+            p.final_stream = fs
             for lpr in a.lpr:
                 if lpr:
                     os.environ["MPGPU_LPR"] = str(lpr)
@@ -78,7 +80,7 @@ def main():
                 sync()
                 el = time.perf_counter() - t0
                 ok = all(bool((o["rc"] == K + 1).all().item()) for o in sets)
-                print(f"rep {rep} contexts {C} lpr {lpr or 'auto'}: {S * K * H * a.steps / el:.4e} rollout-steps/s, "
+                print(f"rep {rep} contexts {C} final_stream {fs} lpr {lpr or 'auto'}: {S * K * H * a.steps / el:.4e} rollout-steps/s, "
                       f"{el / a.steps * 1e3:.4f} ms/step, valid {ok}", flush=True)
     os.environ.pop("MPGPU_LPR", None)
 
