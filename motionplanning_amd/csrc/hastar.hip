@@ -736,6 +736,9 @@ __device__ __forceinline__ int wait_ge(const int* p, int v, int* err) {
 // tag: the scene's search ended.  The go word's value: bit 0 go (a node follows), bit 1 skip (the consumer has
 // nothing to do this round: the node's expansion was made speculatively, or no runner-up exists; HA_SPEC).
 constexpr int HA_NGR = 16;
+// granule slots by iteration (it & 3): a slot is rewritten by the bookkeeping three iterations on, which starts
+// only after its consumers have read it (the bookkeeping of the iteration between waited for them)
+constexpr int HA_NGR_SLOTS = 4;
 constexpr unsigned HA_NGR_DONE = 0xffffffffu;
 __device__ __forceinline__ void ha_publish_node(unsigned long long* g, unsigned tag, int lane, const long long* w,
                                                 unsigned go) {
@@ -1700,14 +1703,14 @@ struct HaSearch {
   long long* pre;        // [B][PRE_W] (RSH tail) the prescan's record: popfirst!'s K least entries before FindNewNode
   double* node_g;        // [2][B] (full-width ha_pipe_kernel) the popped node's g, double-buffered like node
   int* node_nn;          // [2][B] the scene's node count before the FindNewNode that published the node
-  unsigned long long* ngr;  // [2][B][HA_NGR] the popped node as tagged granules (ha_publish_node), by parity
+  unsigned long long* ngr;  // [HA_NGR_SLOTS][B][HA_NGR] the popped node as tagged granules (ha_publish_node), by it & 3
   int* nx;               // [B] (ha_pipe_kernel) 2·it + 2 + go once iteration it's bookkeeping has popped the next node
   int* ex;               // [B] (ha_persist_kernel) expansions finished (neighbour groups, cumulative)
   int* rsr;              // [B] (ha_persist_kernel) 2·it + 2 once RS_connected(n_it) has run
   int* err;              // [1] (ha_persist_kernel) a bounded wait ran out (the search is then not trusted)
   // (ha_persist_kernel, HA_SPEC) the runner-up: popfirst!'s second-least entry when n_{it+1} is popped, the
   // candidate for n_{it+2}, expanded (and RS_connected) speculatively
-  unsigned long long* ngr2;  // [2][B][HA_NGR] the runner-up as tagged granules, by parity
+  unsigned long long* ngr2;  // [HA_NGR_SLOTS][B][HA_NGR] the runner-up as tagged granules, by it & 3
   int* exs;              // [B] speculative expansions finished (neighbour groups, cumulative)
   int* rsrs;             // [B] 2·it + 2 once RS_connected(r_it) has run
   int* nhit;             // [2][B] (diagnostics) pops that were the runner-up, runner-ups published
@@ -3193,7 +3196,7 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
       long long wv[10];
 #pragma unroll
       for (int e = 0; e < 10; e++) wv[e] = go ? s_win[e] : 0;
-      ha_publish_node(Q.ngr + ((size_t)(it & 1) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv,
+      ha_publish_node(Q.ngr + ((size_t)(it & (HA_NGR_SLOTS - 1)) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv,
                       go ? 1u | (hit ? 2u : 0u) : 0u);
       if (go && lane < 3) {
         Q.node[(size_t)(it & 1) * 3 * B + 3 * b + lane] = __longlong_as_double(s_win[3 + lane]);
@@ -3386,7 +3389,8 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
 #pragma unroll
       for (int e = 0; e < 10; e++) wv[e] = valid ? sr[e] : 0;
       // skip (no runner-up): the speculative blocks count the round and wait for the next one
-      ha_publish_node(Q.ngr2 + ((size_t)(it & 1) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv, valid ? 1u : 3u);
+      ha_publish_node(Q.ngr2 + ((size_t)(it & (HA_NGR_SLOTS - 1)) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv,
+                      valid ? 1u : 3u);
       if (lane == 0) sr[10] = valid;
     }
     if (hit_out) *hit_out = s_go ? (int)s_win[11] : 0;
@@ -3554,7 +3558,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         X.node_g = Q.node_g + (size_t)(it & 1) * B;
         X.node_nn = Q.node_nn + (size_t)(it & 1) * B;
       } else if (A.ngr_pub) {  // the node as tagged granules
-        X.ngr = Q.ngr + (size_t)(it & 1) * B * HA_NGR;
+        X.ngr = Q.ngr + (size_t)(it & (HA_NGR_SLOTS - 1)) * B * HA_NGR;
         X.ngr_tag = (unsigned)it + 1;
       }
     }
@@ -3674,7 +3678,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         X.node_flag_min = 2 * it + 2;
         X.node_flag_err = Q.err;
         if (A.ngr_pub || r) {
-          X.ngr = (r ? Q.ngr2 : Q.ngr) + (size_t)(it & 1) * B * HA_NGR;
+          X.ngr = (r ? Q.ngr2 : Q.ngr) + (size_t)(it & (HA_NGR_SLOTS - 1)) * B * HA_NGR;
           X.ngr_tag = (unsigned)it + 1;
         }
         X.do_rs = 0;
@@ -3706,7 +3710,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
           X.node_flag_min = 2 * (it - 1) + 2;
           X.node_flag_err = Q.err;
           if (A.ngr_pub || r) {
-            X.ngr = (r ? Q.ngr2 : Q.ngr) + (size_t)((it - 1) & 1) * B * HA_NGR;
+            X.ngr = (r ? Q.ngr2 : Q.ngr) + (size_t)((it - 1) & (HA_NGR_SLOTS - 1)) * B * HA_NGR;
             X.ngr_tag = (unsigned)it;
           }
         }
@@ -3777,11 +3781,11 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         A.rs_path[(size_t)s * MAXPATH * 3 + i] = ld_ag(F.rs_path + (size_t)s * MAXPATH * 3 + i);
     }
     if (sh_f) {
-      if (A.ngr_pub && threadIdx.x < 2)  // the search ended: both parities' go words (whichever is waited on)
+      if (A.ngr_pub && threadIdx.x < HA_NGR_SLOTS)  // the search ended: every slot's go word (whichever is waited on)
         __hip_atomic_store(Q.ngr + ((size_t)threadIdx.x * B + s) * HA_NGR + 13,
                            (unsigned long long)HA_NGR_DONE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (SPEC && threadIdx.x >= 2 && threadIdx.x < 4)  // and the runner-up's
-        __hip_atomic_store(Q.ngr2 + ((size_t)(threadIdx.x - 2) * B + s) * HA_NGR + 13,
+      if (SPEC && threadIdx.x >= HA_NGR_SLOTS && threadIdx.x < 2 * HA_NGR_SLOTS)  // and the runner-up's
+        __hip_atomic_store(Q.ngr2 + ((size_t)(threadIdx.x - HA_NGR_SLOTS) * B + s) * HA_NGR + 13,
                            (unsigned long long)HA_NGR_DONE << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!A.ngr_pub && threadIdx.x == 0) st_ag(Q.nx + s, HA_DONE);
       return;
@@ -4182,8 +4186,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + nB * 2 * HA_NGR * 8 + 256 * 57 +
-                                           nB * 2 * HA_NGR * 8 + nB * 16 + 256 * 4);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + nB * HA_NGR_SLOTS * HA_NGR * 8 + 256 * 57 +
+                                           nB * HA_NGR_SLOTS * HA_NGR * 8 + nB * 16 + 256 * 4);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -4225,13 +4229,13 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.node_tuv = (double*)take(nB * 48);
   Q.pre = (long long*)take(nB * PRE_W * 8);
   Q.nx = (int*)take(nB * 4);
-  Q.ngr = (unsigned long long*)take(nB * 2 * HA_NGR * 8);
+  Q.ngr = (unsigned long long*)take(nB * HA_NGR_SLOTS * HA_NGR * 8);
   Q.ex = (int*)take(nB * 4);
   Q.rsr = (int*)take(nB * 4);
   Q.err = (int*)take(4);
   Q.node_g = (double*)take(nB * 16);
   Q.node_nn = (int*)take(nB * 8);
-  Q.ngr2 = (unsigned long long*)take(nB * 2 * HA_NGR * 8);
+  Q.ngr2 = (unsigned long long*)take(nB * HA_NGR_SLOTS * HA_NGR * 8);
   Q.exs = (int*)take(nB * 4);
   Q.rsrs = (int*)take(nB * 4);
   Q.nhit = (int*)take(nB * 8);
@@ -4336,10 +4340,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.tk, 0, sizeof(int) * 2 * nB, ctx->stream));  // the finishers reset them
   MP_HIP(ctx, hipMemsetAsync(Q.rec, 0, sizeof(long long) * RC_N * nB, ctx->stream));  // record-ready flags
   MP_HIP(ctx, hipMemsetAsync(Q.nx, 0, sizeof(int) * nB, ctx->stream));  // ha_pipe_kernel's pop flags
-  MP_HIP(ctx, hipMemsetAsync(Q.ngr, 0, sizeof(unsigned long long) * nB * 2 * HA_NGR, ctx->stream));  // granule tags
+  MP_HIP(ctx, hipMemsetAsync(Q.ngr, 0, sizeof(unsigned long long) * nB * HA_NGR_SLOTS * HA_NGR, ctx->stream));  // granule tags
   MP_HIP(ctx, hipMemsetAsync(Q.ex, 0, sizeof(int) * nB, ctx->stream));  // ha_persist_kernel's flags
   MP_HIP(ctx, hipMemsetAsync(Q.rsr, 0, sizeof(int) * nB, ctx->stream));
-  MP_HIP(ctx, hipMemsetAsync(Q.ngr2, 0, sizeof(unsigned long long) * nB * 2 * HA_NGR, ctx->stream));  // (HA_SPEC)
+  MP_HIP(ctx, hipMemsetAsync(Q.ngr2, 0, sizeof(unsigned long long) * nB * HA_NGR_SLOTS * HA_NGR, ctx->stream));  // (HA_SPEC)
   MP_HIP(ctx, hipMemsetAsync(Q.exs, 0, sizeof(int) * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.rsrs, 0, sizeof(int) * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.nhit, 0, sizeof(int) * 2 * nB, ctx->stream));

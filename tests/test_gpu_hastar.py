@@ -70,15 +70,19 @@ def test_scenario_batch_lockstep_bitexact(ctx, n, seed):
     hs = ha.scenario_batch(n, seed=seed)
     _, p, sc, pc = _setup(ctx)
     ha.plan_batch(hs, ctx=ctx)
-    mism = 0
-    for h in hs:
+    bad = []
+    for i, h in enumerate(hs):
         ref = oracle.ha_plan(p, h.s.starting_states, h.s.ending_states, np.array(h.s.obstacle_list), sc, pc)
         same = (h.r.found == ref["found"] and h.r.loop_count == ref["pops"] and h.r.n_nodes == ref["n_nodes"]
                 and np.array_equal(h.r.pop_sequence, ref["pop_seq"])
                 and np.array_equal(h.r.hybrid_astar_states.T, ref["states"])
                 and np.array_equal(h.r.RSpath_final.T, ref["rs_path"]))
-        mism += not same
-    assert mism == 0
+        if not same:
+            ps, rs = np.asarray(h.r.pop_sequence), np.asarray(ref["pop_seq"])
+            m = min(len(ps), len(rs))
+            d = np.nonzero(ps[:m] != rs[:m])[0]
+            bad.append((i, int(h.r.loop_count), int(ref["pops"]), int(d[0]) if len(d) else -1))
+    assert not bad, f"scenarios differing (index, pops, oracle pops, first divergent pop): {bad}"
 
 
 def test_pipelined_tail_without_persistent_launch_bitexact(ctx):

@@ -3,7 +3,7 @@
 shard, device Philox noise, full TrajectoryCollection, final rollout on the side stream); call i runs on
 context i mod C.  Prints rollout-steps/s per (contexts, lane layout).
 
-  python tools/mppi_overlap.py [--ctx 1 2] [--lpr 0 1 2] [--steps 200] [--warmup 40]
+  python tools/mppi_overlap.py [--ctx 1 2] [--lpr 0 1 2] [--steps 200] [--warmup 40] [--timing]
 """
 import argparse
 import ctypes
@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--scenes", type=int, default=8)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--final", type=int, nargs="+", default=[1], help="final_stream values to try (0: inline)")
+    ap.add_argument("--timing", action="store_true", help="per-launch HIP-event timing on (as bench.py)")
     a = ap.parse_args()
     from motionplanning_amd import configs
     from motionplanning_amd.abi import MP_NOISE_PHILOX, ptr
@@ -40,6 +41,8 @@ def main():
     t = lambda x, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(x), dtype=dt, device=dev)
     X0, goal, un, grid = t(c["X0"]), t(c["goal"]), t(np.zeros((S, H, 2))), t(c["grid"], torch.uint8)
     ctxs = [Context(0) for _ in range(max(a.ctx))]
+    for x in ctxs:
+        x.lib.mp_ctx_kernel_timing(x.handle, 1 if a.timing else 0)
     sets = []
     for _ in range(3 * max(a.ctx)):
         sets.append({k: torch.empty(v, dtype=dt, device=dev) for k, (v, dt) in dict(
