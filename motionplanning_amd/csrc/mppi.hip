@@ -1029,8 +1029,12 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
     ctx->fin_par = (par + 1) % MP_FIN_RING;
     const FinRec R(H, D.n_obs, D.gnx * D.gny);
     A.fin_stride = R.stride;
+    // every slot of the ring sized at once: a slot first used by a later call would allocate (hipMalloc, which
+    // can wait for the device) in the middle of a run of calls -- with calls alternating over two contexts, the
+    // bench's first timed calls did
+    for (int q = 0; q < MP_FIN_RING; q++)
+      if (!mp_ws(ctx, WS_FIN0 + q, sizeof(double) * (size_t)S * R.stride)) return MP_ERR_NOMEM;
     A.fin = (double*)mp_ws(ctx, WS_FIN0 + par, sizeof(double) * (size_t)S * R.stride);
-    if (!A.fin) return MP_ERR_NOMEM;
     // The host (not the context stream) waits for the final rollout MP_FIN_RING calls back to
     // have read this slot (long done): a cross-stream wait packet would stall the context
     // stream between kernels, and a wait on the previous call's final rollout (which runs

@@ -164,6 +164,13 @@ extern "C" {
 int mp_ctx_kernel_timing(mp_ctx* ctx, int enable) {
   if (!ctx) return MP_ERR_INVALID;
   ctx->timing = enable != 0;
+  // the event pool made up front (two per timed launch, reused after each mp_ctx_kernel_ms): creating events
+  // on demand would put hipEventCreate calls between the launches being timed
+  while (ctx->timing && ctx->ev_pool.size() < 512) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) break;
+    ctx->ev_pool.push_back(e);
+  }
   return MP_OK;
 }
 
