@@ -26,6 +26,14 @@ import os
 import sys
 import time
 
+# Hardware queues, before the HIP runtime starts (import torch): the headline's two contexts drive four streams
+# (a plan stream and a final-rollout side stream each) beside torch's own, and at HIP's default of 4 queues per
+# process two of them share a queue, so the alternating calls serialise instead of overlapping (r06r, driver
+# args: 2 streams 0.96e10 at 4 queues, 1.10-1.11e10 at 8; 1 stream 1.02e10 either way).
+_HWQ = os.environ.get("GPU_MAX_HW_QUEUES", "")
+if not _HWQ.isdigit() or int(_HWQ) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 import numpy as np
 import torch  # import before libmpgpu so both share torch's HIP runtime
 import torch.distributed as dist
@@ -289,6 +297,7 @@ def main():
             "final_rollout": "in plan kernel" if a.final_inline else
                              "side stream (final_stream=1): overlaps the next step's rollouts",
             "streams": max(1, a.streams),
+            "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"]),
             "parallelism": f"scene-sharded x{world}" + ((" + gloo all_gather(MPPICtrl), all ranks on cuda:0 "
                                                           "(--share-device rehearsal)") if a.share_device and world > 1
                                                          else " + RCCL all_gather(MPPICtrl)" if world > 1 else ""),
