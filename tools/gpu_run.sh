@@ -35,7 +35,7 @@ for step in "$@"; do
         python3 bench.py --steps 30 --warmup 3 --no-cpu > $O/prof.log 2>&1
       rc=$?; find $O -name 'run_kernel_trace.csv' | xargs -r gzip -f ;;
     pass)
-      bash tools/gpu_pass4.sh ${TAG}_pass notest
+      bash tools/gpu_pass4.sh ${TAG}_pass_notest
       rc=$? ;;
     cmd)
       timeout -k 10 900 bash -c "$arg" > $O/cmd$n.log 2>&1
