@@ -17,8 +17,8 @@ fi
 # the persistent Hybrid A* tail ordinarily (the same kernel and grid); the tests above and the bench run at the
 # end use the default cooperative launch
 export MPGPU_HA_COOP=0
-BM="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-single --no-extras"  # MPPI headline launches only
-BX="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-single"
+BM="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-single --no-whole --no-extras"  # MPPI headline launches only
+BX="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-single --no-whole"
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA"
 timeout -k 10 200 rocprofv3 --pmc $SQ -d $O/pmc1 -o run --output-format csv -- $BM > $O/pmc1.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc $SQ -d $O/pmc4 -o run --output-format csv -- $BX > $O/pmc4.log 2>&1 &&
