@@ -8,10 +8,10 @@ TrajectoryCollection (every rollout's trajectory and control list) written to HB
 weights + MPPICtrl + final rollout.  One plan launch per step (Philox noise drawn inside the
 rollout loop) + the final rollout of MPPICtrl on its context's side stream (final_stream=1;
 --final-inline keeps it in the plan kernel); consecutive steps are independent batches and
-alternate over --streams contexts (default 2, one stream each: step i+1's rollouts fill the SIMDs
-step i's last waves leave idle), so step i's serial final rollout and its straggler waves overlap
-step i+1's rollouts; every step's outputs are complete when the timed region's closing
-synchronize returns.  Inputs
+alternate over --streams contexts (default 3, one stream each, calls_in_flight = 3: each launch takes
+the one-rollout-per-lane layout, one wave per SIMD, so the calls in flight share every SIMD and
+step i's serial final rollout and its straggler waves overlap steps i+1 and i+2); every step's
+outputs are complete when the timed region's closing synchronize returns.  Inputs
 are resident in HBM before the timed region.  N>1: one process per GPU, each
 solves its own S scenes (weak scaling) and the ranks all-gather the optimal
 controls over RCCL (the north star's exchange step).  The single-scene
@@ -26,13 +26,13 @@ import os
 import sys
 import time
 
-# Hardware queues, before the HIP runtime starts (import torch): the headline's two contexts drive four streams
+# Hardware queues, before the HIP runtime starts (import torch): the headline's three contexts drive six streams
 # (a plan stream and a final-rollout side stream each) beside torch's own, and at HIP's default of 4 queues per
-# process two of them share a queue, so the alternating calls serialise instead of overlapping (r06r, driver
-# args: 2 streams 0.96e10 at 4 queues, 1.10-1.11e10 at 8; 1 stream 1.02e10 either way).
+# process streams share a queue, so the alternating calls serialise instead of overlapping (r06r, driver args,
+# two contexts: 0.96e10 at 4 queues, 1.10-1.11e10 at 8; r06za, three contexts: 1.31e10 at 8, 1.36e10 at 12).
 _HWQ = os.environ.get("GPU_MAX_HW_QUEUES", "")
-if not _HWQ.isdigit() or int(_HWQ) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+if not _HWQ.isdigit() or int(_HWQ) < 12:
+    os.environ["GPU_MAX_HW_QUEUES"] = "12"
 
 import numpy as np
 import torch  # import before libmpgpu so both share torch's HIP runtime
@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--rotate", type=int, default=3, help="output buffer sets rotated (>256 MB MALL at S=8)")
     ap.add_argument("--no-single", action="store_true", help="skip the single-scene (configs[1]) line")
     ap.add_argument("--no-whole", action="store_true", help="skip the configs[4]-whole (64 scenes, one GPU) line")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=3,
                     help="contexts (streams) the headline's consecutive independent plan calls alternate over")
     ap.add_argument("--roofline", default=os.path.join(ROOT, "profiles", "roofline_latest.json"),
                     help="per-kernel VALU counts + durations (tools/pmc_roofline.py) for the iLQR / HA* rooflines")
@@ -131,6 +131,7 @@ def run(a, S, ctx, dev, world, rank, steps, warmup, rotate, cfg5=True, nstreams=
     p = c["params"]
     p.scene_base = rank * S  # global scene ids: rank r plans scenes [rS, (r+1)S) of the job
     p.final_stream = 0 if a.final_inline else 1  # final rollout on the side stream, overlapping the next step
+    p.calls_in_flight = nstreams  # the launch layout for nstreams calls sharing the device (include/mpgpu.h)
     K, H = p.K, p.H
 
     def t(x, dt=torch.float64):

@@ -107,6 +107,15 @@ typedef struct mp_mppi_params {
                              /*   the context's side stream from a snapshot of  */
                              /*   its inputs, overlapping the next call's       */
                              /*   rollouts (see mp_mppi_plan_dev)               */
+  int32_t calls_in_flight;   /* 0 / 1: the call has the device to itself.  n > 1:*/
+                             /*   the caller keeps n independent calls in       */
+                             /*   flight on n contexts of this device (see      */
+                             /*   INTEGRATION.md); the launch then takes the    */
+                             /*   layout whose waves share the CUs with the     */
+                             /*   other calls' (one rollout per lane).  Same    */
+                             /*   rollouts bit for bit either way; MPPICtrl     */
+                             /*   within the combine tolerance (the weighted    */
+                             /*   sum's partition may differ)                   */
 } mp_mppi_params;
 
 /*

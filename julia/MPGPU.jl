@@ -90,6 +90,7 @@ struct MppiParams
     offset::UInt64
     scene_base::Int32
     final_stream::Int32
+    calls_in_flight::Int32
 end
 
 """MppiParams from an MPPISearcher's settings (MPPI/src/types.jl:10-31, setup.jl:3-59)."""
@@ -103,7 +104,7 @@ function params(mppi; noise_mode = MP_NOISE_PHILOX, seed = 0, offset = 0, grid =
     end
     MppiParams(s.SamplingNumber, s.N, s.FeasibilityCount, length(s.obstacle_list), s.dt, s.lambda,
                (Σ[1, 1], Σ[1, 2], Σ[2, 1], Σ[2, 2]), Tuple(s.XL), Tuple(s.XU), Tuple(s.CL), Tuple(s.CU),
-               s.SlackPenalty, 100 * 712.5, nx, ny, x0, y0, dx, dy, noise_mode, 1, seed, offset, 0, 0)
+               s.SlackPenalty, 100 * 712.5, nx, ny, x0, y0, dx, dy, noise_mode, 1, seed, offset, 0, 0, 0)
 end
 
 """
@@ -119,7 +120,7 @@ coll_cost (K, S), coll_feas (K, S).
 function mppi_plan_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Float64}, Unom::Array{Float64,3};
                          obstacles = nothing, grid = nothing, noise = nothing, collect::Bool = false)
     S = size(X0, 2); H = Int(p.H); K = Int(p.K)
-    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 25)...)
+    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 26)...)
     U = zeros(2, H, S); traj = zeros(7, H + 1, S); cost = zeros(S)
     feas = zeros(Int32, S); rc = zeros(Int32, S); fc = zeros(Int32, S)
     ct = collect ? zeros(K, 7, H + 1, S) : nothing
@@ -204,7 +205,7 @@ function mppi_closed_loop_batch(p::MppiParams, X0::Matrix{Float64}, goal::Matrix
                                 obstacles = nothing, grid = nothing, noise = nothing, poll_every::Integer = 0)
     S = size(X0, 2); H = Int(p.H)
     R = cld(max_steps, update_idx)
-    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 25)...)
+    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 26)...)
     lp = MppiLoopParams(update_idx, max_steps, δt, goal_radius, poll_every, 0)
     h0 = Int32.(hold .- 1)
     his = zeros(8, max_steps + 1, S); nr = zeros(Int32, S); np_ = zeros(Int32, S)
@@ -326,7 +327,7 @@ function mppi_plan_sharded(p::MppiParams, X0::Matrix{Float64}, goal::Matrix{Floa
                            obstacles = nothing, grid = nothing, noise = nothing)
     cs = comm_init()
     S = size(X0, 2); H = Int(p.H)
-    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 25)...)
+    p = noise === nothing ? p : MppiParams(ntuple(i -> i == 20 ? MP_NOISE_EXTERNAL : getfield(p, i), 26)...)
     U = zeros(2, H, S); traj = zeros(7, H + 1, S); cost = zeros(S)
     feas = zeros(Int32, S); rc = zeros(Int32, S); fc = zeros(Int32, S)
     nz(a) = a === nothing ? C_NULL : pointer(a)

@@ -71,6 +71,7 @@ class MPPIParams(ctypes.Structure):
         ("offset", ctypes.c_uint64),
         ("scene_base", ctypes.c_int32),
         ("final_stream", ctypes.c_int32),
+        ("calls_in_flight", ctypes.c_int32),
     ]
 
 

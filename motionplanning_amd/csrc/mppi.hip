@@ -874,6 +874,9 @@ static int make_dev_params(mp_ctx* ctx, const mp_mppi_params* p, int K, MppiDev*
   MP_CHECK(ctx, p->grid_nx >= 0 && p->grid_ny >= 0, "grid dims must be >= 0");
   MP_CHECK(ctx, p->noise_mode == MP_NOISE_EXTERNAL || p->noise_mode == MP_NOISE_PHILOX, "bad noise_mode %d",
            p->noise_mode);
+  MP_CHECK(ctx, p->calls_in_flight >= 0 && p->calls_in_flight <= 64, "calls_in_flight (%d) must be in [0, 64]",
+           p->calls_in_flight);
+  D->in_flight = p->calls_in_flight > 1 ? p->calls_in_flight : 1;
   D->K = K;
   D->H = p->H;
   D->FC = p->feasibility_count;
@@ -933,11 +936,14 @@ static int plan_launch(mp_ctx* ctx, const MppiDev& D, int S, const double* X0, c
   // interleaved in a lane, costs evaluated once) 0.536 ms vs LPR 2 (4 waves/SIMD) 0.703 ms;
   // 8 scenes, LPR 1 (1 wave/SIMD) 0.384 ms vs LPR 2 (2 waves/SIMD) 0.375 ms: a lone wave
   // cannot cover the fp64 dependency latency.
+  // With n calls in flight on n contexts (calls_in_flight), the other calls' waves fill the SIMDs too, so the
+  // rollouts of all of them count: 8 scenes, two calls alternating over two contexts, LPR 1 1.17-1.19e10
+  // rollout-steps/s against LPR 2 1.08-1.10e10; three calls 1.31e10 (r06y, bench driver arguments).
   // (test hook) MPGPU_LPR = 1 / 2 forces the layout: the results are the same bits either way
   // (tests/test_gpu_mppi_lane.py), only the launch shape changes
   const char* lpr_s = getenv("MPGPU_LPR");
   const int lpr_env = lpr_s ? atoi(lpr_s) : 0;
-  const int LPR = lpr_env == 1 || lpr_env == 2 ? lpr_env : ((size_t)S * K >= 131072 ? 1 : 2);
+  const int LPR = lpr_env == 1 || lpr_env == 2 ? lpr_env : ((size_t)S * K * D.in_flight >= 131072 ? 1 : 2);
   // Single scene (64 blocks): BT 128 (2 waves per CU on 128 CUs) 0.278 ms vs BT 256 (4 waves, one per
   // SIMD, on 64 CUs) 0.242 ms -- a CU's four SIMDs each holding one wave beat half-filled CUs.
   const int BT = LPR == 1 ? ((size_t)S * ((K + 511) / 512) >= 256 ? 512 : 256)

@@ -28,6 +28,7 @@ struct MppiDev {
   int noise_mode, ctrl_cost;
   unsigned long long seed, offset;
   int scene_base;
+  int in_flight;  // (host side) mp_mppi_params.calls_in_flight, at least 1: the launch layout's choice
 };
 
 // Exchange a double with the other lane of the pair: DPP quad_perm [1,0,3,2]

@@ -239,6 +239,33 @@ def test_bench_workload_full_size_bitexact(ctx, base):
         _check_plan(gpu, refs[s], s=s)
 
 
+@pytest.mark.parametrize("base", [0, 56])
+def test_bench_workload_in_flight_bitexact(ctx, base):
+    """The headline workload as bench.py runs it with two calls in flight (calls_in_flight = 2: the launch takes
+    the one-rollout-per-lane layout whose waves share the CUs with the other call's) -- the same checks against
+    the oracle as test_bench_workload_full_size_bitexact."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from motionplanning_amd.abi import MP_NOISE_PHILOX
+
+    S = 8
+    c = configs.cfg5_shard(base, S, noise_mode=MP_NOISE_PHILOX, seed=20260415)
+    p = c["params"]
+    p.calls_in_flight = 2
+    p.offset = 5
+    p.final_stream = 1
+    X0, goal, grid = c["X0"], c["goal"], c["grid"]
+    gpu = mppi_plan_batch(p, X0, goal, np.zeros((S, p.H, 2)), None, grid, None, collect=True, ctx=ctx)
+
+    def ref(s):
+        return oracle.mppi_plan(p, X0[s], goal[s], np.zeros((p.H, 2)), None, grid[s], None, scene=s, collect=True)
+
+    with ThreadPoolExecutor(8) as ex:
+        refs = list(ex.map(ref, range(S)))
+    for s in range(S):
+        _check_plan(gpu, refs[s], s=s)
+
+
 def test_scene_batching_invariance(ctx):
     """Sharding correctness on the device: a scene planned inside an 8-scene launch equals the same scene
     planned alone with scene_base = its global index (the Philox counter word a rank of a sharded job

@@ -67,6 +67,7 @@ def main():
 
     for rep in range(a.reps):
         for C in a.ctx:
+          p.calls_in_flight = C
           for fs in a.final:
             p.final_stream = fs
             for lpr in a.lpr:
