@@ -3729,6 +3729,13 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
     }
   }
   // item 1: the bookkeeping of iteration it, it = it0, it0 + 1, ...
+  // on HA_BOOK_WAVES waves of the block (the rest leave: a barrier counts only the waves still running), so its
+  // block-wide steps (barriers, cross-wave reductions) span fewer waves
+#ifndef HA_BOOK_WAVES
+#define HA_BOOK_WAVES 4
+#endif
+  constexpr int NTB = 64 * (HWt < HA_BOOK_WAVES ? HWt : HA_BOOK_WAVES);
+  if ((int)threadIdx.x >= NTB) return;
   if (SPEC && threadIdx.x < 12) sh_run[threadIdx.x] = 0;  // no runner-up yet: iteration it0's pop is no hit
   __syncthreads();
   int hit = 0;  // (SPEC) n_it is r_{it-1}: its records and RS_connected are the speculative ones
@@ -3754,10 +3761,10 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
 #define HA_PREWAIT 1
 #endif
     if (!HA_PREWAIT) wait_exp();  // (A/B build -DHA_PREWAIT=0: the wait before the bookkeeping's first load)
-    const BookRec br = HA_PREWAIT ? ha_book_pipe<64 * HWt, true, decltype(wait_exp), SPEC>(P, Q, Ei, B, it, s, stp,
-                                                                                        wait_exp, sh_run, &hit_next)
-                                  : ha_book_pipe<64 * HWt, true, NoMid, SPEC>(P, Q, Ei, B, it, s, stp, NoMid(),
-                                                                          sh_run, &hit_next);
+    const BookRec br = HA_PREWAIT ? ha_book_pipe<NTB, true, decltype(wait_exp), SPEC>(P, Q, Ei, B, it, s, stp,
+                                                                                 wait_exp, sh_run, &hit_next)
+                                  : ha_book_pipe<NTB, true, NoMid, SPEC>(P, Q, Ei, B, it, s, stp, NoMid(), sh_run,
+                                                                   &hit_next);
     put(stp, 3, now());
     IterArgs F = A;
     rs_slot(F, h ? 2 + ((it - 1) & 3) : it & 1);
@@ -3777,7 +3784,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
     __syncthreads();
     if (sh_f == 1) {  // RSpath_final into the canonical buffer the host reads
       const int n = ld_ag(F.rs_len + s);
-      for (int i = threadIdx.x; i < 3 * n; i += 64 * HWt)
+      for (int i = threadIdx.x; i < 3 * n; i += NTB)
         A.rs_path[(size_t)s * MAXPATH * 3 + i] = ld_ag(F.rs_path + (size_t)s * MAXPATH * 3 + i);
     }
     if (sh_f) {
