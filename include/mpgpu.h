@@ -302,6 +302,11 @@ int mp_ilqr_forward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const d
  * search until |ΔJ/J| <= tol.  X/U in: initial guess; out: solution. */
 int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U,
                   double* J, int32_t* iters);
+/* Same, DEVICE pointers: X (B,N,4) / U (B,N,2) solved in place, J (B) and iters (B) written on the
+ * device.  Synchronous like mp_ilqr_solve (its host loop polls the active count every iteration); it
+ * only skips the host transfers -- the form the bench times, inputs resident in HBM. */
+int mp_ilqr_solve_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U,
+                      double* J, int32_t* iters);
 
 /* ---------------------------------------------------------- Hybrid A* */
 /* Settings mirror HybridAstarSettings (PathPlanning/HybridAstar/src/types.jl:20-43). */

@@ -171,6 +171,7 @@ SIGNATURES = {
     "mp_ilqr_backward_dev": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
     "mp_ilqr_forward_dev": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I] + [_V] * 8),
     "mp_ilqr_solve": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
+    "mp_ilqr_solve_dev": (ctypes.c_int, [_V, ctypes.POINTER(ILQRParams), _I, _V, _V, _V, _V]),
     "mp_ha_set_primitives": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _V, _V]),
     "mp_ha_neighbor_origin": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I, _V, _I, _V, _V, _V]),
     "mp_ha_expand": (ctypes.c_int, [_V, ctypes.POINTER(HAParams), _I] + [_V] * 7),

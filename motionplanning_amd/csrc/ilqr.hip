@@ -1850,8 +1850,10 @@ int mp_ilqr_forward_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, const d
   return MP_OK;
 }
 
-int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U, double* J,
-                  int32_t* iters) {
+// mp_ilqr_solve (dev = false: host X / U / J / iters, uploaded and downloaded here) and mp_ilqr_solve_dev (dev:
+// the caller's device buffers, X / U solved in place)
+static int ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U, double* J,
+                      int32_t* iters, bool dev) {
   if (!ctx) return MP_ERR_INVALID;
   IlqrDev D;
   int st = make_ilqr(ctx, p, B, &D);
@@ -1859,8 +1861,8 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   MP_CHECK(ctx, X && U && J && iters, "required pointer is NULL");
   MP_HIP(ctx, hipSetDevice(ctx->device));
   const size_t N = D.N;
-  double* dX = (double*)mp_upload(ctx, WS_IO0, X, 4 * N * B, &st);
-  double* dU = (double*)mp_upload(ctx, WS_IO1, U, 2 * N * B, &st);
+  double* dX = dev ? X : (double*)mp_upload(ctx, WS_IO0, X, 4 * N * B, &st);
+  double* dU = dev ? U : (double*)mp_upload(ctx, WS_IO1, U, 2 * N * B, &st);
   double* dk = (double*)mp_ws(ctx, WS_IO2, sizeof(double) * 2 * (N - 1) * B);
   double* dK = (double*)mp_ws(ctx, WS_IO3, sizeof(double) * 8 * (N - 1) * B);
   // trial slots for the G-wide line search: G = kSearchG = 16 trials per instance on lane quads
@@ -2079,10 +2081,15 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
     if (stop) break;
   }
   std::vector<int> hfl(B);
-  if ((st = mp_download(ctx, X, (const double*)dX, 4 * N * B))) return st;
-  if ((st = mp_download(ctx, U, (const double*)dU, 2 * N * B))) return st;
-  if ((st = mp_download(ctx, J, (const double*)dJ, (size_t)B))) return st;
-  if ((st = mp_download(ctx, iters, (const int*)dit, (size_t)B))) return st;
+  if (dev) {  // X / U are already the caller's; J and the iteration counts device to device
+    MP_HIP(ctx, hipMemcpyAsync(J, dJ, sizeof(double) * B, hipMemcpyDeviceToDevice, ctx->stream));
+    MP_HIP(ctx, hipMemcpyAsync(iters, dit, sizeof(int) * B, hipMemcpyDeviceToDevice, ctx->stream));
+  } else {
+    if ((st = mp_download(ctx, X, (const double*)dX, 4 * N * B))) return st;
+    if ((st = mp_download(ctx, U, (const double*)dU, 2 * N * B))) return st;
+    if ((st = mp_download(ctx, J, (const double*)dJ, (size_t)B))) return st;
+    if ((st = mp_download(ctx, iters, (const int*)dit, (size_t)B))) return st;
+  }
   if ((st = mp_download(ctx, hfl.data(), (const int*)dfl, (size_t)B))) return st;
   MP_HIP(ctx, hipStreamSynchronize(ctx->stream));
   int any = 0;
@@ -2090,6 +2097,16 @@ int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, do
   if (any & 1) return mp_fail(ctx, MP_ERR_NUMERIC, "line search hit max_ls for some instance (the reference would loop forever)");
   if (any & 2) return mp_fail(ctx, MP_ERR_NUMERIC, "max_iter reached before |dJ/J| <= tol for some instance");
   return MP_OK;
+}
+
+int mp_ilqr_solve(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U, double* J,
+                  int32_t* iters) {
+  return ilqr_solve(ctx, p, B, X, U, J, iters, false);
+}
+
+int mp_ilqr_solve_dev(mp_ctx* ctx, const mp_ilqr_params* p, int32_t B, double* X, double* U, double* J,
+                      int32_t* iters) {
+  return ilqr_solve(ctx, p, B, X, U, J, iters, true);
 }
 
 }  // extern "C"

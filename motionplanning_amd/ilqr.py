@@ -88,3 +88,15 @@ def ilqr_solve(p, X, U, ctx=None, strict=False):
     if st != MP_ERR_NUMERIC or strict:
         ctx.check(st)
     return X, U, J, it, st == 0
+
+
+def ilqr_solve_dev(p, X, U, J, iters, ctx=None, strict=False):
+    """ilqr_solve on device buffers (torch tensors in HBM: X (B, N, 4) and U (B, N, 2) f64 solved in place,
+    J (B,) f64 and iters (B,) int32 written); returns ok (False: some instance hit max_iter / max_ls)."""
+    ctx = ctx or default_context()
+    B = X.shape[0]
+    assert X.shape == (B, p.N, 4) and U.shape == (B, p.N, 2) and J.shape == (B,) and iters.shape == (B,)
+    st = ctx.lib.mp_ilqr_solve_dev(ctx.handle, ctypes.byref(p), B, ptr(X), ptr(U), ptr(J), ptr(iters))
+    if st != MP_ERR_NUMERIC or strict:
+        ctx.check(st)
+    return st == 0

@@ -177,6 +177,28 @@ def test_solve_configs2_horizon_bitexact(ctx):
     assert stalled > 0  # the rest pass (trials 16..max_ls) was exercised
 
 
+def test_solve_dev_matches_host_api(ctx):
+    """mp_ilqr_solve_dev (device buffers, solved in place -- the form the bench times) gives the host API's
+    results bit for bit: states, controls, costs, iteration counts and the status, on the bench's instances."""
+    import torch
+
+    B, N = 1024, 100
+    p = ilqr.params(N=N, max_iter=60)
+    x0, U0 = ilqr.cfg3_instances(B, N, seed=3)
+    X0, _ = ilqr.ilqr_rollout(p, x0, U0, ctx=ctx)
+    X, U, J, it, ok = ilqr.ilqr_solve(p, X0, U0, ctx=ctx)
+    dev = torch.device("cuda", 0)
+    dX, dU = torch.as_tensor(X0, device=dev).clone(), torch.as_tensor(U0, device=dev).clone()
+    dJ = torch.empty(B, dtype=torch.float64, device=dev)
+    dit = torch.empty(B, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()  # (torch's copies ran on its own stream, the solve runs on the context's)
+    ok_dev = ilqr.ilqr_solve_dev(p, dX, dU, dJ, dit, ctx=ctx)
+    torch.cuda.synchronize()
+    assert ok_dev == ok
+    assert np.array_equal(dX.cpu().numpy(), X) and np.array_equal(dU.cpu().numpy(), U)
+    assert np.array_equal(dJ.cpu().numpy(), J) and np.array_equal(dit.cpu().numpy(), it)
+
+
 def test_solve_bench_workload_full_size_bitexact(ctx):
     """The bench's own configs[2] solve (bench.py bench_ilqr: 4,096 instances x H=100 from
     cfg3_instances(seed=3), rolled out, then mp_ilqr_solve with max_iter 60; ILQR.jl:44-88) vs the

@@ -169,6 +169,6 @@ def test_every_entry_point_has_a_julia_stub():
     # diagnostics and timing hooks are for the Python test/bench harness, not the planner surface
     harness_only = {"mp_math_eval", "mp_ctx_kernel_timing", "mp_ctx_kernel_ms", "mp_ctx_stream", "mp_ctx_trim",
                     "mp_ctx_set_workspace_limit", "mp_ctx_synchronize", "mp_mppi_plan_dev", "mp_ilqr_backward_dev",
-                    "mp_ilqr_forward_dev", "mp_version", "mp_comm_allgather_dev"}
+                    "mp_ilqr_forward_dev", "mp_ilqr_solve_dev", "mp_version", "mp_comm_allgather_dev"}
     missing = sorted(set(protos) - bound - harness_only)
     assert not missing, missing
