@@ -1,6 +1,5 @@
 """Time mp_ha_plan on configs[3] (256 scenarios) a few times: the whole plan_batch call and the library
-call inside it (r.planning_time); with MPGPU_HA_PROFILE=1 the library prints its host pop /
-launch+kernel+copies / bookkeeping split per plan.  --shards: also the one-GPU world-8 projection of
+call inside it (r.planning_time).  --shards: also the one-GPU world-8 projection of
 bench.py (each strided / contiguous shard planned alone, median of 3; a projection, not a multi-GPU run)."""
 import sys
 import time

@@ -1,8 +1,8 @@
 """Plan-kernel time (HIP events, mp_ctx_kernel_ms) of mppi_plan_kernel for a grid of scene counts and
-lane layouts (MPGPU_LPR / MPGPU_BT overrides), configs[1] scenes with device Philox noise and the
-full TrajectoryCollection, as bench.py runs them.
+lane layouts (the MPGPU_LPR test hook), configs[1] scenes with device Philox noise and the full
+TrajectoryCollection, as bench.py runs them.
 
-  python tools/plan_time.py [--scenes 8 16] [--lpr 1 2] [--bt 0] [--reps 20]
+  python tools/plan_time.py [--scenes 8 16] [--lpr 1 2] [--reps 20]
 """
 import argparse
 import ctypes
@@ -20,7 +20,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", type=int, nargs="+", default=[8, 16])
     ap.add_argument("--lpr", type=int, nargs="+", default=[1, 2])
-    ap.add_argument("--bt", type=int, nargs="+", default=[0])
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     from motionplanning_amd import configs
@@ -46,12 +45,8 @@ def main():
             ct=((S, H + 1, 7, K), torch.float64), cc=((S, H, K, 2), torch.float64), ck=((S, K), torch.float64),
             cf=((S, K), torch.uint8)).items()}
         for lpr in a.lpr:
-            for bt in a.bt:
+            if True:
                 os.environ["MPGPU_LPR"] = str(lpr)
-                if bt:
-                    os.environ["MPGPU_BT"] = str(bt)
-                else:
-                    os.environ.pop("MPGPU_BT", None)
                 ms, cnt = ctypes.c_double(), ctypes.c_int32()
                 for i in range(a.reps + 3):
                     p.offset = i
@@ -65,7 +60,7 @@ def main():
                 torch.cuda.synchronize()
                 ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
                 kms = ms.value / max(1, cnt.value)
-                print(f"S={S:3d} LPR={lpr} BT={bt or 'auto':>4}  kernel {kms * 1e3:8.1f} us  "
+                print(f"S={S:3d} LPR={lpr}  kernel {kms * 1e3:8.1f} us  "
                       f"{S * K * H / (kms * 1e-3):.3e} rollout-steps/s", flush=True)
 
 
