@@ -45,23 +45,22 @@ def main():
             ct=((S, H + 1, 7, K), torch.float64), cc=((S, H, K, 2), torch.float64), ck=((S, K), torch.float64),
             cf=((S, K), torch.uint8)).items()}
         for lpr in a.lpr:
-            if True:
-                os.environ["MPGPU_LPR"] = str(lpr)
-                ms, cnt = ctypes.c_double(), ctypes.c_int32()
-                for i in range(a.reps + 3):
-                    p.offset = i
-                    ctx.check(ctx.lib.mp_mppi_plan_dev(ctx.handle, ctypes.byref(p), S, ptr(X0), ptr(goal), ptr(un),
-                                                       None, ptr(grid), None, ptr(o["U"]), ptr(o["traj"]),
-                                                       ptr(o["cost"]), ptr(o["fe"]), ptr(o["rc"]), ptr(o["fc"]),
-                                                       ptr(o["ct"]), ptr(o["cc"]), ptr(o["ck"]), ptr(o["cf"])))
-                    if i == 2:
-                        torch.cuda.synchronize()
-                        ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
-                torch.cuda.synchronize()
-                ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
-                kms = ms.value / max(1, cnt.value)
-                print(f"S={S:3d} LPR={lpr}  kernel {kms * 1e3:8.1f} us  "
-                      f"{S * K * H / (kms * 1e-3):.3e} rollout-steps/s", flush=True)
+            os.environ["MPGPU_LPR"] = str(lpr)
+            ms, cnt = ctypes.c_double(), ctypes.c_int32()
+            for i in range(a.reps + 3):
+                p.offset = i
+                ctx.check(ctx.lib.mp_mppi_plan_dev(ctx.handle, ctypes.byref(p), S, ptr(X0), ptr(goal), ptr(un),
+                                                   None, ptr(grid), None, ptr(o["U"]), ptr(o["traj"]),
+                                                   ptr(o["cost"]), ptr(o["fe"]), ptr(o["rc"]), ptr(o["fc"]),
+                                                   ptr(o["ct"]), ptr(o["cc"]), ptr(o["ck"]), ptr(o["cf"])))
+                if i == 2:
+                    torch.cuda.synchronize()
+                    ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+            torch.cuda.synchronize()
+            ctx.check(ctx.lib.mp_ctx_kernel_ms(ctx.handle, ctypes.byref(ms), ctypes.byref(cnt)))
+            kms = ms.value / max(1, cnt.value)
+            print(f"S={S:3d} LPR={lpr}  kernel {kms * 1e3:8.1f} us  "
+                  f"{S * K * H / (kms * 1e-3):.3e} rollout-steps/s", flush=True)
 
 
 if __name__ == "__main__":
