@@ -736,9 +736,11 @@ __device__ __forceinline__ int wait_ge(const int* p, int v, int* err) {
 // tag: the scene's search ended.  The go word's value: bit 0 go (a node follows), bit 1 skip (the consumer has
 // nothing to do this round: the node's expansion was made speculatively, or no runner-up exists; HA_SPEC).
 constexpr int HA_NGR = 16;
-// granule slots by iteration (it & 3): a slot is rewritten by the bookkeeping three iterations on, which starts
-// only after its consumers have read it (the bookkeeping of the iteration between waited for them)
-constexpr int HA_NGR_SLOTS = 4;
+// granule slots by iteration (it & 7): a slot is rewritten by the bookkeeping seven iterations on -- its consumers
+// (the expansion groups, and one of the scene's two RS_connected blocks) take it as soon as it appears and run at
+// most a couple of iterations behind; a consumer that found its slot overwritten would wait out its bounded spin
+// and fail the plan (Q.err), not read another iteration's node
+constexpr int HA_NGR_SLOTS = 8;
 constexpr unsigned HA_NGR_DONE = 0xffffffffu;
 __device__ __forceinline__ void ha_publish_node(unsigned long long* g, unsigned tag, int lane, const long long* w,
                                                 unsigned go) {
@@ -1706,13 +1708,13 @@ struct HaSearch {
   unsigned long long* ngr;  // [HA_NGR_SLOTS][B][HA_NGR] the popped node as tagged granules (ha_publish_node), by it & 3
   int* nx;               // [B] (ha_pipe_kernel) 2·it + 2 + go once iteration it's bookkeeping has popped the next node
   int* ex;               // [B] (ha_persist_kernel) expansions finished (neighbour groups, cumulative)
-  int* rsr;              // [B] (ha_persist_kernel) 2·it + 2 once RS_connected(n_it) has run
+  int* rsr;              // [2][B] (ha_persist_kernel) 2·it + 2 once RS_connected(n_it) has run, by it & 1 (its RS block)
   int* err;              // [1] (ha_persist_kernel) a bounded wait ran out (the search is then not trusted)
   // (ha_persist_kernel, HA_SPEC) the runner-up: popfirst!'s second-least entry when n_{it+1} is popped, the
   // candidate for n_{it+2}, expanded (and RS_connected) speculatively
   unsigned long long* ngr2;  // [HA_NGR_SLOTS][B][HA_NGR] the runner-up as tagged granules, by it & 3
   int* exs;              // [B] speculative expansions finished (neighbour groups, cumulative)
-  int* rsrs;             // [B] 2·it + 2 once RS_connected(r_it) has run
+  int* rsrs;             // [2][B] 2·it + 2 once RS_connected(r_it) has run, by it & 1
   int* nhit;             // [2][B] (diagnostics) pops that were the runner-up, runner-ups published
 };
 // prescan record: [0] iteration tag, [1] kc = min(K, n_open), then K entries of 13 words: f (bits), seq, position,
@@ -3636,12 +3638,15 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
 #ifndef HA_SPEC
 #define HA_SPEC 1
 #endif
+// blocks per scene of the persistent launch: two RS_connected blocks, the bookkeeping, ng expansion groups
+#define HA_PERSIST_PER(ng) (3 + (ng))
 template <int HWt, int NBGt, bool SPEC = HA_SPEC>
 __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt == HW_TAIL ? HA_WPE_TAIL : 3))) void ha_persist_kernel(
     HaDev P, HaSearch Q, IterArgs A, int B, int it0, double* rs_path2, unsigned char* rs_ok2, int* rs_len2) {
   __shared__ int sh_f;
   __shared__ long long sh_run[12];  // (SPEC, the bookkeeping block) the last runner-up: payload + valid
-  const int np = P.n_prim, ng = (np + NBGt - 1) / NBGt, per = 2 + ng;
+  // per scene: item 0 / 2 RS_connected of the even / odd iterations, item 1 the bookkeeping, items 3.. the groups
+  const int np = P.n_prim, ng = (np + NBGt - 1) / NBGt, per = HA_PERSIST_PER(ng);
   const int slot = blockIdx.x / per, item = blockIdx.x % per;
   const int n_live = A.n_live ? *A.n_live : A.n_active;
   if (slot >= n_live) return;
@@ -3665,7 +3670,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
   auto put = [](unsigned long long* p, int i, unsigned long long v) {
     if (p) __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
-  if (item >= 2) {  // the expansion of n_{it+1} (skipped when it is the runner-up), then (SPEC) of r_{it+1}
+  if (item >= 3) {  // the expansion of n_{it+1} (skipped when it is the runner-up), then (SPEC) of r_{it+1}
     for (int it = it0;; it++) {
       unsigned long long* stp0 = pst(it);  // (stamps: the r job's start / end in slots 6 / 7 of the n job's record)
       for (int job = 0; job < (SPEC ? 2 : 1); job++) {  // (one body for both: a loop, not two inlined copies)
@@ -3684,18 +3689,21 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         X.do_rs = 0;
         unsigned long long* stp = r ? nullptr : pst(it);
         put(stp, 0, now());
-        if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 1)) return;  // the search ended
+        if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 2)) return;  // the search ended
         ha_stores_done();
         __syncthreads();
         if (threadIdx.x == 0) __hip_atomic_fetch_add((r ? Q.exs : Q.ex) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (r) put(stp0, 7, now());
         put(stp, 1, now());
-        put(stp, 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 1) << 32));
+        put(stp, 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 2) << 32));
       }
     }
   }
-  if (item == 0) {  // RS_connected(n_it) (skipped when it is the runner-up), then (SPEC) RS_connected(r_it)
-    for (int it = it0;; it++) {
+  if (item == 0 || item == 2) {  // RS_connected(n_it) (skipped when it is the runner-up), then (SPEC) RS_connected(r_it)
+    // two blocks, iterations of parity par each: RS_connected of the runner-up takes longer than the bookkeeping's
+    // iteration (createActPath + the path sweep), so one block alone set the pace of a lone scene
+    const int par = item == 0 ? 0 : 1;
+    for (int it = it0 + ((par - it0) & 1);; it += 2) {
       unsigned long long* stp0 = pst(it);
       for (int job = 0; job < (SPEC && it > it0 ? 2 : 1); job++) {  // r_it: published by iteration it - 1 too
         const bool r = SPEC && job == 1;
@@ -3721,7 +3729,7 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, 0)) return;
         ha_stores_done();
         __syncthreads();
-        if (threadIdx.x == 0) st_ag((r ? Q.rsrs : Q.rsr) + s, 2 * it + 2);
+        if (threadIdx.x == 0) st_ag((r ? Q.rsrs : Q.rsr) + (size_t)par * B + s, 2 * it + 2);
         if (r) put(stp0, 7, now());
         put(stp, 1, now());
         put(stp, 5, 2ull | ((unsigned long long)s << 4));
@@ -3771,7 +3779,8 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
     if (threadIdx.x == 0) {
       // RS_connected(n_it) done; Q.rsr may already hold iteration it + 1's flag (that RS block starts once this
       // iteration's pop is published), the verdict itself stays in its slot until iteration it + 2 (+ 4: runner-up)
-      const int f = h ? wait_ge(Q.rsrs + s, 2 * (it - 1) + 2, Q.err) : wait_ge(Q.rsr + s, 2 * it + 2, Q.err);
+      const int f = h ? wait_ge(Q.rsrs + (size_t)((it - 1) & 1) * B + s, 2 * (it - 1) + 2, Q.err)
+                      : wait_ge(Q.rsr + (size_t)(it & 1) * B + s, 2 * it + 2, Q.err);
       if (f == HA_DONE) {
         sh_f = 2;
       } else {
@@ -4193,8 +4202,8 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // search state: node arrays and open list indexed [scene][node / cell]
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
-                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 12 + 4 + nB * 24 + nB * HA_NGR_SLOTS * HA_NGR * 8 + 256 * 57 +
-                                           nB * HA_NGR_SLOTS * HA_NGR * 8 + nB * 16 + 256 * 4);
+                                           sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 16 + 4 + nB * 24 + nB * HA_NGR_SLOTS * HA_NGR * 8 + 256 * 57 +
+                                           nB * HA_NGR_SLOTS * HA_NGR * 8 + nB * 20 + 256 * 4);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -4238,13 +4247,13 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.nx = (int*)take(nB * 4);
   Q.ngr = (unsigned long long*)take(nB * HA_NGR_SLOTS * HA_NGR * 8);
   Q.ex = (int*)take(nB * 4);
-  Q.rsr = (int*)take(nB * 4);
+  Q.rsr = (int*)take(nB * 8);
   Q.err = (int*)take(4);
   Q.node_g = (double*)take(nB * 16);
   Q.node_nn = (int*)take(nB * 8);
   Q.ngr2 = (unsigned long long*)take(nB * HA_NGR_SLOTS * HA_NGR * 8);
   Q.exs = (int*)take(nB * 4);
-  Q.rsrs = (int*)take(nB * 4);
+  Q.rsrs = (int*)take(nB * 8);
   Q.nhit = (int*)take(nB * 8);
   IterArgs A{};
   A.goal = mp_upload(ctx, WS_HA0, goal, 3 * nB, &st);
@@ -4323,7 +4332,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   static const bool stamps_on = HA_STAMP_CODE && getenv("MPGPU_HA_STAMPS") && atoi(getenv("MPGPU_HA_STAMPS")) == 1;
   const int stamp_slots = std::min(mp / HA_STAMP_EVERY + 1, 40);  // iterations < 1,000
   A.stamps = nullptr;
-  A.stamp_blocks = B * (2 + (np + NBG_TAIL - 1) / NBG_TAIL);  // + the RSH tail's prescan block
+  A.stamp_blocks = B * HA_PERSIST_PER((np + NBG_TAIL - 1) / NBG_TAIL);  // (the largest per-scene block count)
   if (stamps_on) {
     A.stamps = (unsigned long long*)mp_ws(ctx, WS_HA3, sizeof(unsigned long long) * HA_STAMP_N * (size_t)stamp_slots * A.stamp_blocks);
     if (!A.stamps) return MP_ERR_NOMEM;
@@ -4349,10 +4358,10 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.nx, 0, sizeof(int) * nB, ctx->stream));  // ha_pipe_kernel's pop flags
   MP_HIP(ctx, hipMemsetAsync(Q.ngr, 0, sizeof(unsigned long long) * nB * HA_NGR_SLOTS * HA_NGR, ctx->stream));  // granule tags
   MP_HIP(ctx, hipMemsetAsync(Q.ex, 0, sizeof(int) * nB, ctx->stream));  // ha_persist_kernel's flags
-  MP_HIP(ctx, hipMemsetAsync(Q.rsr, 0, sizeof(int) * nB, ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.rsr, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.ngr2, 0, sizeof(unsigned long long) * nB * HA_NGR_SLOTS * HA_NGR, ctx->stream));  // (HA_SPEC)
   MP_HIP(ctx, hipMemsetAsync(Q.exs, 0, sizeof(int) * nB, ctx->stream));
-  MP_HIP(ctx, hipMemsetAsync(Q.rsrs, 0, sizeof(int) * nB, ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.rsrs, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.nhit, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.err, 0, sizeof(int), ctx->stream));
   hipLaunchKernelGGL(ha_init_kernel, dim3(B), dim3(256), 0, ctx->stream, D, Q, B, dstart);
@@ -4393,7 +4402,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   // (the tail then starts at 28 live scenes).  Measured: a lone scenario 18.7 / 18.9 / 20.4 us per iteration
   // with 12 / 6 / 4 (r05zg, r05zh); the 256-plan 24.0 ms with 6 or 4, 24.7 with 12; a 32-scene shard 16.4 ms with
   // 4 against 18.4-20.1 with 6, whose tail starts only at 28 live scenes, two blocks sharing each CU.
-  const int per_ps = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
+  const int per_ps = HA_PERSIST_PER((np + NBG_TAIL - 1) / NBG_TAIL);
   const void* pfn[3] = {reinterpret_cast<const void*>(ha_persist_kernel<HW_TAIL, NBG_TAIL>),
                         reinterpret_cast<const void*>(ha_persist_kernel<6, NBG_TAIL>),
                         reinterpret_cast<const void*>(ha_persist_kernel<4, NBG_TAIL>)};
@@ -4473,7 +4482,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
     A.node_rw = rs_full ? nullptr : Q.node_rw + (size_t)((it - 1) & 1) * B;
     A.node_tuv = Q.node_tuv + (size_t)((it - 1) & 1) * 3 * B;
     const bool tail = known * per_tail <= tail_blocks;
-    if (tail_pipe && known * (2 + (np + NBG_TAIL - 1) / NBG_TAIL) <= persist_cap) {
+    if (tail_pipe && known * per_ps <= persist_cap) {
       // the rest of the search in one cooperative launch, after the current nodes' expansion (bootstrap)
       const int per_pipe = 2 + (np + NBG_TAIL - 1) / NBG_TAIL;
       if (piped != 2) {
@@ -4490,9 +4499,9 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
       // rocprofv3 runs: the profiler's exit handlers crash in a process that made a cooperative launch)
       static const bool coop_env = !getenv("MPGPU_HA_COOP") || atoi(getenv("MPGPU_HA_COOP")) != 0;
       const hipError_t le =
-          coop_env ? hipLaunchCooperativeKernel(persist_fn, dim3((unsigned)(known * per_pipe)), dim3(64 * phw), args, 0,
+          coop_env ? hipLaunchCooperativeKernel(persist_fn, dim3((unsigned)(known * per_ps)), dim3(64 * phw), args, 0,
                                                 ctx->stream)
-                   : hipLaunchKernel(persist_fn, dim3((unsigned)(known * per_pipe)), dim3(64 * phw), args, 0, ctx->stream);
+                   : hipLaunchKernel(persist_fn, dim3((unsigned)(known * per_ps)), dim3(64 * phw), args, 0, ctx->stream);
       if (le != hipSuccess) {
         // refused (e.g. the device's co-residency changed under this context): the per-iteration pipelined
         // tail from this iteration on -- the bootstrap above already expanded the current nodes
