@@ -3671,6 +3671,10 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
     if (p) __hip_atomic_store(p + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   if (item >= 3) {  // the expansion of n_{it+1} (skipped when it is the runner-up), then (SPEC) of r_{it+1}
+#ifndef HA_GROUP_PRIO
+#define HA_GROUP_PRIO 2
+#endif
+    if (HA_GROUP_PRIO) __builtin_amdgcn_s_setprio(HA_GROUP_PRIO);
     for (int it = it0;; it++) {
       unsigned long long* stp0 = pst(it);  // (stamps: the r job's start / end in slots 6 / 7 of the n job's record)
       for (int job = 0; job < (SPEC ? 2 : 1); job++) {  // (one body for both: a loop, not two inlined copies)
@@ -3744,6 +3748,11 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
 #endif
   constexpr int NTB = 64 * (HWt < HA_BOOK_WAVES ? HWt : HA_BOOK_WAVES);
   if ((int)threadIdx.x >= NTB) return;
+#ifndef HA_BOOK_PRIO
+#define HA_BOOK_PRIO 3
+#endif
+  // the scene's chain: issued first where its CU is shared (other scenes' blocks, many scenes live)
+  if (HA_BOOK_PRIO) __builtin_amdgcn_s_setprio(HA_BOOK_PRIO);
   if (SPEC && threadIdx.x < 12) sh_run[threadIdx.x] = 0;  // no runner-up yet: iteration it0's pop is no hit
   __syncthreads();
   int hit = 0;  // (SPEC) n_it is r_{it-1}: its records and RS_connected are the speculative ones
