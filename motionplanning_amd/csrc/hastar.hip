@@ -1713,7 +1713,7 @@ struct HaSearch {
   // (ha_persist_kernel, HA_SPEC) the runner-up: popfirst!'s second-least entry when n_{it+1} is popped, the
   // candidate for n_{it+2}, expanded (and RS_connected) speculatively
   unsigned long long* ngr2;  // [HA_NGR_SLOTS][B][HA_NGR] the runner-up as tagged granules, by it & 3
-  int* exs;              // [B] speculative expansions finished (neighbour groups, cumulative)
+  int* exs;              // [2][B] speculative expansions finished (neighbour groups, cumulative), by the parity of the runner-up's iteration
   int* rsrs;             // [2][B] 2·it + 2 once RS_connected(r_it) has run, by it & 1
   int* nhit;             // [2][B] (diagnostics) pops that were the runner-up, runner-ups published
 };
@@ -3696,7 +3696,10 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
         if (!ha_iter_body<HWt, NBGt, true>(P, X, stp, slot, item - 2)) return;  // the search ended
         ha_stores_done();
         __syncthreads();
-        if (threadIdx.x == 0) __hip_atomic_fetch_add((r ? Q.exs : Q.ex) + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // (the runner-up rounds count by the parity of the runner-up's iteration, see the bookkeeping's wait)
+        if (threadIdx.x == 0)
+          __hip_atomic_fetch_add(r ? Q.exs + (size_t)((it + 1) & 1) * B + s : Q.ex + s, 1, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
         if (r) put(stp0, 7, now());
         put(stp, 1, now());
         put(stp, 5, ((unsigned long long)s << 4) | ((unsigned long long)(item - 2) << 32));
@@ -3765,7 +3768,11 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
     const auto wait_exp = [&] {
       if (it > it0) {
         if (threadIdx.x == 0) {
-          if (h) wait_ge(Q.exs + s, ng * (it - 1 - it0), Q.err);
+          // r_{it-1}'s expansion: the groups' runner-up rounds of r_{it0+1}, r_{it0+3}, ... of r_{it-1}'s parity.
+          // Counted by parity, not in one sum: r_it is published before this wait, so a fast group can already
+          // have counted its round for r_it while a slow one still expands r_{it-1} (the groups' n rounds
+          // cannot run ahead that way -- n_{it+1} is published after the wait)
+          if (h) wait_ge(Q.exs + (size_t)((it - 1) & 1) * B + s, ng * ((it - 2 - it0) / 2 + 1), Q.err);
           else wait_ge(Q.ex + s, ng * (it - it0), Q.err);
         }
         __syncthreads();
@@ -4212,7 +4219,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   const size_t per_cell = 8 + 24 + 8 + 24 + 8 + 4 + 4 + 8 + 8 + 4 + 8 + 8 + 24 + 4 + 4 + 24 + 24;
   char* ws = (char*)mp_ws(ctx, WS_HA2, nB * C * per_cell + nB * (SI_N * 4 + 32) + nB * mp * 32 + nB * 48 +
                                            sizeof(int) * (mp + 2) + sizeof(int) * 4 * nB + nB * RC_N * 8 + nB * 8 + nB * 48 + nB * PRE_W * 8 + nB * 16 + 4 + nB * 24 + nB * HA_NGR_SLOTS * HA_NGR * 8 + 256 * 57 +
-                                           nB * HA_NGR_SLOTS * HA_NGR * 8 + nB * 20 + 256 * 4);
+                                           nB * HA_NGR_SLOTS * HA_NGR * 8 + nB * 24 + 256 * 4);
   if (!ws) return MP_ERR_NOMEM;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += (bytes + 255) & ~(size_t)255; return q; };
@@ -4261,7 +4268,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   Q.node_g = (double*)take(nB * 16);
   Q.node_nn = (int*)take(nB * 8);
   Q.ngr2 = (unsigned long long*)take(nB * HA_NGR_SLOTS * HA_NGR * 8);
-  Q.exs = (int*)take(nB * 4);
+  Q.exs = (int*)take(nB * 8);
   Q.rsrs = (int*)take(nB * 8);
   Q.nhit = (int*)take(nB * 8);
   IterArgs A{};
@@ -4369,7 +4376,7 @@ int mp_ha_plan(mp_ctx* ctx, const mp_ha_params* p, int32_t B, const double* star
   MP_HIP(ctx, hipMemsetAsync(Q.ex, 0, sizeof(int) * nB, ctx->stream));  // ha_persist_kernel's flags
   MP_HIP(ctx, hipMemsetAsync(Q.rsr, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.ngr2, 0, sizeof(unsigned long long) * nB * HA_NGR_SLOTS * HA_NGR, ctx->stream));  // (HA_SPEC)
-  MP_HIP(ctx, hipMemsetAsync(Q.exs, 0, sizeof(int) * nB, ctx->stream));
+  MP_HIP(ctx, hipMemsetAsync(Q.exs, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.rsrs, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.nhit, 0, sizeof(int) * 2 * nB, ctx->stream));
   MP_HIP(ctx, hipMemsetAsync(Q.err, 0, sizeof(int), ctx->stream));
