@@ -2903,6 +2903,11 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
   __shared__ int r_p[NT / 64];
   __shared__ long long r_pay[NT / 64][11];  // each wave winner's payload: id, g, ix, st[3], rw, tuv[3]
   __shared__ long long s_win[12];           // the pop's winner: payload as r_pay, position, (SPEC) hit
+  // (SPEC) the runner-up: each wave's candidate and its payload (staged by the candidate's owner thread)
+  __shared__ double u_f[SPEC ? NT / 64 : 1];
+  __shared__ long long u_s[SPEC ? NT / 64 : 1];
+  __shared__ int u_p[SPEC ? NT / 64 : 1];
+  __shared__ long long u_pay[SPEC ? NT / 64 : 1][10];
   static_assert(NT >= 256 && NT / 64 <= 16, "four waves for the duplicate check, the wave winners fit a row");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const size_t base = (size_t)b * Q.C;
@@ -3225,6 +3230,72 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
       if (SPEC) s_win[11] = hit;
     }
     PSTAMP(8);
+  }
+  if (SPEC) {
+    // ---- the runner-up: the least of the same candidates without the winner -- each thread's least old entry
+    // (its second when its least won) and, in wave 0, the lanes' changed / appended entries, reduced per wave
+    // here, before FindNewNode's writes; wave 1 takes the least of the waves' beside wave 0's writes, off the
+    // iteration's chain.  The candidate's owner stages its payload: a lane's own entry, the thread's least from
+    // the registers the pop's scan filled, its second from the open list (read before this iteration's writes)
+    __syncthreads();  // the pop's position and go
+    const int wpos = (int)s_win[10];
+    if (s_go) {  // block-uniform
+      double cf = own_f;
+      long long cs = own_s;
+      int cp = own;
+      if (own >= 0 && own == wpos) { cf = bf2; cs = bs2; cp = bp2; }
+      bool cl = false;
+      if (myp >= 0 && myp != wpos && (cp < 0 || key_before(tf, nseq, cf, cs))) { cf = tf; cs = nseq; cp = myp; cl = true; }
+      const int cand = cp;
+      key_min_dpp<0xB1>(cf, cs, cp);
+      key_min_dpp<0x4E>(cf, cs, cp);
+      key_min_dpp<0x141>(cf, cs, cp);
+      key_min_dpp<0x140>(cf, cs, cp);
+      double wf = __longlong_as_double(readlane_l(__double_as_longlong(cf), 0));
+      long long ws = readlane_l(cs, 0);
+      int wp_ = __builtin_amdgcn_readlane(cp, 0);
+#pragma unroll
+      for (int q = 1; q < 4; q++) {
+        const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(cf), 16 * q));
+        const long long os = readlane_l(cs, 16 * q);
+        const int op = __builtin_amdgcn_readlane(cp, 16 * q);
+        if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
+      }
+      if (lane == 0) { u_f[wave] = wf; u_s[wave] = ws; u_p[wave] = wp_; }
+      if (wp_ >= 0 && cand == wp_) {
+        long long* u = u_pay[SPEC ? wave : 0];
+        if (cl) {
+          u[0] = id;
+          u[1] = __double_as_longlong(tg);
+          u[2] = nix;
+          u[3] = __double_as_longlong(nst0);
+          u[4] = __double_as_longlong(nst1);
+          u[5] = __double_as_longlong(nst2);
+          u[6] = nrw;
+          u[7] = __double_as_longlong(nt0);
+          u[8] = __double_as_longlong(nt1);
+          u[9] = __double_as_longlong(nt2);
+        } else if (cand == own) {
+#pragma unroll
+          for (int e = 0; e < 10; e++) u[e] = pay[e];
+        } else {
+          const size_t q = base + cand;
+          u[0] = Q.oid[q];
+          u[1] = __double_as_longlong(Q.og[q]);
+          u[2] = Q.oix[q];
+#pragma unroll
+          for (int e = 0; e < 3; e++) u[3 + e] = __double_as_longlong(Q.ost[q * 3 + e]);
+          u[6] = Q.orw[q];
+#pragma unroll
+          for (int e = 0; e < 3; e++) u[7 + e] = __double_as_longlong(Q.otuv[q * 3 + e]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < 64) {
+    const bool go = s_go;
+    const int wpos = (int)s_win[10];
     // ---- FindNewNode's writes (as ha_book_spec)
     if (chg || app) {
       const size_t q = base + id;
@@ -3309,98 +3380,48 @@ __device__ __forceinline__ BookRec ha_book_pipe(const HaDev& P, const HaSearch& 
         Q.cur_ix[b] = s_win[2];
       }
     }
+  } else if (SPEC && tid < 128 && s_go) {
+    // ---- (wave 1) the runner-up: the least of the waves' candidates, its payload into sr, then its granules
+    double cf = __builtin_inf();
+    long long cs = 0x7fffffffffffffffLL;
+    int cp = -1;
+    if (lane < NT / 64 && u_p[lane] >= 0) { cf = u_f[lane]; cs = u_s[lane]; cp = u_p[lane]; }
+    const int mine = cp;
+    key_min_dpp<0xB1>(cf, cs, cp);
+    key_min_dpp<0x4E>(cf, cs, cp);
+    key_min_dpp<0x141>(cf, cs, cp);
+    key_min_dpp<0x140>(cf, cs, cp);
+    double wf = __longlong_as_double(readlane_l(__double_as_longlong(cf), 0));
+    long long ws = readlane_l(cs, 0);
+    int rpos = __builtin_amdgcn_readlane(cp, 0);
+#pragma unroll
+    for (int q = 1; q < 4; q++) {
+      const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(cf), 16 * q));
+      const long long os = readlane_l(cs, 16 * q);
+      const int op = __builtin_amdgcn_readlane(cp, 16 * q);
+      if (op >= 0 && (rpos < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; rpos = op; }
+    }
+    if (rpos >= 0 && mine == rpos) {  // the owner lane (lane = the candidate's wave)
+#pragma unroll
+      for (int e = 0; e < 10; e++) sr[e] = u_pay[SPEC ? lane : 0][e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the owner's LDS writes before the wave reads them
+    const bool valid = rpos >= 0;
+    long long wv[10];
+#pragma unroll
+    for (int e = 0; e < 10; e++) wv[e] = valid ? sr[e] : 0;
+    // skip (no runner-up): the speculative blocks count the round and wait for the next one
+    ha_publish_node(Q.ngr2 + ((size_t)(it & (HA_NGR_SLOTS - 1)) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv,
+                    valid ? 1u : 3u);
+    if (lane == 0) sr[10] = valid;
   }
   __syncthreads();
   if (SPEC) {
-    // ---- the runner-up: the least of the same candidates without the winner -- each thread's least old entry
-    // (its second when its least won), the waves' minima, then wave 0 with the lanes' changed / appended entries
-    __shared__ double u_f[NT / 64];
-    __shared__ long long u_s[NT / 64];
-    __shared__ int u_p[NT / 64];
-    const int wpos = (int)s_win[10];
-    if (s_go) {  // block-uniform
-      double cf = own_f;
-      long long cs = own_s;
-      int cp = own;
-      if (own >= 0 && own == wpos) { cf = bf2; cs = bs2; cp = bp2; }
-      key_min_dpp<0xB1>(cf, cs, cp);
-      key_min_dpp<0x4E>(cf, cs, cp);
-      key_min_dpp<0x141>(cf, cs, cp);
-      key_min_dpp<0x140>(cf, cs, cp);
-      double wf = __longlong_as_double(readlane_l(__double_as_longlong(cf), 0));
-      long long ws = readlane_l(cs, 0);
-      int wp_ = __builtin_amdgcn_readlane(cp, 0);
-#pragma unroll
-      for (int q = 1; q < 4; q++) {
-        const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(cf), 16 * q));
-        const long long os = readlane_l(cs, 16 * q);
-        const int op = __builtin_amdgcn_readlane(cp, 16 * q);
-        if (op >= 0 && (wp_ < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; wp_ = op; }
-      }
-      if (lane == 0) { u_f[wave] = wf; u_s[wave] = ws; u_p[wave] = wp_; }
-    }
-    __syncthreads();
-    if (s_go && tid < 64) {
-      double cf = __builtin_inf();
-      long long cs = 0x7fffffffffffffffLL;
-      int cp = -1, src = -1;
-      if (lane < NT / 64 && u_p[lane] >= 0) { cf = u_f[lane]; cs = u_s[lane]; cp = u_p[lane]; src = lane; }
-      if (myp >= 0 && myp != wpos && (cp < 0 || key_before(tf, nseq, cf, cs))) { cf = tf; cs = nseq; cp = myp; src = 64 + lane; }
-      const int mine = cp, msrc = src;
-      key_min_dpp<0xB1>(cf, cs, cp);
-      key_min_dpp<0x4E>(cf, cs, cp);
-      key_min_dpp<0x141>(cf, cs, cp);
-      key_min_dpp<0x140>(cf, cs, cp);
-      double wf = __longlong_as_double(readlane_l(__double_as_longlong(cf), 0));
-      long long ws = readlane_l(cs, 0);
-      int rpos = __builtin_amdgcn_readlane(cp, 0);
-#pragma unroll
-      for (int q = 1; q < 4; q++) {
-        const double of_ = __longlong_as_double(readlane_l(__double_as_longlong(cf), 16 * q));
-        const long long os = readlane_l(cs, 16 * q);
-        const int op = __builtin_amdgcn_readlane(cp, 16 * q);
-        if (op >= 0 && (rpos < 0 || key_before(of_, os, wf, ws))) { wf = of_; ws = os; rpos = op; }
-      }
-      if (rpos >= 0 && mine == rpos) {  // the owner lane: its own values, or the old entry (this block wrote it)
-        if (msrc >= 64) {
-          sr[0] = id;
-          sr[1] = __double_as_longlong(tg);
-          sr[2] = nix;
-          sr[3] = __double_as_longlong(nst0);
-          sr[4] = __double_as_longlong(nst1);
-          sr[5] = __double_as_longlong(nst2);
-          sr[6] = nrw;
-          sr[7] = __double_as_longlong(nt0);
-          sr[8] = __double_as_longlong(nt1);
-          sr[9] = __double_as_longlong(nt2);
-        } else {
-          const size_t q = base + rpos;
-          sr[0] = Q.oid[q];
-          sr[1] = __double_as_longlong(Q.og[q]);
-          sr[2] = Q.oix[q];
-#pragma unroll
-          for (int e = 0; e < 3; e++) sr[3 + e] = __double_as_longlong(Q.ost[q * 3 + e]);
-          sr[6] = Q.orw[q];
-#pragma unroll
-          for (int e = 0; e < 3; e++) sr[7 + e] = __double_as_longlong(Q.otuv[q * 3 + e]);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the owner's LDS writes before the wave reads
-      const bool valid = rpos >= 0;
-      long long wv[10];
-#pragma unroll
-      for (int e = 0; e < 10; e++) wv[e] = valid ? sr[e] : 0;
-      // skip (no runner-up): the speculative blocks count the round and wait for the next one
-      ha_publish_node(Q.ngr2 + ((size_t)(it & (HA_NGR_SLOTS - 1)) * B + b) * HA_NGR, (unsigned)it + 1, lane, wv,
-                      valid ? 1u : 3u);
-      if (lane == 0) sr[10] = valid;
-    }
     if (hit_out) *hit_out = s_go ? (int)s_win[11] : 0;
     if (tid == 0 && s_go) {  // (diagnostics: MPGPU_HA_SPEC_STATS=1 prints the sums)
       Q.nhit[b] += (int)s_win[11];
       Q.nhit[B + b] += (int)sr[10];
     }
-    __syncthreads();  // sr and s_win reused by the next iteration
   }
   BookRec br;
   br.v[RC_GO] = s_go;
