@@ -3640,21 +3640,21 @@ __global__ __launch_bounds__(64 * HWt) __attribute__((amdgpu_waves_per_eu(HWt ==
 
 
 // ha_persist_kernel: the pipelined tail as ONE launch for the rest of the search, once every block of it can be
-// resident at once (cooperative launch): per scene an RS_connected block, the bookkeeping block and the expansion
-// groups each loop over the iterations, handing over through per-scene flags instead of launch boundaries --
-// the bookkeeping publishes n_{it+1} (Q.nx, as ha_pipe_kernel), the groups expand it into E[(it+1) & 1] and
-// count themselves in (Q.ex), RS_connected(n_it) signals its verdict (Q.rsr; verdict and path in the iteration's
-// parity buffer); the bookkeeping of iteration it waits for E[it & 1] and RS_connected(n_it) and finishes the
+// resident at once (cooperative launch): per scene two RS_connected blocks (even / odd iterations), the
+// bookkeeping block and the expansion groups each loop over the iterations, handing over through per-scene flags
+// instead of launch boundaries -- the bookkeeping publishes n_{it+1} (tagged granules), the groups expand it into
+// E[(it+1) & 1] and count themselves in (Q.ex), RS_connected(n_it) signals its verdict (Q.rsr by it & 1; verdict and
+// path in the iteration's parity buffer); the bookkeeping of iteration it waits for E[it & 1] and RS_connected(n_it) and finishes the
 // iteration as ha_step_kernel's finisher.  A finished scene publishes HA_DONE: every block of it leaves its loop.
 // Same operations on the same values as ha_pipe_kernel: the same search, bit for bit.  Every wait is bounded.
 // HA_SPEC (default 1): the speculative runner-up (ha_book_pipe<..., SPEC>).  The bookkeeping of iteration it also
 // publishes r_{it+1}, the second-least of popfirst!'s candidates (Q.ngr2): the next pop is r_{it+1} or one of
 // n_{it+1}'s children (the least of the two), and in configs[3] it is r_{it+1} for 87 % of the pops.  The
-// expansion groups, after n_{it+1}, expand r_{it+1} into E slot 2 + ((it+1) & 3) (Q.exs), the RS block, after
-// RS_connected(n_it), runs RS_connected(r_it) into RS slot 2 + (it & 3) (Q.rsrs).  When the pop IS the runner-up
-// (same node id, state and stored commands: the inputs of both), its granules carry skip, the groups and the RS
-// block skip it and the bookkeeping reads the speculative records instead: the lone chain per iteration is then
-// the bookkeeping (~10 us) instead of expansion + bookkeeping (~18.5 us).  The same records, the same decisions:
+// expansion groups, after n_{it+1}, expand r_{it+1} into E slot 2 + ((it+1) & 3) (Q.exs, by the parity of it+1), the
+// RS block of iteration it, after RS_connected(n_it), runs RS_connected(r_it) into RS slot 2 + (it & 3) (Q.rsrs).
+// When the pop IS the runner-up (same node id, state and stored commands: the inputs of both), its granules carry
+// skip, the groups and the RS block skip it and the bookkeeping reads the speculative records instead: the lone
+// chain per hit iteration is then the bookkeeping (~14 us) instead of expansion + bookkeeping.  The same records, the same decisions:
 // the search is bit for bit the same (the expansion and RS_connected are functions of the node alone).
 #ifndef HA_SPEC
 #define HA_SPEC 1
